@@ -1,0 +1,283 @@
+#!/usr/bin/env python3
+"""Device-resident batched Internet-checksum benchmark (BASELINE.json metric).
+
+One step = one pass of the hot path (IPv4 header checksum + TCP checksum with
+pseudo-header, i.e. ip_cksum + tcp_cksum of subr.h:176-177, for every packet)
+over one batch of synthetic packets already resident in HBM.  The headline
+workload is BASELINE.json configs[2]: 16M x 1500 B packets on each GPU
+(configs[4] = 128M x 1500 B over 8 GPUs, i.e. weak scaling at 16M per GPU).
+The 64 B (configs[1]) and IMIX (configs[3]) batches are timed the same way and
+reported under "extra".
+
+    python bench.py --gpus N --steps K --warmup W
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+Rank 0 prints one JSON line.  The CPU baseline (rank 0, N = 1 only) times the
+reference's own subr.c checksum unit (oracle/_ref, when built) or the oracle
+restatement on a bounded sample of the same workload.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "con-gen_amd"))
+
+HBM_PEAK = 8.0e12          # MI355X HBM3E peak, B/s (MI355X_MICROARCH.md)
+SEED = 0xC0C0              # splitmix64(seed = 0xC0C0 + shard)
+METRIC = "Gpkts/s + GB/s device-resident checksum, 64B & 1500B batches; %HBM peak"
+
+
+def shard_plan(rank, world, n_per_gpu):
+    """Weak scaling, no collective on the data path: rank r owns packets
+    [r*n, (r+1)*n) of the global batch, generated with seed 0xC0C0 + r."""
+    return {"first": rank * n_per_gpu, "n": n_per_gpu, "seed": SEED + rank, "world": world}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--packets", type=int, default=16 << 20, help="packets per GPU")
+    ap.add_argument("--no-extra", action="store_true", help="skip the 64 B / IMIX lines")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--only", choices=["1500", "64", "imix"], default=None,
+                    help="time one workload only (profiling runs)")
+    return ap.parse_args()
+
+
+class Dist:
+    """Barrier and max-over-ranks; a no-op at world size 1."""
+
+    def __init__(self):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.pg = None
+        if self.world > 1:
+            import torch.distributed as dist
+            dist.init_process_group("gloo")
+            self.dist = dist
+
+    def barrier(self):
+        if self.world > 1:
+            self.dist.barrier()
+
+    def max(self, x):
+        if self.world == 1:
+            return x
+        import torch
+        t = torch.tensor([float(x)], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def close(self):
+        if self.world > 1:
+            self.dist.destroy_process_group()
+
+
+def timed(torch, dist, eng, cgck, step, steps, warmup):
+    """W untimed steps, then K steps bracketed by barrier + synchronize on both
+    sides.  Returns (max-over-ranks wall seconds, HIP-event ms per launch on
+    the launch stream)."""
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    e0, e1 = cgck.Event(), cgck.Event()
+    t0 = time.perf_counter()
+    eng.record(e0)
+    for _ in range(steps):
+        step()
+    eng.record(e1)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    dist.barrier()
+    wall = dist.max(t1 - t0)
+    return wall, cgck.Engine.elapsed_ms(e0, e1) / steps
+
+
+def bench_strided(torch, dist, eng, cgck, n, size, plan, steps, warmup):
+    buf = cgck.DeviceBuffer(n * size)
+    out = cgck.DeviceBuffer(4 * n)
+    eng.synth_strided(buf.ptr, n, size, size, plan["seed"])
+    eng.sync()
+
+    def step():
+        eng.strided(buf.ptr, n, size, 0, size, cgck.GEN_BOTH, out.ptr)
+
+    wall, ev_ms = timed(torch, dist, eng, cgck, step, steps, warmup)
+    # spot parity of this very run (first/last packets) against the fixtures' generator
+    o = __import__("numpy").zeros(n, "uint32")
+    out.download(o, stream=eng.stream)
+    eng.sync()
+    buf.free()
+    out.free()
+    return wall, ev_ms, o
+
+
+def bench_imix(torch, dist, eng, cgck, n, plan, steps, warmup):
+    nbytes = cgck.load().cgck_imix_bytes(n)
+    buf = cgck.DeviceBuffer(nbytes)
+    desc = cgck.DeviceBuffer(12 * n)
+    out = cgck.DeviceBuffer(4 * n)
+    eng.synth_imix(buf.ptr, desc.ptr, n, plan["seed"])
+    eng.sync()
+
+    def step():
+        eng.desc(buf.ptr, desc.ptr, n, cgck.GEN_BOTH, out.ptr)
+
+    wall, ev_ms = timed(torch, dist, eng, cgck, step, steps, warmup)
+    buf.free()
+    desc.free()
+    out.free()
+    return wall, ev_ms, nbytes
+
+
+def cpu_baseline(seconds):
+    """The reference's checksum loop on this box's host cores (rank 0, N = 1):
+    in_cksum(ip, 20) + udp_cksum(ip, 1480) per 1500 B packet, dense stride,
+    cache-cold (sample larger than the LLC), one pinned core."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    P = oracle.port()
+    R = oracle.reference()
+    fin, fudp = (R or P).fn_pointers()
+    kind = "reference" if R else "port"
+    n = 262144
+    buf = np.zeros(n * 1500, np.uint8)
+    for k in range(0, n, 4096):   # same synthetic bytes as the device batch
+        m = min(4096, n - k)
+        blk = P.stream_bytes(k * 1500, m * 1500, SEED)
+        buf[k * 1500:(k + m) * 1500] = blk
+    for k in range(n):
+        P.stamp_header(buf, k * 1500, 1500)
+    cpus = sorted(os.sched_getaffinity(0))
+    old = set(cpus)
+    try:
+        os.sched_setaffinity(0, {cpus[len(cpus) // 2]})
+        sec, _ = P.cpu_bench(fin, fudp, buf, n, 1500, 1500, threads=1, reps=1)
+        reps = max(1, int(seconds / max(sec, 1e-3)))
+        sec, _ = P.cpu_bench(fin, fudp, buf, n, 1500, 1500, threads=1, reps=reps)
+    finally:
+        os.sched_setaffinity(0, old)
+    rate = n * reps / sec
+    allc = min(len(cpus), 64)
+    sec_all, _ = P.cpu_bench(fin, fudp, buf, n, 1500, 1500, threads=allc, reps=max(1, reps // 4))
+    rate_all = n * max(1, reps // 4) / sec_all
+    return {
+        "value": rate / 1e9, "unit": "Gpkt/s", "cores": 1, "kind": kind,
+        "sample": f"{n} x 1500 B packets (393 MB, cache-cold), in_cksum(ip,20)+udp_cksum(ip,1480) "
+                  f"each, {reps} passes, {sec:.1f} s on 1 pinned core",
+        "gbps": rate * 1500 / 1e9,
+        "all_cores": {"value": rate_all / 1e9, "cores": allc, "gbps": rate_all * 1500 / 1e9},
+    }
+
+
+def load_traffic():
+    """Per-launch HBM bytes of the dominant kernel from the committed PMC
+    summary (profiles/pmc_latest.json, written by tools/pmc_traffic.py from
+    separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench)."""
+    p = os.path.join(ROOT, "profiles", "pmc_latest.json")
+    try:
+        with open(p) as f:
+            return json.load(f).get("bytes_per_launch_1500")
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    args = parse()
+    import torch   # first: the process then shares torch's HIP runtime
+    dist = Dist()
+    torch.cuda.set_device(dist.local)
+    import cgck
+    import numpy as np
+    eng = cgck.Engine(dist.local)
+    plan = shard_plan(dist.rank, dist.world, args.packets)
+    n = plan["n"]
+    res = {}
+
+    if args.only in (None, "1500"):
+        wall, ev_ms, o = bench_strided(torch, dist, eng, cgck, n, 1500, plan, args.steps, args.warmup)
+        res["1500"] = (wall, ev_ms)
+        # parity spot check of the timed run's output (first packets vs the referee)
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle
+        bad, chk = oracle.port().check_synth_strided(min(n, 65536), 1500, 1500, plan["seed"],
+                                                     cgck.GEN_BOTH, o, 16)
+        res["parity_1500"] = {"checked": chk, "mismatches": bad}
+    if not args.no_extra and args.only in (None, "64"):
+        wall, ev_ms, _ = bench_strided(torch, dist, eng, cgck, n, 64, plan, args.steps, args.warmup)
+        res["64"] = (wall, ev_ms)
+    if not args.no_extra and args.only in (None, "imix"):
+        wall, ev_ms, nbytes = bench_imix(torch, dist, eng, cgck, n, plan, args.steps, args.warmup)
+        res["imix"] = (wall, ev_ms, nbytes)
+
+    cpu = None
+    if dist.rank == 0 and dist.world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(args.cpu_seconds)
+    dist.barrier()
+
+    if dist.rank == 0:
+        W = dist.world
+        K = args.steps
+
+        def line(size, wall, ev_ms, extra_bytes=0):
+            pkts = n * W * K
+            gpkt = pkts / wall / 1e9
+            algo = n * (size + 4) + extra_bytes       # bytes per launch per GPU
+            ach = algo / (ev_ms * 1e-3)
+            return {"gpkt_s": gpkt, "gb_s": gpkt * size, "ms_per_step": wall / K * 1e3,
+                    "kernel_ms": ev_ms, "hbm_frac": ach / HBM_PEAK, "achieved_gbs": ach / 1e9}
+
+        out = {"metric": METRIC, "unit": "Gpkt/s", "n_gpus": W, "steps": K, "warmup": args.warmup,
+               "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u16",
+               "data": "synthetic (device-generated splitmix64 IPv4+TCP packets, SURVEY §8(d))"}
+        if "1500" in res:
+            wall, ev_ms = res["1500"]
+            L = line(1500, wall, ev_ms)
+            algo = n * 1504
+            traffic = load_traffic()
+            out.update({
+                "value": L["gpkt_s"], "ms_per_step": L["ms_per_step"],
+                "config": {"workload": f"{n} x 1500 B IPv4+TCP per GPU, dense stride 1500, "
+                                       "ip_cksum + tcp_cksum per packet (BASELINE configs[2]; "
+                                       "configs[4] at 8 GPUs)",
+                           "packets_per_gpu": n, "packet_bytes": 1500, "parallelism": f"batch-split x{W}",
+                           "gb_s": L["gb_s"]},
+                "roofline": {"bound": "hbm", "achieved": L["achieved_gbs"], "peak": HBM_PEAK / 1e9,
+                             "unit": "GB/s", "frac": L["hbm_frac"],
+                             "traffic": traffic,
+                             "kernel": "cksum_kernel<16,6,1,false>",
+                             "algorithmic_bytes_per_launch": algo,
+                             "kernel_ms_hip_events": ev_ms},
+                "parity": res.get("parity_1500"),
+            })
+        extra = {}
+        if "64" in res:
+            extra["64B"] = line(64, *res["64"])
+        if "imix" in res:
+            wall, ev_ms, nbytes = res["imix"]
+            extra["imix"] = line(0, wall, ev_ms, nbytes + 16 * n)
+            extra["imix"]["gb_s"] = nbytes * W * K / wall / 1e9
+        if extra:
+            out["extra"] = extra
+        if "value" not in out:   # --only 64 / imix profiling runs
+            k = "64B" if "64B" in extra else "imix"
+            out["value"] = extra[k]["gpkt_s"]
+            out["config"] = {"workload": k}
+        if cpu:
+            out["cpu_baseline"] = cpu
+        print(json.dumps(out), flush=True)
+    eng.close()
+    dist.close()
+
+
+if __name__ == "__main__":
+    main()

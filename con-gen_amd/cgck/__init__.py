@@ -1,0 +1,309 @@
+"""cgck — Python binding of libcgck.so, the gfx950 Internet-checksum engine.
+
+Mirrors the reference's checksum interface (subr.h:176-177, 373-374):
+
+    in_cksum(buf, off, n)        uint16_t in_cksum(void *, int)
+    udp_cksum(buf, ip_off, n)    uint16_t udp_cksum(struct ip *, int)
+    ip_cksum(buf, ip_off)        #define ip_cksum(ip) in_cksum(ip, ip->ip_hl << 2)
+    tcp_cksum                    #define tcp_cksum udp_cksum
+
+plus the batched C-ABI of include/cgck.h (`Engine`).  Everything here calls
+the HIP kernels through the C-ABI; there is no Python or host arithmetic
+path, and loading fails loudly when the library is missing.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("CGCK_LIB", os.path.join(os.path.dirname(HERE), "libcgck.so"))
+
+# Flags and verdict bits (include/cgck.h).
+RAW = 1 << 0
+IP = 1 << 1
+L4 = 1 << 2
+L4_NOPSEUDO = 1 << 3
+ZERO_FIELDS = 1 << 4
+STORE = 1 << 5
+VERIFY = 1 << 6
+V_IP_ZERO_IS_FFFF = 1 << 7
+V_UDP_ZERO_SKIP = 1 << 8
+GEN_BOTH = IP | L4
+FILL_BOTH = IP | L4 | ZERO_FIELDS | STORE
+VERIFY_BSD = IP | L4 | VERIFY | V_IP_ZERO_IS_FFFF | V_UDP_ZERO_SKIP
+VERIFY_TOY = IP | L4 | VERIFY
+BAD_IP = 1
+BAD_L4 = 2
+BAD_LEN = 4
+
+DESC_DTYPE = np.dtype([("frame_off", "<u8"), ("l3_off", "<u2"), ("ip_len", "<u2")], align=False)
+assert DESC_DTYPE.itemsize == 12
+
+# Every symbol include/cgck.h declares (checked by tests/test_abi.py).
+EXPORTS = (
+    "in_cksum", "udp_cksum", "cgck_last_error", "cgck_abi_version", "cgck_ctx_create",
+    "cgck_ctx_destroy", "cgck_ctx_stream", "cgck_ctx_sync", "cgck_strided", "cgck_desc",
+    "cgck_set_desc_len_hint", "cgck_desc_host", "cgck_host_register", "cgck_host_unregister",
+    "cgck_thread_release", "cgck_tx_begin", "cgck_tx_flush", "cgck_synth_strided",
+    "cgck_synth_imix", "cgck_imix_bytes", "cgck_device_count", "cgck_dev_alloc", "cgck_dev_free",
+    "cgck_host_alloc", "cgck_host_free", "cgck_memcpy", "cgck_memset", "cgck_event_create",
+    "cgck_event_destroy", "cgck_event_record", "cgck_event_elapsed_ms",
+)
+
+
+class CgckError(RuntimeError):
+    pass
+
+
+_lib = None
+_vp = ctypes.c_void_p
+_u64 = ctypes.c_uint64
+_u32 = ctypes.c_uint32
+
+
+def load(path=None):
+    """Load libcgck.so (once).  Raises if it is missing: there is no fallback."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = path or LIB_PATH
+    if not os.path.exists(path):
+        raise CgckError(f"libcgck.so not built at {path} (run make -C con-gen_amd)")
+    L = ctypes.CDLL(path)
+    L.in_cksum.restype = ctypes.c_uint16
+    L.in_cksum.argtypes = [_vp, ctypes.c_int]
+    L.udp_cksum.restype = ctypes.c_uint16
+    L.udp_cksum.argtypes = [_vp, ctypes.c_int]
+    L.cgck_last_error.restype = ctypes.c_char_p
+    L.cgck_abi_version.restype = ctypes.c_int
+    L.cgck_device_count.restype = ctypes.c_int
+    L.cgck_ctx_create.argtypes = [ctypes.c_int, ctypes.POINTER(_vp)]
+    L.cgck_ctx_destroy.argtypes = [_vp]
+    L.cgck_ctx_stream.restype = _vp
+    L.cgck_ctx_stream.argtypes = [_vp]
+    L.cgck_ctx_sync.argtypes = [_vp]
+    L.cgck_set_desc_len_hint.argtypes = [_vp, _u32]
+    L.cgck_strided.argtypes = [_vp, _vp, _u64, _u64, _u32, _u32, _u32, _vp, _vp, _vp, _vp]
+    L.cgck_desc.argtypes = [_vp, _vp, _vp, _u64, _u32, _vp, _vp, _vp, _vp]
+    L.cgck_desc_host.argtypes = [_vp, _vp, ctypes.c_size_t, _vp, _u64, _u32, _vp, _vp]
+    L.cgck_host_register.argtypes = [_vp, ctypes.c_size_t]
+    L.cgck_host_unregister.argtypes = [_vp]
+    L.cgck_synth_strided.argtypes = [_vp, _vp, _u64, _u64, _u32, _u64, _vp]
+    L.cgck_synth_imix.argtypes = [_vp, _vp, _vp, _u64, _u64, _vp]
+    L.cgck_imix_bytes.restype = _u64
+    L.cgck_imix_bytes.argtypes = [_u64]
+    L.cgck_dev_alloc.argtypes = [ctypes.c_size_t, ctypes.POINTER(_vp)]
+    L.cgck_dev_free.argtypes = [_vp]
+    L.cgck_host_alloc.argtypes = [ctypes.c_size_t, ctypes.POINTER(_vp)]
+    L.cgck_host_free.argtypes = [_vp]
+    L.cgck_memcpy.argtypes = [_vp, _vp, ctypes.c_size_t, _vp]
+    L.cgck_memset.argtypes = [_vp, ctypes.c_int, ctypes.c_size_t, _vp]
+    L.cgck_event_create.argtypes = [ctypes.POINTER(_vp)]
+    L.cgck_event_destroy.argtypes = [_vp]
+    L.cgck_event_record.argtypes = [_vp, _vp, _vp]
+    L.cgck_event_elapsed_ms.argtypes = [_vp, _vp, ctypes.POINTER(ctypes.c_float)]
+    _lib = L
+    return L
+
+
+def _check(rc, what):
+    if rc < 0:
+        msg = _lib.cgck_last_error().decode(errors="replace")
+        raise CgckError(f"{what} failed ({rc}): {msg}")
+    return rc
+
+
+def device_count():
+    return load().cgck_device_count()
+
+
+# ---------------------------------------------------------------------------
+# Drop-in interface (reference names and argument meaning).
+# ---------------------------------------------------------------------------
+
+def _addr(buf, off):
+    if not isinstance(buf, np.ndarray) or buf.dtype != np.uint8:
+        raise TypeError("buf must be a numpy uint8 array")
+    return buf.ctypes.data + off
+
+
+def in_cksum(buf, off=0, n=None):
+    """in_cksum(buf + off, n) — subr.c:186-195, on the GPU."""
+    if n is None:
+        n = len(buf) - off
+    return load().in_cksum(_addr(buf, off), n)
+
+
+def udp_cksum(buf, ip_off, n):
+    """udp_cksum((struct ip *)(buf + ip_off), n) — subr.c:212-223, on the GPU."""
+    return load().udp_cksum(_addr(buf, ip_off), n)
+
+
+tcp_cksum = udp_cksum
+
+
+def ip_cksum(buf, ip_off=0):
+    """ip_cksum(ip) = in_cksum(ip, ip->ip_hl << 2) — subr.h:176."""
+    return in_cksum(buf, ip_off, (int(buf[ip_off]) & 0x0F) << 2)
+
+
+def tx_begin():
+    _check(load().cgck_tx_begin(), "cgck_tx_begin")
+
+
+def tx_flush():
+    return _check(load().cgck_tx_flush(), "cgck_tx_flush")
+
+
+def thread_release():
+    load().cgck_thread_release()
+
+
+# ---------------------------------------------------------------------------
+# Batched engine (device memory owned by the library).
+# ---------------------------------------------------------------------------
+
+class DeviceBuffer:
+    def __init__(self, nbytes):
+        L = load()
+        p = _vp()
+        _check(L.cgck_dev_alloc(nbytes, ctypes.byref(p)), "cgck_dev_alloc")
+        self.ptr = p.value
+        self.nbytes = nbytes
+
+    def free(self):
+        if self.ptr:
+            load().cgck_dev_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+    def upload(self, arr, off=0, stream=None):
+        arr = np.ascontiguousarray(arr)
+        assert off + arr.nbytes <= self.nbytes
+        _check(load().cgck_memcpy(self.ptr + off, arr.ctypes.data, arr.nbytes, stream), "upload")
+
+    def download(self, arr, off=0, stream=None):
+        assert arr.flags.c_contiguous and off + arr.nbytes <= self.nbytes
+        _check(load().cgck_memcpy(arr.ctypes.data, self.ptr + off, arr.nbytes, stream), "download")
+
+
+class Event:
+    def __init__(self):
+        p = _vp()
+        _check(load().cgck_event_create(ctypes.byref(p)), "cgck_event_create")
+        self.ptr = p.value
+
+    def __del__(self):
+        try:
+            load().cgck_event_destroy(self.ptr)
+        except Exception:
+            pass
+
+
+class Engine:
+    """One context (stream + staging) on one device — use one per thread."""
+
+    def __init__(self, device=0):
+        L = load()
+        p = _vp()
+        _check(L.cgck_ctx_create(device, ctypes.byref(p)), "cgck_ctx_create")
+        self.ctx = p.value
+        self.device = device
+
+    def close(self):
+        if self.ctx:
+            load().cgck_ctx_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def stream(self):
+        return load().cgck_ctx_stream(self.ctx)
+
+    def sync(self):
+        _check(load().cgck_ctx_sync(self.ctx), "cgck_ctx_sync")
+
+    def set_desc_len_hint(self, n):
+        _check(load().cgck_set_desc_len_hint(self.ctx, n), "cgck_set_desc_len_hint")
+
+    def strided(self, base, n, stride, l3_off, ip_len, flags, out=None, verdict=None, bad=None,
+                stream=None):
+        """Device pointers in, asynchronous (cgck_strided)."""
+        _check(load().cgck_strided(self.ctx, base, n, stride, l3_off, ip_len, flags, out, verdict,
+                                   bad, stream), "cgck_strided")
+
+    def desc(self, base, desc, n, flags, out=None, verdict=None, bad=None, stream=None):
+        _check(load().cgck_desc(self.ctx, base, desc, n, flags, out, verdict, bad, stream),
+               "cgck_desc")
+
+    def desc_host(self, base, desc, flags, out=None, verdict=None):
+        """Host-resident batch (numpy): H2D, kernel, D2H.  Synchronous."""
+        n = len(desc)
+        assert desc.dtype == DESC_DTYPE
+        _check(load().cgck_desc_host(self.ctx, base.ctypes.data, base.nbytes, desc.ctypes.data, n,
+                                     flags, None if out is None else out.ctypes.data,
+                                     None if verdict is None else verdict.ctypes.data),
+               "cgck_desc_host")
+
+    def synth_strided(self, base, n, stride, ip_len, seed, stream=None):
+        _check(load().cgck_synth_strided(self.ctx, base, n, stride, ip_len, seed, stream),
+               "cgck_synth_strided")
+
+    def synth_imix(self, base, desc, n, seed, stream=None):
+        _check(load().cgck_synth_imix(self.ctx, base, desc, n, seed, stream), "cgck_synth_imix")
+
+    def record(self, ev, stream=None):
+        _check(load().cgck_event_record(self.ctx, ev.ptr, stream), "cgck_event_record")
+
+    @staticmethod
+    def elapsed_ms(a, b):
+        ms = ctypes.c_float()
+        _check(load().cgck_event_elapsed_ms(a.ptr, b.ptr, ctypes.byref(ms)), "elapsed")
+        return ms.value
+
+    # -- numpy conveniences (tests) --
+    def run_host_strided(self, buf, n, stride, l3_off, ip_len, flags, want_verdict=False):
+        """Copy a host batch to the device, run cgck_strided, copy results (and,
+        with STORE, the bytes) back.  Returns (out, verdict)."""
+        d = DeviceBuffer(max(buf.nbytes, 1))
+        o = DeviceBuffer(4 * max(n, 1))
+        v = DeviceBuffer(max(n, 1))
+        d.upload(buf, stream=self.stream)
+        self.strided(d.ptr, n, stride, l3_off, ip_len, flags, o.ptr, v.ptr, None)
+        out = np.zeros(n, np.uint32)
+        ver = np.zeros(n, np.uint8)
+        o.download(out, stream=self.stream)
+        v.download(ver, stream=self.stream)
+        if flags & STORE:
+            d.download(buf, stream=self.stream)
+        self.sync()
+        return out, ver
+
+    def run_host_desc(self, buf, desc, flags):
+        n = len(desc)
+        d = DeviceBuffer(max(buf.nbytes, 1))
+        dd = DeviceBuffer(max(desc.nbytes, 12))
+        o = DeviceBuffer(4 * max(n, 1))
+        v = DeviceBuffer(max(n, 1))
+        d.upload(buf, stream=self.stream)
+        dd.upload(desc, stream=self.stream)
+        self.desc(d.ptr, dd.ptr, n, flags, o.ptr, v.ptr, None)
+        out = np.zeros(n, np.uint32)
+        ver = np.zeros(n, np.uint8)
+        o.download(out, stream=self.stream)
+        v.download(ver, stream=self.stream)
+        if flags & STORE:
+            d.download(buf, stream=self.stream)
+        self.sync()
+        return out, ver

@@ -1,0 +1,599 @@
+// cgck_api.cpp — host side of libcgck.so: the C-ABI declared in
+// include/cgck.h.  Contexts (stream + staging), the drop-in in_cksum /
+// udp_cksum symbols (subr.h:373-374), device-resident and host-resident
+// batches, the deferred TX fill, synthetic generation and timing.
+//
+// Every checksum this library returns is computed by the gfx950 kernels in
+// cgck_kernels.hip; there is no host arithmetic path.  Without a usable
+// device every entry point fails with -ENODEV (the drop-in symbols print the
+// reason and abort, since their prototype has no error channel).
+#include <hip/hip_runtime.h>
+
+#include <errno.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <vector>
+
+#include "cgck_internal.h"
+
+using namespace cgck;
+
+// --------------------------------------------------------------------------
+// Errors
+// --------------------------------------------------------------------------
+
+static thread_local char t_err[256];
+
+static int set_err(int code, const char *fmt, ...)
+{
+	va_list ap;
+	va_start(ap, fmt);
+	vsnprintf(t_err, sizeof(t_err), fmt, ap);
+	va_end(ap);
+	return code;
+}
+
+#define HIP_TRY(expr)                                                                     \
+	do {                                                                              \
+		hipError_t e_ = (expr);                                                   \
+		if (e_ != hipSuccess)                                                     \
+			return set_err(-EIO, "%s: %s", #expr, hipGetErrorString(e_));     \
+	} while (0)
+
+extern "C" const char *cgck_last_error(void) { return t_err; }
+extern "C" int cgck_abi_version(void) { return CGCK_ABI_VERSION; }
+
+// --------------------------------------------------------------------------
+// Context
+// --------------------------------------------------------------------------
+
+struct cgck_ctx {
+	int device;
+	int num_cus;
+	hipStream_t stream;
+	uint32_t desc_len_hint;
+	// pinned host staging (drop-in calls, deferred TX)
+	uint8_t *h_stage;
+	size_t h_stage_cap;
+	uint32_t *h_out;
+	size_t h_out_cap;
+	// device scratch (host-resident batches)
+	uint8_t *d_bytes;
+	size_t d_bytes_cap;
+	uint8_t *d_aux; // descriptors | out | verdict
+	size_t d_aux_cap;
+};
+
+struct cgck_event {
+	hipEvent_t ev;
+};
+
+static int grow_host(void **p, size_t *cap, size_t need)
+{
+	if (need <= *cap)
+		return 0;
+	size_t n = need < 4096 ? 4096 : need + need / 2;
+	if (*p)
+		(void)hipHostFree(*p);
+	*p = nullptr;
+	*cap = 0;
+	HIP_TRY(hipHostMalloc(p, n, hipHostMallocDefault));
+	*cap = n;
+	return 0;
+}
+
+static int grow_dev(void **p, size_t *cap, size_t need)
+{
+	if (need <= *cap)
+		return 0;
+	size_t n = need < 65536 ? 65536 : need + need / 4;
+	if (*p)
+		(void)hipFree(*p);
+	*p = nullptr;
+	*cap = 0;
+	HIP_TRY(hipMalloc(p, n));
+	*cap = n;
+	return 0;
+}
+
+extern "C" int cgck_device_count(void)
+{
+	int n = 0;
+	if (hipGetDeviceCount(&n) != hipSuccess)
+		return 0;
+	return n;
+}
+
+extern "C" int cgck_ctx_create(int device, cgck_ctx_t **out)
+{
+	if (!out)
+		return set_err(-EINVAL, "cgck_ctx_create: out is NULL");
+	*out = nullptr;
+	int n = cgck_device_count();
+	if (n <= 0)
+		return set_err(-ENODEV, "cgck: no HIP device visible (gfx950 required)");
+	if (device < 0 || device >= n)
+		return set_err(-ENODEV, "cgck: device %d out of range (%d visible)", device, n);
+	HIP_TRY(hipSetDevice(device));
+	hipDeviceProp_t prop;
+	HIP_TRY(hipGetDeviceProperties(&prop, device));
+	if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+		return set_err(-ENODEV, "cgck: device %d is %s, this build targets gfx950", device,
+			       prop.gcnArchName);
+	cgck_ctx *c = (cgck_ctx *)calloc(1, sizeof(*c));
+	if (!c)
+		return set_err(-ENOMEM, "cgck_ctx_create: out of memory");
+	c->device = device;
+	c->num_cus = prop.multiProcessorCount;
+	c->desc_len_hint = 1500;
+	hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+	if (e != hipSuccess) {
+		free(c);
+		return set_err(-EIO, "hipStreamCreate: %s", hipGetErrorString(e));
+	}
+	*out = c;
+	return 0;
+}
+
+extern "C" int cgck_ctx_destroy(cgck_ctx_t *c)
+{
+	if (!c)
+		return 0;
+	(void)hipSetDevice(c->device);
+	(void)hipStreamSynchronize(c->stream);
+	(void)hipStreamDestroy(c->stream);
+	if (c->h_stage)
+		(void)hipHostFree(c->h_stage);
+	if (c->h_out)
+		(void)hipHostFree(c->h_out);
+	if (c->d_bytes)
+		(void)hipFree(c->d_bytes);
+	if (c->d_aux)
+		(void)hipFree(c->d_aux);
+	free(c);
+	return 0;
+}
+
+extern "C" void *cgck_ctx_stream(cgck_ctx_t *c) { return c ? (void *)c->stream : nullptr; }
+
+extern "C" int cgck_ctx_sync(cgck_ctx_t *c)
+{
+	if (!c)
+		return set_err(-EINVAL, "cgck_ctx_sync: NULL context");
+	HIP_TRY(hipStreamSynchronize(c->stream));
+	return 0;
+}
+
+extern "C" int cgck_set_desc_len_hint(cgck_ctx_t *c, uint32_t max_ip_len)
+{
+	if (!c)
+		return set_err(-EINVAL, "cgck_set_desc_len_hint: NULL context");
+	c->desc_len_hint = max_ip_len ? max_ip_len : 1500;
+	return 0;
+}
+
+static inline hipStream_t pick(cgck_ctx *c, void *stream)
+{
+	return stream ? (hipStream_t)stream : c->stream;
+}
+
+// --------------------------------------------------------------------------
+// Device-resident batches
+// --------------------------------------------------------------------------
+
+static int check_flags(uint32_t flags)
+{
+	const uint32_t known = CGCK_RAW | CGCK_IP | CGCK_L4 | CGCK_L4_NOPSEUDO | CGCK_ZERO_FIELDS |
+			       CGCK_STORE | CGCK_VERIFY | CGCK_V_IP_ZERO_IS_FFFF | CGCK_V_UDP_ZERO_SKIP;
+	if (flags & ~known)
+		return set_err(-EINVAL, "cgck: unknown flag bits 0x%x", flags & ~known);
+	if ((flags & CGCK_RAW) && (flags & ~CGCK_RAW))
+		return set_err(-EINVAL, "cgck: CGCK_RAW excludes every other flag");
+	if (!(flags & (CGCK_RAW | CGCK_IP | CGCK_L4)))
+		return set_err(-EINVAL, "cgck: flags select no checksum (RAW, IP or L4)");
+	return 0;
+}
+
+static int run(cgck_ctx *c, const KParams &p, uint32_t max_len, hipStream_t st)
+{
+	HIP_TRY(hipSetDevice(c->device));
+	hipError_t e = launch_cksum(p, max_len, c->num_cus, st);
+	if (e != hipSuccess)
+		return set_err(-EIO, "cksum launch: %s", hipGetErrorString(e));
+	return 0;
+}
+
+extern "C" int cgck_strided(cgck_ctx_t *c, void *base, uint64_t n, uint64_t stride, uint32_t l3_off,
+			    uint32_t ip_len, uint32_t flags, uint32_t *out, uint8_t *verdict,
+			    uint32_t *bad, void *stream)
+{
+	if (!c)
+		return set_err(-EINVAL, "cgck_strided: NULL context");
+	int rc = check_flags(flags);
+	if (rc)
+		return rc;
+	if (n && !base)
+		return set_err(-EINVAL, "cgck_strided: NULL base");
+	if (ip_len > 0x7fffffffu)
+		return set_err(-EINVAL, "cgck_strided: ip_len too large");
+	KParams p = {(const uint8_t *)base, nullptr, n, stride, l3_off, ip_len, flags, out, verdict, bad};
+	return run(c, p, ip_len, pick(c, stream));
+}
+
+extern "C" int cgck_desc(cgck_ctx_t *c, void *base, const cgck_desc_t *desc, uint64_t n, uint32_t flags,
+			 uint32_t *out, uint8_t *verdict, uint32_t *bad, void *stream)
+{
+	if (!c)
+		return set_err(-EINVAL, "cgck_desc: NULL context");
+	int rc = check_flags(flags);
+	if (rc)
+		return rc;
+	if (n && (!base || !desc))
+		return set_err(-EINVAL, "cgck_desc: NULL base or descriptors");
+	if (((uintptr_t)desc & 3) != 0)
+		return set_err(-EINVAL, "cgck_desc: descriptors must be 4-byte aligned");
+	KParams p = {(const uint8_t *)base, desc, n, 0, 0, 0, flags, out, verdict, bad};
+	return run(c, p, c->desc_len_hint, pick(c, stream));
+}
+
+// --------------------------------------------------------------------------
+// Host-resident batch: H2D, kernel, D2H
+// --------------------------------------------------------------------------
+
+extern "C" int cgck_desc_host(cgck_ctx_t *c, void *base, size_t bytes, const cgck_desc_t *desc,
+			      uint64_t n, uint32_t flags, uint32_t *out, uint8_t *verdict)
+{
+	if (!c)
+		return set_err(-EINVAL, "cgck_desc_host: NULL context");
+	int rc = check_flags(flags);
+	if (rc)
+		return rc;
+	if (n == 0)
+		return 0;
+	if (!base || !desc)
+		return set_err(-EINVAL, "cgck_desc_host: NULL base or descriptors");
+	HIP_TRY(hipSetDevice(c->device));
+	const size_t dbytes = 12 * n, obytes = 4 * n, vbytes = n;
+	if ((rc = grow_dev((void **)&c->d_bytes, &c->d_bytes_cap, bytes)))
+		return rc;
+	if ((rc = grow_dev((void **)&c->d_aux, &c->d_aux_cap, dbytes + obytes + vbytes + 64)))
+		return rc;
+	uint8_t *d_desc = c->d_aux;
+	uint32_t *d_out = (uint32_t *)(c->d_aux + ((dbytes + 15) & ~(size_t)15));
+	uint8_t *d_ver = (uint8_t *)(d_out + n);
+	hipStream_t st = c->stream;
+	HIP_TRY(hipMemcpyAsync(c->d_bytes, base, bytes, hipMemcpyHostToDevice, st));
+	HIP_TRY(hipMemcpyAsync(d_desc, desc, dbytes, hipMemcpyHostToDevice, st));
+	KParams p = {c->d_bytes, (const cgck_desc_t *)d_desc, n, 0, 0, 0, flags, d_out, d_ver, nullptr};
+	if ((rc = run(c, p, c->desc_len_hint, st)))
+		return rc;
+	if (out)
+		HIP_TRY(hipMemcpyAsync(out, d_out, obytes, hipMemcpyDeviceToHost, st));
+	if (verdict)
+		HIP_TRY(hipMemcpyAsync(verdict, d_ver, vbytes, hipMemcpyDeviceToHost, st));
+	if (flags & CGCK_STORE)
+		HIP_TRY(hipMemcpyAsync(base, c->d_bytes, bytes, hipMemcpyDeviceToHost, st));
+	HIP_TRY(hipStreamSynchronize(st));
+	return 0;
+}
+
+extern "C" int cgck_host_register(void *ptr, size_t bytes)
+{
+	HIP_TRY(hipHostRegister(ptr, bytes, hipHostRegisterDefault));
+	return 0;
+}
+
+extern "C" int cgck_host_unregister(void *ptr)
+{
+	HIP_TRY(hipHostUnregister(ptr));
+	return 0;
+}
+
+// --------------------------------------------------------------------------
+// Drop-in symbols (subr.h:373-374) and the deferred TX window
+// --------------------------------------------------------------------------
+
+namespace {
+
+struct TxEntry {
+	uint8_t *ip; // IPv4 header in caller (ring) memory
+	uint32_t span; // bytes staged
+	uint16_t hl;
+	int16_t fo; // -1: IP header entry (field ip+10); else L4 field offset after the header
+};
+
+struct ThreadState {
+	cgck_ctx *ctx = nullptr;
+	bool tx_open = false;
+	std::vector<TxEntry> txq;
+};
+
+thread_local ThreadState t_state;
+
+[[noreturn]] void die(const char *what)
+{
+	fprintf(stderr, "libcgck: %s: %s\n", what, t_err);
+	abort();
+}
+
+cgck_ctx *tls_ctx()
+{
+	if (!t_state.ctx) {
+		const char *e = getenv("CGCK_DEVICE");
+		int dev = e ? atoi(e) : 0;
+		if (cgck_ctx_create(dev, &t_state.ctx) != 0)
+			die("no gfx950 context for the drop-in checksum");
+	}
+	return t_state.ctx;
+}
+
+// One region through the kernel: stage `span` bytes from `src` into pinned
+// memory (the kernel reads pinned host memory directly over the fabric),
+// launch, wait, return the u32 result.
+uint32_t one_packet(const void *src, uint32_t span, uint32_t ip_len, uint32_t flags)
+{
+	cgck_ctx *c = tls_ctx();
+	if (grow_host((void **)&c->h_stage, &c->h_stage_cap, span + 16) ||
+	    grow_host((void **)&c->h_out, &c->h_out_cap, 64))
+		die("staging allocation");
+	if (span)
+		memcpy(c->h_stage, src, span);
+	KParams p = {c->h_stage, nullptr, 1, 0, 0, ip_len, flags, c->h_out, nullptr, nullptr};
+	if (run(c, p, ip_len, c->stream) != 0)
+		die("kernel launch");
+	if (hipStreamSynchronize(c->stream) != hipSuccess) {
+		set_err(-EIO, "hipStreamSynchronize failed");
+		die("kernel completion");
+	}
+	return c->h_out[0];
+}
+
+} // namespace
+
+extern "C" uint16_t in_cksum(void *data, int len)
+{
+	if (len < 0) {
+		// The reference's cksum_raw never terminates sensibly on a negative
+		// size (subr.c:164 compares it as size_t); refuse loudly instead.
+		set_err(-EINVAL, "in_cksum: negative length %d", len);
+		die("in_cksum");
+	}
+	const uint8_t *b = (const uint8_t *)data;
+	if (t_state.tx_open && len >= 20 && (b[0] >> 4) == 4 && len == (b[0] & 15) * 4) {
+		t_state.txq.push_back({(uint8_t *)data, (uint32_t)len, (uint16_t)len, -1});
+		return 0;
+	}
+	return (uint16_t)one_packet(data, (uint32_t)len, (uint32_t)len, CGCK_RAW);
+}
+
+extern "C" uint16_t udp_cksum(struct ip *ipp, int len)
+{
+	const uint8_t *ip = (const uint8_t *)ipp;
+	if (len < 0) {
+		set_err(-EINVAL, "udp_cksum: negative length %d", len);
+		die("udp_cksum");
+	}
+	const uint32_t hl = (ip[0] & 15) * 4;
+	const uint32_t ip_len = hl + (uint32_t)len;
+	if (t_state.tx_open && hl >= 20 && ip_len <= 0xffff && (ip[9] == 6 || ip[9] == 17)) {
+		const int fo = ip[9] == 6 ? 16 : 6;
+		if ((uint32_t)len >= (uint32_t)fo + 2) {
+			t_state.txq.push_back({(uint8_t *)ip, ip_len, (uint16_t)hl, (int16_t)fo});
+			return 0;
+		}
+	}
+	// The pseudo-header reads ip+9 and ip+12..19 whatever ip_hl says
+	// (subr.c:205-207), so at least 20 bytes are staged.
+	const uint32_t span = ip_len < 20 ? 20 : ip_len;
+	return (uint16_t)(one_packet(ip, span, ip_len, CGCK_L4 | kFlagNoLenCheck) >> 16);
+}
+
+extern "C" int cgck_thread_release(void)
+{
+	t_state.txq.clear();
+	t_state.tx_open = false;
+	if (t_state.ctx) {
+		cgck_ctx_destroy(t_state.ctx);
+		t_state.ctx = nullptr;
+	}
+	return 0;
+}
+
+extern "C" int cgck_tx_begin(void)
+{
+	if (t_state.tx_open)
+		return set_err(-EBUSY, "cgck_tx_begin: window already open on this thread");
+	t_state.tx_open = true;
+	t_state.txq.clear();
+	return 0;
+}
+
+extern "C" int cgck_tx_flush(void)
+{
+	if (!t_state.tx_open)
+		return set_err(-EINVAL, "cgck_tx_flush: no open window on this thread");
+	t_state.tx_open = false;
+	std::vector<TxEntry> q;
+	q.swap(t_state.txq);
+	const uint64_t n = q.size();
+	if (n == 0)
+		return 0;
+	cgck_ctx *c = tls_ctx();
+	HIP_TRY(hipSetDevice(c->device));
+	// Stage every region 16-byte aligned, descriptors after them.
+	size_t bytes = 0;
+	for (const TxEntry &e : q)
+		bytes += (e.span + 15) & ~(size_t)15;
+	const size_t desc_off = bytes, out_off = (desc_off + 12 * n + 15) & ~(size_t)15;
+	int rc;
+	if ((rc = grow_host((void **)&c->h_stage, &c->h_stage_cap, out_off + 4 * n)))
+		return rc;
+	cgck_desc_t *d = (cgck_desc_t *)(c->h_stage + desc_off);
+	uint32_t *o = (uint32_t *)(c->h_stage + out_off);
+	size_t at = 0;
+	for (uint64_t i = 0; i < n; i++) {
+		memcpy(c->h_stage + at, q[i].ip, q[i].span);
+		d[i].frame_off = at;
+		d[i].l3_off = 0;
+		d[i].ip_len = (uint16_t)q[i].span;
+		at += (q[i].span + 15) & ~(size_t)15;
+	}
+	// Both kinds in one launch: IP entries ask for the header checksum, L4
+	// entries for the segment checksum; both read their fields as zero, as
+	// the reference's callers have just stored them (ip_output.c:61,
+	// tcp_subr.c:75 / gbtcp/tcp.c:426,436).
+	KParams p = {c->h_stage, d, n, 0, 0, 0, CGCK_IP | CGCK_L4 | CGCK_ZERO_FIELDS, o, nullptr, nullptr};
+	if ((rc = run(c, p, 1500, c->stream)))
+		return rc;
+	HIP_TRY(hipStreamSynchronize(c->stream));
+	int written = 0;
+	for (uint64_t i = 0; i < n; i++) {
+		uint16_t v;
+		uint8_t *dst;
+		if (q[i].fo < 0) {
+			v = (uint16_t)o[i];
+			dst = q[i].ip + 10;
+		} else {
+			v = (uint16_t)(o[i] >> 16);
+			dst = q[i].ip + q[i].hl + q[i].fo;
+		}
+		memcpy(dst, &v, 2);
+		written++;
+	}
+	return written;
+}
+
+// --------------------------------------------------------------------------
+// Synthetic batches
+// --------------------------------------------------------------------------
+
+extern "C" uint64_t cgck_imix_bytes(uint64_t n)
+{
+	static const uint16_t cum[13] = {0, 64, 640, 704, 768, 1344, 1408, 2908, 2972, 3548, 3612, 3676, 4252};
+	return (n / 12) * (uint64_t)kImixCycleBytes + cum[n % 12];
+}
+
+extern "C" int cgck_synth_strided(cgck_ctx_t *c, void *base, uint64_t n, uint64_t stride, uint32_t ip_len,
+				  uint64_t seed, void *stream)
+{
+	if (!c || (n && !base))
+		return set_err(-EINVAL, "cgck_synth_strided: bad arguments");
+	if (ip_len < 20 || ip_len > stride)
+		return set_err(-EINVAL, "cgck_synth_strided: need 20 <= ip_len <= stride");
+	if ((uintptr_t)base & 15)
+		return set_err(-EINVAL, "cgck_synth_strided: base must be 16-byte aligned");
+	HIP_TRY(hipSetDevice(c->device));
+	hipStream_t st = pick(c, stream);
+	HIP_TRY(launch_synth_fill((uint8_t *)base, n * stride, seed, c->num_cus, st));
+	HIP_TRY(launch_synth_stamp((uint8_t *)base, n, stride, ip_len, c->num_cus, st));
+	return 0;
+}
+
+extern "C" int cgck_synth_imix(cgck_ctx_t *c, void *base, cgck_desc_t *desc, uint64_t n, uint64_t seed,
+			       void *stream)
+{
+	if (!c || (n && (!base || !desc)))
+		return set_err(-EINVAL, "cgck_synth_imix: bad arguments");
+	if (((uintptr_t)base & 15) || ((uintptr_t)desc & 3))
+		return set_err(-EINVAL, "cgck_synth_imix: misaligned buffers");
+	HIP_TRY(hipSetDevice(c->device));
+	hipStream_t st = pick(c, stream);
+	HIP_TRY(launch_synth_fill((uint8_t *)base, cgck_imix_bytes(n), seed, c->num_cus, st));
+	HIP_TRY(launch_synth_imix((uint8_t *)base, (uint32_t *)desc, n, c->num_cus, st));
+	return 0;
+}
+
+// --------------------------------------------------------------------------
+// Plumbing
+// --------------------------------------------------------------------------
+
+extern "C" int cgck_dev_alloc(size_t bytes, void **ptr)
+{
+	if (!ptr)
+		return set_err(-EINVAL, "cgck_dev_alloc: NULL out");
+	*ptr = nullptr;
+	if (cgck_device_count() <= 0)
+		return set_err(-ENODEV, "cgck: no HIP device visible");
+	HIP_TRY(hipMalloc(ptr, bytes ? bytes : 1));
+	return 0;
+}
+
+extern "C" int cgck_dev_free(void *ptr)
+{
+	if (ptr)
+		HIP_TRY(hipFree(ptr));
+	return 0;
+}
+
+extern "C" int cgck_host_alloc(size_t bytes, void **ptr)
+{
+	if (!ptr)
+		return set_err(-EINVAL, "cgck_host_alloc: NULL out");
+	*ptr = nullptr;
+	HIP_TRY(hipHostMalloc(ptr, bytes ? bytes : 1, hipHostMallocDefault));
+	return 0;
+}
+
+extern "C" int cgck_host_free(void *ptr)
+{
+	if (ptr)
+		HIP_TRY(hipHostFree(ptr));
+	return 0;
+}
+
+extern "C" int cgck_memcpy(void *dst, const void *src, size_t bytes, void *stream)
+{
+	HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, (hipStream_t)stream));
+	return 0;
+}
+
+extern "C" int cgck_memset(void *dst, int value, size_t bytes, void *stream)
+{
+	HIP_TRY(hipMemsetAsync(dst, value, bytes, (hipStream_t)stream));
+	return 0;
+}
+
+extern "C" int cgck_event_create(cgck_event_t **ev)
+{
+	if (!ev)
+		return set_err(-EINVAL, "cgck_event_create: NULL out");
+	cgck_event *e = (cgck_event *)calloc(1, sizeof(*e));
+	if (!e)
+		return set_err(-ENOMEM, "cgck_event_create: out of memory");
+	hipError_t h = hipEventCreate(&e->ev);
+	if (h != hipSuccess) {
+		free(e);
+		return set_err(-EIO, "hipEventCreate: %s", hipGetErrorString(h));
+	}
+	*ev = e;
+	return 0;
+}
+
+extern "C" int cgck_event_destroy(cgck_event_t *ev)
+{
+	if (ev) {
+		(void)hipEventDestroy(ev->ev);
+		free(ev);
+	}
+	return 0;
+}
+
+extern "C" int cgck_event_record(cgck_ctx_t *c, cgck_event_t *ev, void *stream)
+{
+	if (!c || !ev)
+		return set_err(-EINVAL, "cgck_event_record: bad arguments");
+	HIP_TRY(hipEventRecord(ev->ev, pick(c, stream)));
+	return 0;
+}
+
+extern "C" int cgck_event_elapsed_ms(cgck_event_t *a, cgck_event_t *b, float *ms)
+{
+	if (!a || !b || !ms)
+		return set_err(-EINVAL, "cgck_event_elapsed_ms: bad arguments");
+	HIP_TRY(hipEventSynchronize(b->ev));
+	HIP_TRY(hipEventElapsedTime(ms, a->ev, b->ev));
+	return 0;
+}

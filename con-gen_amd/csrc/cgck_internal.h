@@ -1,0 +1,36 @@
+// cgck_internal.h — shared between the kernels and the host C-ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/cgck.h"
+
+namespace cgck {
+
+// Internal flag (never part of the public enum): skip the BAD_LEN rule so the
+// drop-in udp_cksum keeps the pure-function semantics of subr.c:212-223 even
+// for malformed headers.
+constexpr uint32_t kFlagNoLenCheck = 1u << 15;
+
+constexpr uint32_t kImixCycleBytes = 4252; // 7*64 + 4*576 + 1500
+
+struct KParams {
+	const uint8_t *base;
+	const cgck_desc_t *desc; // nullptr: strided batch
+	uint64_t n;
+	uint64_t stride;
+	uint32_t l3_off;
+	uint32_t ip_len;
+	uint32_t flags;
+	uint32_t *out;
+	uint8_t *verdict;
+	uint32_t *bad;
+};
+
+hipError_t launch_cksum(const KParams &p, uint32_t max_len, int num_cus, hipStream_t st);
+hipError_t launch_synth_fill(uint8_t *base, uint64_t nbytes, uint64_t seed, int num_cus, hipStream_t st);
+hipError_t launch_synth_stamp(uint8_t *base, uint64_t n, uint64_t stride, uint32_t len, int num_cus,
+			      hipStream_t st);
+hipError_t launch_synth_imix(uint8_t *base, uint32_t *desc, uint64_t n, int num_cus, hipStream_t st);
+
+} // namespace cgck

@@ -1,0 +1,186 @@
+/*
+ * cgck.h — C-ABI of the MI355X (gfx950) Internet-checksum engine that stands in
+ * for con-gen's checksum unit (reference: kogdenko/con-gen, subr.c:119-223).
+ *
+ * Two layers, one shared library (libcgck.so):
+ *
+ *  1. Drop-in symbols.  `in_cksum` and `udp_cksum` keep the exact prototypes of
+ *     subr.h:373-374 (and therefore the `ip_cksum` / `tcp_cksum` macros of
+ *     subr.h:176-177 keep working unchanged).  They are synchronous: each call
+ *     runs the gfx950 kernel on the calling thread's own context (stream +
+ *     pinned staging) and returns the host-order u16 the call sites store
+ *     verbatim into the header.  Inside a deferred TX window
+ *     (cgck_tx_begin .. cgck_tx_flush) the same symbols queue the packet and
+ *     return 0; the flush fills every queued field in one batched launch
+ *     (the bsd_flush / toy_flush batch point).
+ *
+ *  2. Batched API (`cgck_*`).  Packet batches described either by a fixed
+ *     stride or by 12-byte descriptors, device-resident (all pointers are
+ *     device pointers) or host-resident (pinned staging, H2D + kernel + D2H).
+ *     Every entry point returns 0 or a negative errno and never aborts.
+ *
+ * Semantics (bit-exact with the reference on the same bytes):
+ *   S   = sum of the region's little-endian 16-bit words counted from the
+ *         region's first byte (odd trailing byte = low byte), plus the
+ *         12-byte pseudo-header for L4 (subr.c:119-125, 197-210);
+ *   out = (S mod 65535 == 0) ? 0xFFFF : 0xFFFF - (S mod 65535)
+ *         (reduce(), subr.c:137-156: a folded sum of 0 maps to 0xFFFF).
+ *
+ * No HIP or torch types appear in any signature: streams are `void *`
+ * (a hipStream_t, or NULL for the context's own stream).
+ */
+#ifndef CGCK_H
+#define CGCK_H
+
+#include <stdint.h>
+#include <stddef.h>
+#include <netinet/ip.h> /* struct ip, as subr.h:29 uses it */
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CGCK_ABI_VERSION 1
+
+/* ------------------------------------------------------------------------ */
+/* 1. Drop-in symbols (subr.h:373-374; bodies subr.c:186-195, 212-223).     */
+/* ------------------------------------------------------------------------ */
+
+/* Checksum of [data, data+len).  ip_cksum(ip) == in_cksum(ip, ip->ip_hl<<2)
+ * (subr.h:176).  Callers: ip_output.c:63, ip_input.c:51, ip_icmp.c:77,191,
+ * gbtcp/inet.c:322, gbtcp/tcp.c:374. */
+uint16_t in_cksum(void *data, int len);
+
+/* TCP/UDP checksum: `len` bytes at ip + ip_hl*4 plus the pseudo-header
+ * {ip_src, ip_dst, 0, ip_p, htons(len)}.  tcp_cksum == udp_cksum (subr.h:177).
+ * Callers: tcp_output.c:417, tcp_input.c:78, tcp_subr.c:122,
+ * udp_usrreq.c:89,189, gbtcp/inet.c:145, gbtcp/tcp.c:377. */
+uint16_t udp_cksum(struct ip *ip, int len);
+
+/* ------------------------------------------------------------------------ */
+/* 2. Batched API.                                                           */
+/* ------------------------------------------------------------------------ */
+
+typedef struct cgck_ctx cgck_ctx_t;
+
+/* One packet of a descriptor batch: the IPv4 header sits at
+ * base + frame_off + l3_off; ip_len bytes of datagram follow it
+ * (ip_hl*4 header bytes + the L4 region).  12 bytes, 4-byte aligned. */
+typedef struct cgck_desc {
+	uint64_t frame_off; /* byte offset of the frame from the batch base   */
+	uint16_t l3_off;    /* IPv4 header offset inside the frame (14: Ethernet) */
+	uint16_t ip_len;    /* datagram bytes covered (IPv4 total length)      */
+} __attribute__((packed, aligned(4))) cgck_desc_t;
+
+/* Operation flags. */
+enum {
+	CGCK_RAW         = 1u << 0, /* out.lo = in_cksum(ip, ip_len): whole region, no header semantics */
+	CGCK_IP          = 1u << 1, /* out.lo = ip_cksum(ip) = in_cksum(ip, ip_hl<<2) */
+	CGCK_L4          = 1u << 2, /* out.hi = udp_cksum(ip, ip_len - ip_hl*4) (pseudo-header) */
+	CGCK_L4_NOPSEUDO = 1u << 3, /* with CGCK_L4: out.hi = in_cksum(ip+hl, ip_len-hl) (ICMP, ip_icmp.c:77,191) */
+	CGCK_ZERO_FIELDS = 1u << 4, /* read the checksum fields as zero: ip+10 and the L4 field by ip_p
+	                               (TCP +16, UDP +6, ICMP +2 after the header) — the "field = 0,
+	                               recompute" step every call site performs */
+	CGCK_STORE       = 1u << 5, /* write out.lo to ip+10 and out.hi to the L4 field (TX fill) */
+	CGCK_VERIFY      = 1u << 6, /* compare with the stored fields (implies ZERO_FIELDS), verdict bits */
+	CGCK_V_IP_ZERO_IS_FFFF = 1u << 7, /* bsd44 ip_input.c:46-48: a received ip_sum of 0 counts as 0xFFFF */
+	CGCK_V_UDP_ZERO_SKIP   = 1u << 8, /* udp_usrreq.c:86: uh_sum == 0 means "not checksummed" */
+};
+#define CGCK_GEN_BOTH    (CGCK_IP | CGCK_L4)
+#define CGCK_FILL_BOTH   (CGCK_IP | CGCK_L4 | CGCK_ZERO_FIELDS | CGCK_STORE)
+#define CGCK_VERIFY_BSD  (CGCK_IP | CGCK_L4 | CGCK_VERIFY | CGCK_V_IP_ZERO_IS_FFFF | CGCK_V_UDP_ZERO_SKIP)
+#define CGCK_VERIFY_TOY  (CGCK_IP | CGCK_L4 | CGCK_VERIFY)
+
+/* Verdict bits (one byte per packet). */
+enum {
+	CGCK_BAD_IP  = 1u << 0, /* -> ips_badsum    (netstat.h:40)  */
+	CGCK_BAD_L4  = 1u << 1, /* -> tcps_rcvbadsum / udps_badsum (netstat.h:103,129) */
+	CGCK_BAD_LEN = 1u << 2, /* header modes only: ip_len < 20 or ip_len < ip_hl*4
+	                           (ip_input.c:24-37 drops these before any checksum):
+	                           out = 0, nothing stored, not counted as bad */
+};
+
+/* Error codes are negative errno values; this gives a thread-local message. */
+const char *cgck_last_error(void);
+int cgck_abi_version(void);
+
+/* Contexts: one per calling thread (a HIP stream, pinned staging, scratch).
+ * A context is never shared between threads without external locking. */
+int cgck_ctx_create(int device, cgck_ctx_t **out);
+int cgck_ctx_destroy(cgck_ctx_t *ctx);
+void *cgck_ctx_stream(cgck_ctx_t *ctx);
+int cgck_ctx_sync(cgck_ctx_t *ctx);
+
+/* Device-resident batches.  `out` (u32 per packet: lo16 = IP/RAW result,
+ * hi16 = L4 result), `verdict` (u8 per packet) and `bad` (u32[2] running
+ * counters: [0] += bad IP, [1] += bad L4) are optional (NULL).  `stream`
+ * NULL = the context's stream.  Asynchronous: returns after the launch. */
+int cgck_strided(cgck_ctx_t *ctx, void *base, uint64_t n, uint64_t stride,
+		 uint32_t l3_off, uint32_t ip_len, uint32_t flags,
+		 uint32_t *out, uint8_t *verdict, uint32_t *bad, void *stream);
+int cgck_desc(cgck_ctx_t *ctx, void *base, const cgck_desc_t *desc, uint64_t n,
+	      uint32_t flags, uint32_t *out, uint8_t *verdict, uint32_t *bad,
+	      void *stream);
+
+/* Shape hint for descriptor batches: the longest ip_len the batch may hold
+ * (default 1500).  Longer packets are still handled, just less efficiently. */
+int cgck_set_desc_len_hint(cgck_ctx_t *ctx, uint32_t max_ip_len);
+
+/* Host-resident batch (ring memory): H2D of [base, base+bytes) and of the
+ * descriptors through pinned staging, kernel, D2H of out/verdict (and, with
+ * CGCK_STORE, the filled bytes back into `base`).  Synchronous. */
+int cgck_desc_host(cgck_ctx_t *ctx, void *base, size_t bytes,
+		   const cgck_desc_t *desc, uint64_t n, uint32_t flags,
+		   uint32_t *out, uint8_t *verdict);
+
+/* Zero-copy ring memory: page-lock a transport's
+ * buffer pool (netmap slots, XDP UMEM, DPDK mempool) so H2D copies read it
+ * directly.  Thin wrappers of hipHostRegister / hipHostUnregister. */
+int cgck_host_register(void *ptr, size_t bytes);
+int cgck_host_unregister(void *ptr);
+
+/* The drop-in symbols run on a per-thread context created on first use
+ * (device from $CGCK_DEVICE, default 0).  A worker thread that exits calls
+ * this to release it. */
+int cgck_thread_release(void);
+
+/* Deferred TX fill.  Between begin and flush, the
+ * drop-in in_cksum/udp_cksum calls of THIS thread that target an IPv4
+ * header (len == ip_hl*4) or a TCP/UDP segment return 0 and are queued; the
+ * flush computes them in one launch and writes each result into its field
+ * (ip+10; TCP +16 / UDP +6 after the header).  Returns the number of
+ * fields written, or a negative errno. */
+int cgck_tx_begin(void);
+int cgck_tx_flush(void);
+
+/* Synthetic batches generated on the device.  Byte j of the
+ * stream is byte (j & 7) of splitmix64(seed, j >> 3); each packet then gets
+ * ver/ihl 0x45, tos 0, total length, ip_p = 6 and zeroed IP/TCP checksum
+ * fields.  IMIX: 64/576/1500 at 7:4:1 in a fixed 12-packet cycle, packed
+ * densely, with the descriptors written to `desc`. */
+int cgck_synth_strided(cgck_ctx_t *ctx, void *base, uint64_t n, uint64_t stride,
+		       uint32_t ip_len, uint64_t seed, void *stream);
+int cgck_synth_imix(cgck_ctx_t *ctx, void *base, cgck_desc_t *desc, uint64_t n,
+		    uint64_t seed, void *stream);
+uint64_t cgck_imix_bytes(uint64_t n); /* bytes an n-packet IMIX batch occupies */
+
+/* Plumbing for callers without their own runtime (tests, bench, C users). */
+int cgck_device_count(void);
+int cgck_dev_alloc(size_t bytes, void **ptr);
+int cgck_dev_free(void *ptr);
+int cgck_host_alloc(size_t bytes, void **ptr); /* pinned */
+int cgck_host_free(void *ptr);
+int cgck_memcpy(void *dst, const void *src, size_t bytes, void *stream); /* async, any direction */
+int cgck_memset(void *dst, int value, size_t bytes, void *stream);
+
+/* HIP-event timing on a given stream (NULL = context stream). */
+typedef struct cgck_event cgck_event_t;
+int cgck_event_create(cgck_event_t **ev);
+int cgck_event_destroy(cgck_event_t *ev);
+int cgck_event_record(cgck_ctx_t *ctx, cgck_event_t *ev, void *stream);
+int cgck_event_elapsed_ms(cgck_event_t *start, cgck_event_t *stop, float *ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CGCK_H */

@@ -1,0 +1,194 @@
+"""ctypes loader for the oracle — TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import
+this module.  It exposes two referees:
+
+* ``port()``: the clean C restatement in ``oracle/cksum_oracle.c`` (always
+  built by ``make -C oracle``);
+* ``reference()``: the reference's own checksum unit (subr.c:119-223) built by
+  ``oracle/build_ref.sh`` into ``oracle/_ref/libref_cksum.so`` — ``None`` when
+  that build is absent (no /root/reference at build time).
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PORT_SO = os.path.join(HERE, "liboracle.so")
+REF_SO = os.path.join(HERE, "_ref", "libref_cksum.so")
+
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+_u32p = ctypes.POINTER(ctypes.c_uint32)
+
+
+def _ptr(a, t=_u8p):
+    return a.ctypes.data_as(t)
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+class Port:
+    """The C restatement (oracle/cksum_oracle.c)."""
+
+    def __init__(self, path=PORT_SO):
+        if not os.path.exists(path):
+            build()
+        L = ctypes.CDLL(path)
+        self.lib = L
+        L.oracle_in_cksum.restype = ctypes.c_uint16
+        L.oracle_in_cksum.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.oracle_udp_cksum.restype = ctypes.c_uint16
+        L.oracle_udp_cksum.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        for name in ("oracle_bsd_ip_input_verify", "oracle_toy_ip_verify"):
+            getattr(L, name).restype = ctypes.c_int
+            getattr(L, name).argtypes = [ctypes.c_void_p]
+        for name in ("oracle_bsd_tcp_input_verify", "oracle_bsd_udp_input_verify",
+                     "oracle_toy_tcp_verify"):
+            getattr(L, name).restype = ctypes.c_int
+            getattr(L, name).argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.oracle_ip_output_fill.argtypes = [ctypes.c_void_p]
+        L.oracle_tcp_output_fill.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.oracle_packet.restype = ctypes.c_uint32
+        L.oracle_packet.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, _u32p]
+        L.oracle_batch_strided.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
+                                           ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                           ctypes.c_void_p, ctypes.c_void_p]
+        L.oracle_batch_desc.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                        ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
+        L.oracle_splitmix64.restype = ctypes.c_uint64
+        L.oracle_splitmix64.argtypes = [ctypes.c_uint64, ctypes.c_uint64]
+        L.oracle_stream_bytes.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
+                                          ctypes.c_uint64]
+        L.oracle_stamp_header.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
+        L.oracle_synth_packet.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
+                                          ctypes.c_uint32, ctypes.c_uint64]
+        L.oracle_imix_desc.argtypes = [ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64),
+                                       ctypes.POINTER(ctypes.c_uint16)]
+        L.oracle_cpu_bench.restype = ctypes.c_double
+        L.oracle_cpu_bench.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                       ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
+                                       ctypes.c_int, ctypes.c_int,
+                                       ctypes.POINTER(ctypes.c_uint64)]
+        L.oracle_check_synth_strided.restype = ctypes.c_uint64
+        L.oracle_check_synth_strided.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
+                                                 ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p,
+                                                 ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]
+        L.oracle_check_synth_imix.restype = ctypes.c_uint64
+        L.oracle_check_synth_imix.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
+                                              ctypes.c_void_p, ctypes.c_uint64,
+                                              ctypes.POINTER(ctypes.c_uint64)]
+        L.oracle_fn_in_cksum.restype = ctypes.c_void_p
+        L.oracle_fn_udp_cksum.restype = ctypes.c_void_p
+
+    # -- pure functions (subr.c:186-195, 212-223) --
+    def in_cksum(self, buf, off=0, n=None):
+        """in_cksum(buf+off, n) on a numpy uint8 array."""
+        if n is None:
+            n = len(buf) - off
+        return self.lib.oracle_in_cksum(buf.ctypes.data + off, n)
+
+    def udp_cksum(self, buf, off, n):
+        return self.lib.oracle_udp_cksum(buf.ctypes.data + off, n)
+
+    def fn_pointers(self):
+        return self.lib.oracle_fn_in_cksum(), self.lib.oracle_fn_udp_cksum()
+
+    # -- batch referees (mirror include/cgck.h flags) --
+    def batch_strided(self, base, n, stride, l3_off, ip_len, flags):
+        out = np.zeros(n, np.uint32)
+        ver = np.zeros(n, np.uint8)
+        self.lib.oracle_batch_strided(base.ctypes.data, n, stride, l3_off, ip_len, flags,
+                                      out.ctypes.data, ver.ctypes.data)
+        return out, ver
+
+    def batch_desc(self, base, desc12, n, flags):
+        out = np.zeros(n, np.uint32)
+        ver = np.zeros(n, np.uint8)
+        self.lib.oracle_batch_desc(base.ctypes.data, desc12.ctypes.data, n, flags,
+                                   out.ctypes.data, ver.ctypes.data)
+        return out, ver
+
+    # -- synthetic input --
+    def stream_bytes(self, off, n, seed):
+        out = np.empty(n, np.uint8)
+        self.lib.oracle_stream_bytes(out.ctypes.data, off, n, seed)
+        return out
+
+    def synth_packet(self, k, stride, ip_len, seed):
+        out = np.empty(ip_len, np.uint8)
+        self.lib.oracle_synth_packet(out.ctypes.data, k, stride, ip_len, seed)
+        return out
+
+    def stamp_header(self, buf, off, ip_len):
+        self.lib.oracle_stamp_header(buf.ctypes.data + off, ip_len)
+
+    def imix_desc(self, k):
+        off = ctypes.c_uint64()
+        ln = ctypes.c_uint16()
+        self.lib.oracle_imix_desc(k, ctypes.byref(off), ctypes.byref(ln))
+        return off.value, ln.value
+
+    def check_synth_strided(self, n, stride, ip_len, seed, flags, out, every=1):
+        """(mismatches, packets checked) of device results `out` vs the referee."""
+        chk = ctypes.c_uint64()
+        bad = self.lib.oracle_check_synth_strided(n, stride, ip_len, seed, flags, out.ctypes.data,
+                                                  every, ctypes.byref(chk))
+        return bad, chk.value
+
+    def check_synth_imix(self, n, seed, flags, out, every=1):
+        chk = ctypes.c_uint64()
+        bad = self.lib.oracle_check_synth_imix(n, seed, flags, out.ctypes.data, every,
+                                               ctypes.byref(chk))
+        return bad, chk.value
+
+    def cpu_bench(self, fin, fudp, base, n, stride, ip_len, threads=1, reps=1):
+        sink = ctypes.c_uint64()
+        sec = self.lib.oracle_cpu_bench(fin, fudp, base.ctypes.data, n, stride, ip_len,
+                                        threads, reps, ctypes.byref(sink))
+        return sec, sink.value
+
+
+class Reference:
+    """The reference's own subr.c checksum unit (oracle/_ref, built from /root/reference)."""
+
+    def __init__(self, path=REF_SO):
+        L = ctypes.CDLL(path)
+        self.lib = L
+        L.in_cksum.restype = ctypes.c_uint16
+        L.in_cksum.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.udp_cksum.restype = ctypes.c_uint16
+        L.udp_cksum.argtypes = [ctypes.c_void_p, ctypes.c_int]
+
+    def in_cksum(self, buf, off=0, n=None):
+        if n is None:
+            n = len(buf) - off
+        return self.lib.in_cksum(buf.ctypes.data + off, n)
+
+    def udp_cksum(self, buf, off, n):
+        return self.lib.udp_cksum(buf.ctypes.data + off, n)
+
+    def fn_pointers(self):
+        return (ctypes.cast(self.lib.in_cksum, ctypes.c_void_p).value,
+                ctypes.cast(self.lib.udp_cksum, ctypes.c_void_p).value)
+
+
+_port = None
+
+
+def port():
+    global _port
+    if _port is None:
+        _port = Port()
+    return _port
+
+
+def reference():
+    """The reference build, or None where it was not built (e.g. on the GPU box
+    when /root/reference was absent at build time)."""
+    if not os.path.exists(REF_SO):
+        return None
+    return Reference()

@@ -1,0 +1,399 @@
+"""GPU parity: the gfx950 kernels (through the C-ABI) against the golden
+fixtures made from the reference's own subr.c checksum unit and against the
+oracle referee on the same bytes.  Integer work: every comparison is
+bit-exact.  Run on an MI355X with `pytest -m gpu`."""
+import ctypes
+
+import numpy as np
+import pytest
+
+import cgck
+
+pytestmark = pytest.mark.gpu
+
+SEED = 0xC0C0
+
+
+def hexa(s):
+    return np.frombuffer(bytes.fromhex(s), np.uint8).copy()
+
+
+# ---------------------------------------------------------------------------
+# Drop-in symbols (subr.h:373-374) against the reference-made fixtures
+# ---------------------------------------------------------------------------
+
+def test_dropin_kat(engine, golden_basic):
+    kat = golden_basic["kat_ipv4"]
+    a = hexa(kat["hex"])
+    assert cgck.in_cksum(a, 0, 20) == kat["in_cksum"]
+    assert cgck.ip_cksum(a, 0) == kat["in_cksum"]
+
+
+def test_dropin_zero_classes(engine, golden_basic):
+    for z in golden_basic["zero_class"]["fills"]:
+        a = np.full(max(z["len"], 1), z["fill"], np.uint8)
+        assert cgck.in_cksum(a, 0, z["len"]) == z["in_cksum"], z
+    for c in golden_basic["zero_class"]["crafted"]:
+        a = hexa(c["hex"])
+        assert cgck.in_cksum(a, 0, len(a)) == c["in_cksum"]
+
+
+def test_dropin_length_offset_grid(engine, golden_basic):
+    g = golden_basic["len_off_grid"]
+    buf = hexa(g["buf_hex"])
+    for off in range(16):
+        got = [cgck.in_cksum(buf, off, n) for n in g["lens"]]
+        assert got == g["in_cksum"][off], f"offset {off}"
+
+
+def test_dropin_udp_frames(engine, golden_basic):
+    for f in golden_basic["udp_frames"]:
+        fr = hexa(f["frame_hex"])
+        assert cgck.udp_cksum(fr, 14, f["l4len"]) == f["udp_cksum"]
+        assert cgck.tcp_cksum(fr, 14, f["l4len"]) == f["udp_cksum"]
+
+
+# ---------------------------------------------------------------------------
+# Batched, device-resident synthetic sets against the fixtures
+# ---------------------------------------------------------------------------
+
+@pytest.mark.parametrize("name", ["64", "1500"])
+def test_synth_strided_fixture(engine, golden_synth, name):
+    s = golden_synth["sets"][name]
+    n, stride, ln = len(s["expect"]), s["stride"], s["ip_len"]
+    buf = cgck.DeviceBuffer(n * stride)
+    out = cgck.DeviceBuffer(4 * n)
+    engine.synth_strided(buf.ptr, n, stride, ln, golden_synth["seed"])
+    engine.strided(buf.ptr, n, stride, 0, ln, cgck.GEN_BOTH, out.ptr)
+    host = np.zeros(len(s["raw_hex"]) * stride, np.uint8)
+    o = np.zeros(n, np.uint32)
+    buf.download(host, stream=engine.stream)
+    out.download(o, stream=engine.stream)
+    engine.sync()
+    for k, h in enumerate(s["raw_hex"]):
+        assert host[k * stride:k * stride + ln].tobytes().hex() == h, f"device bytes, packet {k}"
+    exp = np.array(s["expect"], np.uint32)
+    assert np.array_equal(o & 0xFFFF, exp[:, 0])
+    assert np.array_equal(o >> 16, exp[:, 1])
+
+
+def test_synth_imix_fixture(engine, golden_synth):
+    s = golden_synth["sets"]["imix"]
+    n = len(s["expect"])
+    nbytes = cgck.load().cgck_imix_bytes(n)
+    buf = cgck.DeviceBuffer(nbytes)
+    desc = cgck.DeviceBuffer(12 * n)
+    out = cgck.DeviceBuffer(4 * n)
+    engine.synth_imix(buf.ptr, desc.ptr, n, golden_synth["seed"])
+    engine.desc(buf.ptr, desc.ptr, n, cgck.GEN_BOTH, out.ptr)
+    d = np.zeros(n, cgck.DESC_DTYPE)
+    o = np.zeros(n, np.uint32)
+    host = np.zeros(nbytes, np.uint8)
+    desc.download(d, stream=engine.stream)
+    out.download(o, stream=engine.stream)
+    buf.download(host, stream=engine.stream)
+    engine.sync()
+    assert [[int(a), int(b)] for a, b in zip(d["frame_off"], d["ip_len"])] == s["desc"]
+    assert not d["l3_off"].any()
+    for k, h in enumerate(s["raw_hex"]):
+        off, ln = s["desc"][k]
+        assert host[off:off + ln].tobytes().hex() == h
+    exp = np.array(s["expect"], np.uint32)
+    assert np.array_equal(o & 0xFFFF, exp[:, 0])
+    assert np.array_equal(o >> 16, exp[:, 1])
+
+
+# ---------------------------------------------------------------------------
+# Randomised differential tests against the oracle referee, every flag set
+# and every kernel shape (G = 4 / 16 / 64 lanes per packet)
+# ---------------------------------------------------------------------------
+
+FLAG_SETS = [
+    cgck.RAW,
+    cgck.IP,
+    cgck.L4,
+    cgck.GEN_BOTH,
+    cgck.L4 | cgck.L4_NOPSEUDO,
+    cgck.GEN_BOTH | cgck.ZERO_FIELDS,
+    cgck.FILL_BOTH,
+    cgck.IP | cgck.ZERO_FIELDS | cgck.STORE,
+    cgck.VERIFY_BSD,
+    cgck.VERIFY_TOY,
+    cgck.IP | cgck.L4 | cgck.L4_NOPSEUDO | cgck.VERIFY,
+    cgck.VERIFY_BSD | cgck.STORE,
+]
+
+
+def random_batch(rng, n, max_len, odd=True):
+    """Packets at random (also odd) offsets of one host buffer, random ihl,
+    protocols and lengths, some checksum fields 0 / 0xFFFF / correct."""
+    lens = rng.integers(0, max_len + 1, n)
+    lens[rng.random(n) < 0.05] = 0
+    gaps = rng.integers(0, 40, n)
+    if not odd:
+        gaps &= ~1
+        lens &= ~1
+    offs = np.zeros(n, np.int64)
+    at = 32
+    for i in range(n):
+        offs[i] = at
+        at += int(lens[i]) + int(gaps[i]) + 64
+    buf = rng.integers(0, 256, at + 128, dtype=np.uint8)
+    for i in range(n):
+        o, ln = int(offs[i]), int(lens[i])
+        r = rng.random()
+        ihl = 5 if r < 0.7 else int(rng.integers(0, 16))
+        buf[o] = 0x40 | ihl
+        buf[o + 9] = rng.choice([6, 6, 17, 1, int(rng.integers(0, 256))])
+        if rng.random() < 0.2:
+            buf[o + 10:o + 12] = 0
+        if rng.random() < 0.1:
+            buf[o + 10:o + 12] = 0xFF
+        if ln >= 2:
+            buf[o + 2], buf[o + 3] = (ln >> 8) & 0xFF, ln & 0xFF
+    desc = np.zeros(n, cgck.DESC_DTYPE)
+    l3 = rng.integers(0, 20, n)
+    desc["frame_off"] = offs - l3
+    desc["l3_off"] = l3
+    desc["ip_len"] = lens
+    return buf, desc
+
+
+@pytest.mark.parametrize("hint", [64, 256, 1500, 4000])
+@pytest.mark.parametrize("flags", FLAG_SETS)
+def test_fuzz_desc_vs_oracle(engine, port, flags, hint):
+    rng = np.random.default_rng(flags * 131 + hint)
+    max_len = {64: 80, 256: 300, 1500: 1600, 4000: 5000}[hint]
+    n = 700
+    buf, desc = random_batch(rng, n, max_len)
+    ref_buf = buf.copy()
+    exp, ever = port.batch_desc(ref_buf, desc.view(np.uint8), n, flags)
+    engine.set_desc_len_hint(hint)
+    got_buf = buf.copy()
+    out, ver = engine.run_host_desc(got_buf, desc, flags)
+    engine.set_desc_len_hint(1500)
+    bad = np.nonzero((out != exp) | (ver != ever))[0]
+    assert len(bad) == 0, (f"{len(bad)} mismatches, first {bad[:5]}: got {out[bad[:5]]} "
+                           f"{ver[bad[:5]]} want {exp[bad[:5]]} {ever[bad[:5]]} "
+                           f"len {desc['ip_len'][bad[:5]]}")
+    assert np.array_equal(got_buf, ref_buf), "STORE bytes differ"
+
+
+STRIDED = [  # (stride, l3_off, ip_len) — covers every launch shape and alignment
+    (64, 0, 64), (64, 0, 60), (72, 14, 54), (61, 3, 58), (80, 0, 80),
+    (128, 14, 100), (256, 0, 255), (300, 1, 256),
+    (1500, 0, 1500), (1514, 14, 1500), (2048, 14, 1500), (1501, 0, 1501), (1600, 7, 1590),
+    (2048, 14, 2000), (9000, 0, 9000), (4000, 1, 3999),
+]
+
+
+@pytest.mark.parametrize("stride,l3,ln", STRIDED)
+@pytest.mark.parametrize("flags", [cgck.GEN_BOTH, cgck.RAW, cgck.FILL_BOTH, cgck.VERIFY_BSD])
+def test_fuzz_strided_vs_oracle(engine, port, stride, l3, ln, flags):
+    rng = np.random.default_rng(stride * 7 + ln)
+    n = 333
+    buf = rng.integers(0, 256, n * stride + l3 + ln + 64, dtype=np.uint8)
+    for k in range(n):
+        o = k * stride + l3
+        buf[o] = 0x45 if k % 5 else (0x40 | int(rng.integers(5, 16)))
+        buf[o + 9] = (6, 17, 1, 6, 99)[k % 5]
+    ref = buf.copy()
+    exp, ever = port.batch_strided(ref, n, stride, l3, ln, flags)
+    got = buf.copy()
+    out, ver = engine.run_host_strided(got, n, stride, l3, ln, flags)
+    assert np.array_equal(out, exp)
+    assert np.array_equal(ver, ever)
+    assert np.array_equal(got, ref)
+
+
+def test_edges(engine, port):
+    # empty batch
+    engine.strided(0, 0, 64, 0, 64, cgck.GEN_BOTH)
+    engine.sync()
+    # zero-length and maximal regions in one descriptor batch
+    buf = np.random.default_rng(9).integers(0, 256, 70000, dtype=np.uint8)
+    buf[16] = 0x45
+    desc = np.zeros(4, cgck.DESC_DTYPE)
+    desc[0] = (0, 16, 0)
+    desc[1] = (0, 16, 65535)
+    desc[2] = (1, 16, 19)    # too short for a header: BAD_LEN
+    desc[3] = (3, 0, 40000)
+    for flags in (cgck.RAW, cgck.GEN_BOTH, cgck.VERIFY_TOY):
+        exp, ever = port.batch_desc(buf.copy(), desc.view(np.uint8), 4, flags)
+        out, ver = engine.run_host_desc(buf.copy(), desc, flags)
+        assert np.array_equal(out, exp) and np.array_equal(ver, ever), flags
+    assert cgck.in_cksum(buf, 0, 0) == 0xFFFF
+
+
+def test_bad_counters(engine, port, golden_verify):
+    cases = golden_verify["cases"]
+    buf, desc = pack_cases(cases)
+    d = cgck.DeviceBuffer(buf.nbytes)
+    dd = cgck.DeviceBuffer(desc.nbytes)
+    bad = cgck.DeviceBuffer(8)
+    d.upload(buf, stream=engine.stream)
+    dd.upload(desc, stream=engine.stream)
+    cgck.load().cgck_memset(bad.ptr, 0, 8, engine.stream)
+    ver = cgck.DeviceBuffer(len(cases))
+    engine.desc(d.ptr, dd.ptr, len(cases), cgck.VERIFY_BSD, None, ver.ptr, bad.ptr)
+    b = np.zeros(2, np.uint32)
+    v = np.zeros(len(cases), np.uint8)
+    bad.download(b, stream=engine.stream)
+    ver.download(v, stream=engine.stream)
+    engine.sync()
+    assert b[0] == sum(1 - c["bsd_ip"] for c in cases)
+    assert b[1] == sum(1 - c["bsd_l4"] for c in cases)
+    assert b[0] == int(((v & 1) != 0).sum()) and b[1] == int(((v & 2) != 0).sum())
+
+
+def pack_cases(cases, align=1):
+    parts, descs, at = [], [], 0
+    for c in cases:
+        p = hexa(c["hex"])
+        pad = (-at) % align + 3
+        parts.append(np.zeros(pad, np.uint8))
+        at += pad
+        parts.append(p)
+        descs.append((at, 0, len(p)))
+        at += len(p)
+    parts.append(np.zeros(64, np.uint8))
+    desc = np.zeros(len(descs), cgck.DESC_DTYPE)
+    for i, d in enumerate(descs):
+        desc[i] = d
+    return np.concatenate(parts), desc
+
+
+@pytest.mark.parametrize("align", [1, 2, 16])
+def test_verify_fixture_verdicts(engine, golden_verify, align):
+    """RX verify modes reproduce the reference call sites' verdicts:
+    bsd44 ip_input.c:45-58 + tcp_input.c:75-85 / udp_usrreq.c:86-94 and
+    gbtcp/inet.c:319-330 + 142-153."""
+    cases = golden_verify["cases"]
+    buf, desc = pack_cases(cases, align)
+    out, ver = engine.run_host_desc(buf.copy(), desc, cgck.VERIFY_BSD)
+    for c, v in zip(cases, ver):
+        assert (v & 1) == 1 - c["bsd_ip"], c["kind"]
+        assert ((v >> 1) & 1) == 1 - c["bsd_l4"], c["kind"]
+    tcp = [c for c in cases if c["proto"] == 6]
+    buf, desc = pack_cases(tcp, align)
+    out, ver = engine.run_host_desc(buf.copy(), desc, cgck.VERIFY_TOY)
+    for c, v in zip(tcp, ver):
+        assert (v & 1) == 1 - c["toy_ip"] and ((v >> 1) & 1) == 1 - c["toy_l4"], c["kind"]
+
+
+def test_host_resident_batch(engine, port):
+    rng = np.random.default_rng(21)
+    buf, desc = random_batch(rng, 500, 1500)
+    for flags in (cgck.GEN_BOTH, cgck.FILL_BOTH, cgck.VERIFY_BSD):
+        ref = buf.copy()
+        exp, ever = port.batch_desc(ref, desc.view(np.uint8), len(desc), flags)
+        got = buf.copy()
+        out = np.zeros(len(desc), np.uint32)
+        ver = np.zeros(len(desc), np.uint8)
+        engine.desc_host(got, desc, flags, out, ver)
+        assert np.array_equal(out, exp) and np.array_equal(ver, ever) and np.array_equal(got, ref)
+
+
+def test_deferred_tx_fill(engine, port):
+    """Deferred TX window: the stack's own call pattern (tcp_output.c:416-418
+    then ip_output.c:61-64, each storing the return value) inside
+    cgck_tx_begin/flush yields the same bytes as the synchronous reference
+    sequence."""
+    rng = np.random.default_rng(23)
+    ring = np.zeros((256, 2048), np.uint8)   # netmap-like slots, IP at +14
+    want = []
+    for i in range(256):
+        ln = int(rng.integers(40, 523))       # MTU 522 (con-gen.c:741)
+        pkt = rng.integers(0, 256, ln, dtype=np.uint8)
+        pkt[0] = 0x45
+        pkt[9] = 6 if i % 3 else 17
+        ring[i, 14:14 + ln] = pkt
+        ref = pkt.copy()
+        hl = 20
+        fo = 16 if pkt[9] == 6 else 6
+        ref[hl + fo:hl + fo + 2] = 0
+        ref[hl + fo:hl + fo + 2] = np.frombuffer(
+            np.uint16(port.udp_cksum(ref, 0, ln - hl)).tobytes(), np.uint8)
+        ref[10:12] = 0
+        ref[10:12] = np.frombuffer(np.uint16(port.in_cksum(ref, 0, hl)).tobytes(), np.uint8)
+        want.append((ln, ref, fo))
+    cgck.tx_begin()
+    for i, (ln, ref, fo) in enumerate(want):
+        row = ring[i]
+        row[14 + 20 + fo:14 + 20 + fo + 2] = 0                 # tcp_template zeroes th_sum
+        v = cgck.udp_cksum(row, 14, ln - 20)                   # th->th_sum = tcp_cksum(...)
+        row[14 + 20 + fo:14 + 20 + fo + 2] = np.frombuffer(np.uint16(v).tobytes(), np.uint8)
+        row[14 + 10:14 + 12] = 0                                # ip->ip_sum = 0
+        v = cgck.ip_cksum(row, 14)                              # ip->ip_sum = ip_cksum(ip)
+        row[14 + 10:14 + 12] = np.frombuffer(np.uint16(v).tobytes(), np.uint8)
+    assert cgck.tx_flush() == 2 * len(want)
+    for i, (ln, ref, fo) in enumerate(want):
+        assert np.array_equal(ring[i, 14:14 + ln], ref), i
+
+
+# ---------------------------------------------------------------------------
+# Full BASELINE.json sizes: 100 % at 16M x 64 B, 1/64 sample at 16M x 1500 B
+# and IMIX, plus size-independent round trips (fill -> verify -> corrupt).
+# ---------------------------------------------------------------------------
+
+@pytest.mark.slow
+@pytest.mark.parametrize("stride,every", [(64, 1), (1500, 64)])
+def test_full_size_strided(engine, port, stride, every):
+    n = 16 << 20
+    buf = cgck.DeviceBuffer(n * stride)
+    out = cgck.DeviceBuffer(4 * n)
+    engine.synth_strided(buf.ptr, n, stride, stride, SEED)
+    engine.strided(buf.ptr, n, stride, 0, stride, cgck.GEN_BOTH, out.ptr)
+    o = np.zeros(n, np.uint32)
+    out.download(o, stream=engine.stream)
+    engine.sync()
+    bad, chk = port.check_synth_strided(n, stride, stride, SEED, cgck.GEN_BOTH, o, every)
+    assert bad == 0 and chk == (n + every - 1) // every
+    # round trip: fill both fields in place, then every packet verifies clean
+    ver = cgck.DeviceBuffer(n)
+    badc = cgck.DeviceBuffer(8)
+    cgck.load().cgck_memset(badc.ptr, 0, 8, engine.stream)
+    engine.strided(buf.ptr, n, stride, 0, stride, cgck.FILL_BOTH, None)
+    engine.strided(buf.ptr, n, stride, 0, stride, cgck.VERIFY_BSD, out.ptr, ver.ptr, badc.ptr)
+    o2 = np.zeros(n, np.uint32)
+    b = np.zeros(2, np.uint32)
+    out.download(o2, stream=engine.stream)
+    badc.download(b, stream=engine.stream)
+    engine.sync()
+    assert np.array_equal(o2, o), "verify recomputation differs from generation"
+    assert b.tolist() == [0, 0]
+    # corrupt one payload byte in 1000 random packets: exactly those fail L4
+    rng = np.random.default_rng(31)
+    ks = np.unique(rng.integers(0, n, 1000))
+    one = np.array([0x5A], np.uint8)
+    for k in ks:
+        pos = int(k) * stride + int(rng.integers(40, stride))
+        cur = np.zeros(1, np.uint8)
+        cgck.load().cgck_memcpy(cur.ctypes.data, buf.ptr + pos, 1, engine.stream)
+        engine.sync()
+        cur ^= one
+        cgck.load().cgck_memcpy(buf.ptr + pos, cur.ctypes.data, 1, engine.stream)
+    cgck.load().cgck_memset(badc.ptr, 0, 8, engine.stream)
+    engine.strided(buf.ptr, n, stride, 0, stride, cgck.VERIFY_BSD, None, ver.ptr, badc.ptr)
+    v = np.zeros(n, np.uint8)
+    ver.download(v, stream=engine.stream)
+    badc.download(b, stream=engine.stream)
+    engine.sync()
+    assert b.tolist() == [0, len(ks)]
+    assert np.array_equal(np.nonzero(v)[0], ks)
+
+
+@pytest.mark.slow
+def test_full_size_imix(engine, port):
+    n = 16 << 20
+    nbytes = cgck.load().cgck_imix_bytes(n)
+    buf = cgck.DeviceBuffer(nbytes)
+    desc = cgck.DeviceBuffer(12 * n)
+    out = cgck.DeviceBuffer(4 * n)
+    engine.synth_imix(buf.ptr, desc.ptr, n, SEED)
+    engine.desc(buf.ptr, desc.ptr, n, cgck.GEN_BOTH, out.ptr)
+    o = np.zeros(n, np.uint32)
+    out.download(o, stream=engine.stream)
+    engine.sync()
+    bad, chk = port.check_synth_imix(n, SEED, cgck.GEN_BOTH, o, 64)
+    assert bad == 0 and chk == n // 64
