@@ -48,7 +48,7 @@ EXPORTS = (
     "cgck_thread_release", "cgck_tx_begin", "cgck_tx_flush", "cgck_synth_strided",
     "cgck_synth_imix", "cgck_imix_bytes", "cgck_device_count", "cgck_dev_alloc", "cgck_dev_free",
     "cgck_host_alloc", "cgck_host_free", "cgck_memcpy", "cgck_memset", "cgck_event_create",
-    "cgck_event_destroy", "cgck_event_record", "cgck_event_elapsed_ms",
+    "cgck_event_destroy", "cgck_event_record", "cgck_event_elapsed_ms", "cgck_probe_read",
 )
 
 
@@ -103,6 +103,7 @@ def load(path=None):
     L.cgck_event_destroy.argtypes = [_vp]
     L.cgck_event_record.argtypes = [_vp, _vp, _vp]
     L.cgck_event_elapsed_ms.argtypes = [_vp, _vp, ctypes.POINTER(ctypes.c_float)]
+    L.cgck_probe_read.argtypes = [_vp, _vp, _u64, _vp, _vp]
     _lib = L
     return L
 
@@ -262,6 +263,9 @@ class Engine:
 
     def synth_imix(self, base, desc, n, seed, stream=None):
         _check(load().cgck_synth_imix(self.ctx, base, desc, n, seed, stream), "cgck_synth_imix")
+
+    def probe_read(self, src, nbytes, sink, stream=None):
+        _check(load().cgck_probe_read(self.ctx, src, nbytes, sink, stream), "cgck_probe_read")
 
     def record(self, ev, stream=None):
         _check(load().cgck_event_record(self.ctx, ev.ptr, stream), "cgck_event_record")

@@ -55,6 +55,7 @@ struct cgck_ctx {
 	int num_cus;
 	hipStream_t stream;
 	uint32_t desc_len_hint;
+	int family; // kernel family: 0 auto, 1 group, 2 lane-per-packet ($CGCK_KERNEL)
 	// pinned host staging (drop-in calls, deferred TX)
 	uint8_t *h_stage;
 	size_t h_stage_cap;
@@ -129,6 +130,9 @@ extern "C" int cgck_ctx_create(int device, cgck_ctx_t **out)
 	c->device = device;
 	c->num_cus = prop.multiProcessorCount;
 	c->desc_len_hint = 1500;
+	if (const char *kf = getenv("CGCK_KERNEL"))
+		c->family = !strcmp(kf, "group") ? 1 : !strcmp(kf, "lpp") ? 2
+			  : !strncmp(kf, "lpp", 3) ? atoi(kf + 3) : atoi(kf);
 	hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
 	if (e != hipSuccess) {
 		free(c);
@@ -200,7 +204,7 @@ static int check_flags(uint32_t flags)
 static int run(cgck_ctx *c, const KParams &p, uint32_t max_len, hipStream_t st)
 {
 	HIP_TRY(hipSetDevice(c->device));
-	hipError_t e = launch_cksum(p, max_len, c->num_cus, st);
+	hipError_t e = launch_cksum(p, max_len, c->num_cus, c->family, st);
 	if (e != hipSuccess)
 		return set_err(-EIO, "cksum launch: %s", hipGetErrorString(e));
 	return 0;
@@ -219,7 +223,7 @@ extern "C" int cgck_strided(cgck_ctx_t *c, void *base, uint64_t n, uint64_t stri
 		return set_err(-EINVAL, "cgck_strided: NULL base");
 	if (ip_len > 0x7fffffffu)
 		return set_err(-EINVAL, "cgck_strided: ip_len too large");
-	KParams p = {(const uint8_t *)base, nullptr, n, stride, l3_off, ip_len, flags, out, verdict, bad};
+	KParams p = {(const uint8_t *)base, nullptr, n, stride, l3_off, ip_len, flags, out, verdict, bad, 0};
 	return run(c, p, ip_len, pick(c, stream));
 }
 
@@ -235,7 +239,7 @@ extern "C" int cgck_desc(cgck_ctx_t *c, void *base, const cgck_desc_t *desc, uin
 		return set_err(-EINVAL, "cgck_desc: NULL base or descriptors");
 	if (((uintptr_t)desc & 3) != 0)
 		return set_err(-EINVAL, "cgck_desc: descriptors must be 4-byte aligned");
-	KParams p = {(const uint8_t *)base, desc, n, 0, 0, 0, flags, out, verdict, bad};
+	KParams p = {(const uint8_t *)base, desc, n, 0, 0, 0, flags, out, verdict, bad, 0};
 	return run(c, p, c->desc_len_hint, pick(c, stream));
 }
 
@@ -267,7 +271,7 @@ extern "C" int cgck_desc_host(cgck_ctx_t *c, void *base, size_t bytes, const cgc
 	hipStream_t st = c->stream;
 	HIP_TRY(hipMemcpyAsync(c->d_bytes, base, bytes, hipMemcpyHostToDevice, st));
 	HIP_TRY(hipMemcpyAsync(d_desc, desc, dbytes, hipMemcpyHostToDevice, st));
-	KParams p = {c->d_bytes, (const cgck_desc_t *)d_desc, n, 0, 0, 0, flags, d_out, d_ver, nullptr};
+	KParams p = {c->d_bytes, (const cgck_desc_t *)d_desc, n, 0, 0, 0, flags, d_out, d_ver, nullptr, 0};
 	if ((rc = run(c, p, c->desc_len_hint, st)))
 		return rc;
 	if (out)
@@ -341,7 +345,7 @@ uint32_t one_packet(const void *src, uint32_t span, uint32_t ip_len, uint32_t fl
 		die("staging allocation");
 	if (span)
 		memcpy(c->h_stage, src, span);
-	KParams p = {c->h_stage, nullptr, 1, 0, 0, ip_len, flags, c->h_out, nullptr, nullptr};
+	KParams p = {c->h_stage, nullptr, 1, 0, 0, ip_len, flags, c->h_out, nullptr, nullptr, 0};
 	if (run(c, p, ip_len, c->stream) != 0)
 		die("kernel launch");
 	if (hipStreamSynchronize(c->stream) != hipSuccess) {
@@ -445,7 +449,7 @@ extern "C" int cgck_tx_flush(void)
 	// entries for the segment checksum; both read their fields as zero, as
 	// the reference's callers have just stored them (ip_output.c:61,
 	// tcp_subr.c:75 / gbtcp/tcp.c:426,436).
-	KParams p = {c->h_stage, d, n, 0, 0, 0, CGCK_IP | CGCK_L4 | CGCK_ZERO_FIELDS, o, nullptr, nullptr};
+	KParams p = {c->h_stage, d, n, 0, 0, 0, CGCK_IP | CGCK_L4 | CGCK_ZERO_FIELDS, o, nullptr, nullptr, 0};
 	if ((rc = run(c, p, 1500, c->stream)))
 		return rc;
 	HIP_TRY(hipStreamSynchronize(c->stream));
@@ -503,6 +507,15 @@ extern "C" int cgck_synth_imix(cgck_ctx_t *c, void *base, cgck_desc_t *desc, uin
 	hipStream_t st = pick(c, stream);
 	HIP_TRY(launch_synth_fill((uint8_t *)base, cgck_imix_bytes(n), seed, c->num_cus, st));
 	HIP_TRY(launch_synth_imix((uint8_t *)base, (uint32_t *)desc, n, c->num_cus, st));
+	return 0;
+}
+
+extern "C" int cgck_probe_read(cgck_ctx_t *c, const void *src, uint64_t bytes, uint32_t *sink, void *stream)
+{
+	if (!c || !src || !sink || ((uintptr_t)src & 15))
+		return set_err(-EINVAL, "cgck_probe_read: bad arguments");
+	HIP_TRY(hipSetDevice(c->device));
+	HIP_TRY(launch_probe_read(src, bytes, sink, c->num_cus, c->family, pick(c, stream)));
 	return 0;
 }
 

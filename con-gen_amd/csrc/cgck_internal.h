@@ -25,12 +25,25 @@ struct KParams {
 	uint32_t *out;
 	uint8_t *verdict;
 	uint32_t *bad;
+	uint32_t contig; // set by the launcher: contiguous block ranges
 };
 
-hipError_t launch_cksum(const KParams &p, uint32_t max_len, int num_cus, hipStream_t st);
+// Kernel selection flags (see launch_cksum) and the measured defaults.
+constexpr int kNT = 16, kContig = 32, kExplicit = 64;
+constexpr int kDefaultLpp = 5;
+// Measured (tools/sweep.py, profiles/r01): the group kernel streams whole
+// lines per wave-instruction, so nontemporal loads + contiguous block ranges
+// win (1500 B: 5.79 -> 6.18 TB/s); the lane-per-packet kernel re-touches each
+// line from several instructions, so it wants cached loads (NT: -30..-50 %).
+constexpr bool kDefaultGroupNT = true, kDefaultGroupContig = true;
+constexpr bool kDefaultLppNT = false, kDefaultLppContig = false;
+
+hipError_t launch_cksum(const KParams &p, uint32_t max_len, int num_cus, int family, hipStream_t st);
 hipError_t launch_synth_fill(uint8_t *base, uint64_t nbytes, uint64_t seed, int num_cus, hipStream_t st);
 hipError_t launch_synth_stamp(uint8_t *base, uint64_t n, uint64_t stride, uint32_t len, int num_cus,
 			      hipStream_t st);
+hipError_t launch_probe_read(const void *src, uint64_t bytes, uint32_t *sink, int num_cus, int variant,
+			     hipStream_t st);
 hipError_t launch_synth_imix(uint8_t *base, uint32_t *desc, uint64_t n, int num_cus, hipStream_t st);
 
 } // namespace cgck

@@ -180,6 +180,11 @@ int cgck_event_destroy(cgck_event_t *ev);
 int cgck_event_record(cgck_ctx_t *ctx, cgck_event_t *ev, void *stream);
 int cgck_event_elapsed_ms(cgck_event_t *start, cgck_event_t *stop, float *ms);
 
+/* Diagnostics: a plain coalesced streaming read of [src, src+bytes) (device
+ * memory, 16-byte aligned) with minimal arithmetic — the practical HBM-read
+ * ceiling the checksum kernels are compared with.  `sink` is a device u32. */
+int cgck_probe_read(cgck_ctx_t *ctx, const void *src, uint64_t bytes, uint32_t *sink, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,89 @@
+#!/usr/bin/env python3
+"""In-process A/B of kernel families/variants on the BASELINE workloads.
+
+Interleaves R rounds of K launches per (workload, variant) in ONE process on
+ONE device (cdna_hip_programming.md §5.4 rule 24) and prints the median and
+best HBM rate per cell.  Variants are selected through $CGCK_KERNEL at
+context creation (auto | group | lpp).
+
+    python tools/sweep.py [--packets N] [--rounds R] [--launches K]
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "con-gen_amd"))
+import cgck  # noqa: E402
+
+HBM = 8.0e12
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--packets", type=int, default=16 << 20)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--launches", type=int, default=10)
+    ap.add_argument("--variants", default="group,lpp")
+    ap.add_argument("--workloads", default="1500,64,imix")
+    ap.add_argument("--flags", default="GEN_BOTH")
+    args = ap.parse_args()
+    n = args.packets
+    flags = getattr(cgck, args.flags)
+    engines = {}
+    for v in args.variants.split(","):
+        os.environ["CGCK_KERNEL"] = v
+        engines[v] = cgck.Engine(0)
+    os.environ.pop("CGCK_KERNEL", None)
+    e0 = next(iter(engines.values()))
+    work = {}
+    for w in args.workloads.split(","):
+        if w == "imix":
+            nbytes = cgck.load().cgck_imix_bytes(n)
+            buf = cgck.DeviceBuffer(nbytes)
+            desc = cgck.DeviceBuffer(12 * n)
+            e0.synth_imix(buf.ptr, desc.ptr, n, 0xC0C0)
+            algo = nbytes + 16 * n
+            work[w] = (lambda e, buf=buf, desc=desc: e.desc(buf.ptr, desc.ptr, n, flags, out.ptr), algo,
+                       [buf, desc])
+        else:
+            L = int(w)
+            buf = cgck.DeviceBuffer(n * L)
+            e0.synth_strided(buf.ptr, n, L, L, 0xC0C0)
+            work[w] = (lambda e, buf=buf, L=L: e.strided(buf.ptr, n, L, 0, L, flags, out.ptr),
+                       n * (L + 4), [buf])
+    out = cgck.DeviceBuffer(4 * n)
+    # streaming-read ceiling on the 1500 B buffer (or the first one)
+    pb = work.get("1500", next(iter(work.values())))[2][0]
+    sink = cgck.DeviceBuffer(4)
+    work["probe"] = (lambda e, pb=pb: e.probe_read(pb.ptr, pb.nbytes, sink.ptr), pb.nbytes, [pb])
+    e0.sync()
+    res = {(w, v): [] for w in work for v in engines if w != "probe" or v == next(iter(engines))}
+    a, b = cgck.Event(), cgck.Event()
+    for r in range(args.rounds + 1):
+        for w, (fn, algo, _) in work.items():
+            for v, e in engines.items():
+                if (w, v) not in res:
+                    continue
+                fn(e)  # warm
+                e.record(a)
+                for _ in range(args.launches):
+                    fn(e)
+                e.record(b)
+                ms = cgck.Engine.elapsed_ms(a, b) / args.launches
+                if r > 0:
+                    res[(w, v)].append(algo / (ms * 1e-3))
+    table = {}
+    for (w, v), xs in res.items():
+        med, best = statistics.median(xs), max(xs)
+        table[f"{w}/{v}"] = {"median_GBs": med / 1e9, "best_GBs": best / 1e9,
+                             "median_frac": med / HBM}
+        print(f"{w:>5} {v:>6}: median {med / 1e9:8.1f} GB/s ({med / HBM:6.1%})  best {best / 1e9:8.1f}",
+              flush=True)
+    print(json.dumps(table))
+
+
+if __name__ == "__main__":
+    main()
