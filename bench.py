@@ -126,12 +126,14 @@ def bench_imix(torch, dist, eng, cgck, n, plan, steps, warmup):
     desc = cgck.DeviceBuffer(12 * n)
     out = cgck.DeviceBuffer(4 * n)
     eng.synth_imix(buf.ptr, desc.ptr, n, plan["seed"])
+    eng.set_desc_len_hint(nbytes // n)       # mean IMIX length (354 B)
     eng.sync()
 
     def step():
         eng.desc(buf.ptr, desc.ptr, n, cgck.GEN_BOTH, out.ptr)
 
     wall, ev_ms = timed(torch, dist, eng, cgck, step, steps, warmup)
+    eng.set_desc_len_hint(1500)
     buf.free()
     desc.free()
     out.free()

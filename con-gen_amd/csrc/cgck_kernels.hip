@@ -865,6 +865,26 @@ __global__ __launch_bounds__(256) void probe_block_kernel(const uint4 *src, uint
 		sink[0] = acc;
 }
 
+// Lane-strided variant: lane reads CH consecutive uint4 (one "packet" of
+// 16*CH bytes), lanes 16*CH bytes apart — the lane-per-packet access shape.
+template <int CH>
+__global__ __launch_bounds__(256) void probe_lane_kernel(const uint4 *src, uint64_t n16, uint32_t *sink)
+{
+	uint32_t acc = 0;
+	const uint64_t npk = n16 / CH;
+	for (uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x; k < npk; k += (uint64_t)gridDim.x * 256) {
+		uint4 w[CH];
+#pragma unroll
+		for (int j = 0; j < CH; ++j)
+			w[j] = src[k * CH + j];
+#pragma unroll
+		for (int j = 0; j < CH; ++j)
+			acc = sum4(w[j], acc);
+	}
+	if (acc == 0x12345678u)
+		sink[0] = acc;
+}
+
 hipError_t launch_probe_read(const void *src, uint64_t bytes, uint32_t *sink, int num_cus, int variant,
 			     hipStream_t st)
 {
@@ -885,6 +905,15 @@ hipError_t launch_probe_read(const void *src, uint64_t bytes, uint32_t *sink, in
 		break;
 	case 5:
 		hipLaunchKernelGGL((probe_read_kernel<8, false>), dim3(num_cus * 32), dim3(256), 0, st, s, n, sink);
+		break;
+	case 6:
+		hipLaunchKernelGGL((probe_lane_kernel<4>), dim3(num_cus * 8), dim3(256), 0, st, s, n, sink);
+		break;
+	case 7:
+		hipLaunchKernelGGL((probe_lane_kernel<8>), dim3(num_cus * 8), dim3(256), 0, st, s, n, sink);
+		break;
+	case 8:
+		hipLaunchKernelGGL((probe_lane_kernel<2>), dim3(num_cus * 8), dim3(256), 0, st, s, n, sink);
 		break;
 	default:
 		hipLaunchKernelGGL((probe_read_kernel<8, false>), dim3(num_cus * 8), dim3(256), 0, st, s, n, sink);

@@ -122,8 +122,10 @@ int cgck_desc(cgck_ctx_t *ctx, void *base, const cgck_desc_t *desc, uint64_t n,
 	      uint32_t flags, uint32_t *out, uint8_t *verdict, uint32_t *bad,
 	      void *stream);
 
-/* Shape hint for descriptor batches: the longest ip_len the batch may hold
- * (default 1500).  Longer packets are still handled, just less efficiently. */
+/* Shape hint for descriptor batches: their typical (mean) ip_len, default
+ * 1500.  Below 1 KiB the lane-per-packet kernel is used (mixed/small packets,
+ * e.g. IMIX = 354), from 1 KiB the lane-group kernel.  Any length is still
+ * handled correctly; the hint only picks the faster kernel. */
 int cgck_set_desc_len_hint(cgck_ctx_t *ctx, uint32_t max_ip_len);
 
 /* Host-resident batch (ring memory): H2D of [base, base+bytes) and of the

@@ -1,0 +1,54 @@
+#!/usr/bin/env python3
+"""Per-launch HBM traffic of the dominant kernel from separate rocprofv3
+--pmc FETCH_SIZE / WRITE_SIZE passes (tools/gpu_prof.sh), corrected as
+MI355X_MICROARCH.md's HBM section prescribes: FETCH_SIZE (KB) reads exactly
+half the bytes of a wide coalesced streaming read on gfx950, so it is
+doubled; WRITE_SIZE (KB) is exact for 16-B/lane streaming stores.
+
+    python tools/pmc_traffic.py gpurun_out/prof_fetch gpurun_out/prof_write OUT.json
+"""
+import csv
+import json
+import statistics
+import sys
+
+KERNELS = {
+    "1500": "cksum_kernel<16, 6, 1, false, true>",
+    "64": "lpp_kernel<false, 1, 6, false>",
+    "imix": "lpp_kernel<true, 1, 6, false>",
+}
+ALGO = {"1500": (16 << 20) * 1504, "64": (16 << 20) * 68, "imix": None}
+
+
+def per_kernel(path, counter):
+    out = {}
+    for r in csv.DictReader(open(f"{path}/run_counter_collection.csv")):
+        if r["Counter_Name"] != counter:
+            continue
+        out.setdefault(r["Kernel_Name"], []).append(float(r["Counter_Value"]))
+    return out
+
+
+def main():
+    fetch = per_kernel(sys.argv[1], "FETCH_SIZE")
+    write = per_kernel(sys.argv[2], "WRITE_SIZE")
+    res = {"method": "median per dispatch; bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024",
+           "source": [sys.argv[1], sys.argv[2]]}
+    for key, frag in KERNELS.items():
+        f = [v for k, v in fetch.items() if frag in k]
+        w = [v for k, v in write.items() if frag in k]
+        if not f or not w:
+            continue
+        fb = statistics.median(f[0]) * 1024 * 2
+        wb = statistics.median(w[0]) * 1024
+        res[f"bytes_per_launch_{key}"] = fb + wb
+        res[f"read_bytes_{key}"] = fb
+        res[f"write_bytes_{key}"] = wb
+        if ALGO.get(key):
+            res[f"traffic_over_algorithmic_{key}"] = (fb + wb) / ALGO[key]
+    json.dump(res, open(sys.argv[3], "w"), indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()

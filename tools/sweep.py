@@ -46,6 +46,8 @@ def main():
             desc = cgck.DeviceBuffer(12 * n)
             e0.synth_imix(buf.ptr, desc.ptr, n, 0xC0C0)
             algo = nbytes + 16 * n
+            for e in engines.values():
+                e.set_desc_len_hint(nbytes // n)
             work[w] = (lambda e, buf=buf, desc=desc: e.desc(buf.ptr, desc.ptr, n, flags, out.ptr), algo,
                        [buf, desc])
         else:
