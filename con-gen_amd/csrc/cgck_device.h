@@ -1,0 +1,257 @@
+// cgck_device.h — device-side helpers shared by the gfx950 checksum kernels.
+//
+// Arithmetic of con-gen's checksum unit (subr.c:119-223) restated for lanes:
+// 16-bit halves summed into u32 partials (v_dot2_u32_u16), one's-complement
+// folds, the reduce() finish with its 0 -> 0xFFFF rule (subr.c:150-154).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "cgck_internal.h"
+
+namespace cgck {
+
+#define CGCK_GLOBAL __attribute__((address_space(1)))
+
+__device__ __forceinline__ uint32_t hsum(uint32_t w, uint32_t acc)
+{
+	// (w & 0xffff) + (w >> 16) + acc in one v_dot2_u32_u16.
+	typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+	us2 a = __builtin_bit_cast(us2, w);
+	us2 one = {1, 1};
+	return __builtin_amdgcn_udot2(a, one, acc, false);
+}
+
+__device__ __forceinline__ uint32_t sum4(const uint4 &w, uint32_t acc)
+{
+	return hsum(w.w, hsum(w.z, hsum(w.y, hsum(w.x, acc))));
+}
+
+// Byte mask of bytes [s, e) of a dword, s, e already clamped to [0, 4].
+__device__ __forceinline__ uint32_t bmask(int s, int e)
+{
+	uint32_t hm = e >= 4 ? 0xffffffffu : ((1u << (8 * e)) - 1u);
+	uint32_t lm = 0xffffffffu << (8 * (s & 3));
+	return e > s ? (hm & lm) : 0u;
+}
+
+__device__ __forceinline__ int clamp4(int x)
+{
+	return min(max(x, 0), 4);
+}
+
+// Mask of the bytes of dword i of the chunk at packet-relative byte co that
+// fall inside [r0, r1) (packet-relative, relative to the 16-aligned c0).
+__device__ __forceinline__ uint32_t dmask(int co, int i, int r0, int r1)
+{
+	int b = co + 4 * i;
+	return bmask(clamp4(r0 - b), clamp4(r1 - b));
+}
+
+__device__ __forceinline__ uint32_t msum(const uint4 &w, int co, int r0, int r1, uint32_t acc)
+{
+	acc = hsum(w.x & dmask(co, 0, r0, r1), acc);
+	acc = hsum(w.y & dmask(co, 1, r0, r1), acc);
+	acc = hsum(w.z & dmask(co, 2, r0, r1), acc);
+	acc = hsum(w.w & dmask(co, 3, r0, r1), acc);
+	return acc;
+}
+
+__device__ __forceinline__ void zero_bytes(uint4 &w, int co, int r0, int r1)
+{
+	w.x &= ~dmask(co, 0, r0, r1);
+	w.y &= ~dmask(co, 1, r0, r1);
+	w.z &= ~dmask(co, 2, r0, r1);
+	w.w &= ~dmask(co, 3, r0, r1);
+}
+
+// Group reduction over G lanes (G in {4, 8, 16, 32, 64}); every lane of the
+// group ends with the group's sum.  quad_perm and row mirrors are DPP; the
+// 32/64 steps use cross-row swizzles.
+template <int G>
+__device__ __forceinline__ uint32_t gsum(uint32_t v)
+{
+	// xor 1 and xor 2 inside quads
+	v += __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false); // quad_perm [1,0,3,2]
+	v += __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false); // quad_perm [2,3,0,1]
+	if (G >= 8)
+		v += __builtin_amdgcn_mov_dpp(v, 0x141, 0xF, 0xF, false); // row_half_mirror
+	if (G >= 16)
+		v += __builtin_amdgcn_mov_dpp(v, 0x140, 0xF, 0xF, false); // row_mirror
+	if (G >= 32)
+		v += __shfl_xor(v, 16, 64);
+	if (G >= 64)
+		v += __shfl_xor(v, 32, 64);
+	return v;
+}
+
+// Fold a u32 one's-complement partial to 16 bits (value in [0, 0xffff],
+// congruent mod 65535).
+__device__ __forceinline__ uint32_t fold16(uint32_t x)
+{
+	x = (x & 0xffffu) + (x >> 16);
+	x = (x & 0xffffu) + (x >> 16);
+	x = (x & 0xffffu) + (x >> 16);
+	return x;
+}
+
+__device__ __forceinline__ uint32_t bswap16(uint32_t x)
+{
+	return ((x & 0xffu) << 8) | ((x >> 8) & 0xffu);
+}
+
+// reduce() of subr.c:137-156 applied to a folded, region-relative sum.
+__device__ __forceinline__ uint32_t finish(uint32_t f)
+{
+	uint32_t r = (~f) & 0xffffu;
+	return r ? r : 0xffffu;
+}
+
+__device__ __forceinline__ int l4_field(uint32_t proto, uint32_t flags)
+{
+	if (flags & CGCK_L4_NOPSEUDO)
+		return proto == 1 ? 2 : -1;
+	return proto == 6 ? 16 : (proto == 17 ? 6 : -1);
+}
+
+__device__ __forceinline__ void store16(uint8_t *p, uint32_t v)
+{
+	if ((reinterpret_cast<uintptr_t>(p) & 1) == 0) {
+		*(CGCK_GLOBAL uint16_t *)p = (uint16_t)v;
+	} else {
+		((CGCK_GLOBAL uint8_t *)p)[0] = (uint8_t)v;
+		((CGCK_GLOBAL uint8_t *)p)[1] = (uint8_t)(v >> 8);
+	}
+}
+
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+
+// Packet memory, descriptors and outputs are addressed through explicit
+// GLOBAL (address space 1) pointers.  Pointers rebuilt from integer
+// arithmetic are generic to the compiler, which then emits flat_* memory
+// ops: those count against both vmcnt and lgkmcnt, return out of order and
+// force every wait to vmcnt(0) lgkmcnt(0) — including a wait on each
+// iteration's output store.  global_* ops keep precise, in-order counting.
+template <class T>
+__device__ __forceinline__ CGCK_GLOBAL T *gbl(T *p)
+{
+	return (CGCK_GLOBAL T *)p;
+}
+
+template <class T>
+__device__ __forceinline__ CGCK_GLOBAL T *gbl_at(uint64_t a)
+{
+	return (CGCK_GLOBAL T *)a;
+}
+
+// Streaming chunk load; NT = nontemporal (read-once data, no cache retention).
+template <bool NT>
+__device__ __forceinline__ uint4 ld(const uint4 *p)
+{
+	if (NT) {
+		u32x4_t x = __builtin_nontemporal_load((const CGCK_GLOBAL u32x4_t *)p);
+		return make_uint4(x[0], x[1], x[2], x[3]);
+	}
+	const u32x4_t x = *(const CGCK_GLOBAL u32x4_t *)p;
+	return make_uint4(x[0], x[1], x[2], x[3]);
+}
+
+// Branch-free chunk load for chunk i of a run of nch >= 1 chunks: indices
+// past the run re-read the run's last chunk (same cache line, no extra HBM
+// traffic) and the caller drops their contribution.  Keeping loads out of
+// exec-masked branches keeps vmcnt counting precise.
+template <bool NT>
+__device__ __forceinline__ uint4 ldc(const uint4 *c0, int i, int nch)
+{
+	return ld<NT>(c0 + min(i, nch - 1));
+}
+
+// Chunk i of a run of n chunks, or zero when !ok.  Wave-uniform forms: all
+// lanes valid -> plain load (no exec mask, precise vmcnt); none -> no load;
+// mixed -> predicated load.
+template <bool NT>
+__device__ __forceinline__ uint4 ldz(const uint4 *c, bool ok)
+{
+	if (__all(ok))
+		return ld<NT>(c);
+	if (!__any(ok))
+		return make_uint4(0, 0, 0, 0);
+	return ok ? ld<NT>(c) : make_uint4(0, 0, 0, 0);
+}
+
+template <bool NT>
+struct GChunks {
+	const uint4 *p;
+	__device__ __forceinline__ uint4 operator[](int i) const { return ld<NT>(p + i); }
+};
+
+// Block-iteration schedule: contiguous ranges per block (p.contig) or
+// grid-stride.  Contiguous ranges keep each block's stream sequential in HBM.
+struct Sched {
+	uint64_t it, end, step;
+};
+
+__device__ __forceinline__ Sched sched(uint64_t n_iters, bool contig)
+{
+	Sched s;
+	if (contig) {
+		const uint64_t per = (n_iters + gridDim.x - 1) / gridDim.x;
+		s.it = (uint64_t)blockIdx.x * per;
+		s.end = s.it + per < n_iters ? s.it + per : n_iters;
+		s.step = 1;
+	} else {
+		s.it = blockIdx.x;
+		s.end = n_iters;
+		s.step = gridDim.x;
+	}
+	return s;
+}
+
+struct Pkt {
+	uint64_t a0;  // absolute address of the IPv4 header (or region)
+	uint32_t len; // bytes
+	bool ok;      // packet index < n
+};
+
+template <bool DESC>
+__device__ __forceinline__ Pkt get_pkt(const KParams &p, uint64_t k)
+{
+	Pkt r;
+	r.ok = k < p.n;
+	uint64_t kk = r.ok ? k : 0;
+	if (DESC) {
+		const CGCK_GLOBAL uint32_t *d = (const CGCK_GLOBAL uint32_t *)p.desc + 3 * kk;
+		uint32_t lo = d[0], hi = d[1], w2 = d[2];
+		uint64_t fo = ((uint64_t)hi << 32) | lo;
+		r.a0 = reinterpret_cast<uint64_t>(p.base) + fo + (w2 & 0xffffu);
+		r.len = w2 >> 16;
+	} else {
+		r.a0 = reinterpret_cast<uint64_t>(p.base) + kk * p.stride + p.l3_off;
+		r.len = p.ip_len;
+	}
+	if (!r.ok)
+		r.len = 0;
+	return r;
+}
+
+// (m & a) | (~m & b): one v_bfi_b32.  The mask is made opaque to the
+// optimizer so selects between array elements are never rewritten into a
+// dynamically indexed (scratch) load.
+__device__ __forceinline__ uint32_t pick(uint32_t m, uint32_t a, uint32_t b)
+{
+	return (a & m) | (b & ~m);
+}
+
+__device__ __forceinline__ uint32_t opaque(uint32_t m)
+{
+	asm volatile("" : "+v"(m));
+	return m;
+}
+
+// x - y in one's-complement (mod 65535) on folded 16-bit values.
+__device__ __forceinline__ uint32_t ocsub(uint32_t x, uint32_t y)
+{
+	return fold16(x + (0xffffu - y));
+}
+
+} // namespace cgck

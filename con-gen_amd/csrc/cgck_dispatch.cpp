@@ -1,0 +1,58 @@
+// cgck_dispatch.cpp — picks the kernel family and launch shape for a batch.
+#include "cgck_internal.h"
+
+namespace cgck {
+
+hipError_t launch_group(const KParams &p, uint32_t max_len, int num_cus, bool nt, hipStream_t st);
+hipError_t launch_lpp(const KParams &p, int num_cus, bool nt, bool occ, hipStream_t st);
+hipError_t launch_slot(const KParams &p, int num_cus, bool nt, bool occ, hipStream_t st);
+hipError_t launch_lppp(const KParams &p, int num_cus, bool nt, hipStream_t st);
+
+// `kernel` = variant | flags (include/cgck.h is agnostic of this; $CGCK_KERNEL
+// overrides it for A/B runs):
+//   variant (bits 0-3): 0 auto, 1 group (G lanes per packet), 2 lane per
+//     packet, 3 lane per 128-byte slot, 4 software-pipelined lane per packet,
+//     5 / 6 = 2 / 3 compiled for 8 / 6 waves per SIMD;
+//   kNT (bit 4) nontemporal loads, kContig (bit 5) contiguous block ranges,
+//   kExplicit (bit 6) take bits 4-5 as given instead of the measured defaults.
+// len_hint = the batch's packet length (strided) or typical length (descriptors).
+hipError_t launch_cksum(const KParams &p0, uint32_t len_hint, int num_cus, int kernel, hipStream_t st)
+{
+	if (p0.n == 0)
+		return hipSuccess;
+	KParams p = p0;
+	const bool lane_ok = !(p.flags & kFlagNoLenCheck);
+	int variant = kernel & 15;
+	if (variant == 0)
+		variant = !lane_ok ? 1 : len_hint >= kGroupFromLen ? 1 : len_hint <= kLppUpToLen ? 2 : 3;
+	if (variant >= 2 && !lane_ok)
+		variant = 1;
+	bool nt, contig;
+	if (kernel & kExplicit) {
+		nt = kernel & kNT;
+		contig = kernel & kContig;
+	} else if (variant == 1) {
+		nt = kDefaultGroupNT;
+		contig = kDefaultGroupContig;
+	} else {
+		nt = kDefaultLaneNT;
+		contig = kDefaultLaneContig;
+	}
+	p.contig = contig;
+	switch (variant) {
+	case 2:
+		return launch_lpp(p, num_cus, nt, false, st);
+	case 3:
+		return launch_slot(p, num_cus, nt, false, st);
+	case 5:
+		return launch_lpp(p, num_cus, nt, true, st);
+	case 6:
+		return launch_slot(p, num_cus, nt, true, st);
+	case 4:
+		return launch_lppp(p, num_cus, nt, st);
+	default:
+		return launch_group(p, len_hint, num_cus, nt, st);
+	}
+}
+
+} // namespace cgck

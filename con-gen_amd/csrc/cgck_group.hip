@@ -1,0 +1,235 @@
+// cgck_group.hip — the lane-group kernel: G lanes own one packet and walk
+// its 16-byte chunks with coalesced uint4 loads, S steps unrolled; group
+// partials are reduced with DPP.  Used for large packets (>= 1 KiB, the
+// 1500 B MTU configuration) and for the single-region drop-in calls.
+//
+// Per packet three masked sums are formed from one HBM stream:
+//   tot = sum over [ip, ip+ip_len)           (all lanes)
+//   ip  = sum over [ip, ip+ip_hl*4)          (header-zone lanes only)
+//   ps  = sum over [ip+12, ip+20)            (src/dst of the pseudo-header)
+// and the L4 sum is tot - ip (one's complement), plus ps, ip_p<<8 and
+// htons(l4len) read as a little-endian word (struct pseudo, subr.c:119-125).
+#include "cgck_device.h"
+
+namespace cgck {
+
+// Per-packet, per-lane partial state.
+struct Part {
+	uint32_t tot, ip, ps, fld; // fld = stored ip field | stored l4 field << 16 (abs frame)
+};
+
+// Accumulate one loaded chunk (k = chunk index inside the packet).
+template <bool HDR>
+__device__ __forceinline__ void eat(Part &pt, uint4 w, int k, int q, int len, int hl, int fo,
+				    uint32_t flags)
+{
+	const int co = k * 16;
+	if (HDR && co < q + 80) {
+		// Header zone: stored fields, optional zeroing, header sums.
+		if (flags & (CGCK_VERIFY | CGCK_ZERO_FIELDS)) {
+			uint32_t f = msum(w, co, q + 10, q + 12, 0);
+			uint32_t g = fo >= 0 ? msum(w, co, q + hl + fo, q + hl + fo + 2, 0) : 0u;
+			pt.fld += f | (g << 16);
+			zero_bytes(w, co, q + 10, q + 12);
+			if (fo >= 0)
+				zero_bytes(w, co, q + hl + fo, q + hl + fo + 2);
+		}
+		pt.ip = msum(w, co, q, q + hl, pt.ip);
+		pt.ps = msum(w, co, q + 12, q + 20, pt.ps);
+	}
+	if (co >= q && co + 16 <= q + len)
+		pt.tot = sum4(w, pt.tot);
+	else
+		pt.tot = msum(w, co, q, q + len, pt.tot);
+}
+
+template <int G, int S, int U, bool DESC, bool NT>
+__global__ __launch_bounds__(256) void cksum_kernel(KParams p)
+{
+	constexpr int GPB = 256 / G;        // groups per block
+	constexpr int PPB = GPB * U;        // packets per block iteration
+	const int lane = threadIdx.x;
+	const int gib = lane / G;           // group in block
+	const int gl = lane % G;            // lane in group
+	const uint32_t flags = p.flags;
+	const bool raw = flags & CGCK_RAW;
+	const bool need_hdr = !raw;
+
+	const Sched sc = sched((p.n + PPB - 1) / PPB, p.contig);
+	for (uint64_t blk = sc.it; blk < sc.end; blk += sc.step) {
+		Pkt pk[U];
+		uint32_t b0[U], proto[U];
+		uint4 v[U][S];
+		int nch[U];
+#pragma unroll
+		for (int u = 0; u < U; ++u) {
+			pk[u] = get_pkt<DESC>(p, blk * PPB + (uint64_t)u * GPB + gib);
+			const uint64_t a0 = pk[u].a0;
+			// Bytes read: the region, or (drop-in udp_cksum, host-guaranteed)
+			// at least the 20 header bytes the pseudo-header needs.
+			uint32_t span = pk[u].len;
+			if ((flags & kFlagNoLenCheck) && pk[u].ok && span < 20)
+				span = 20;
+			nch[u] = span ? (int)(((a0 + span + 15) >> 4) - (a0 >> 4)) : 0;
+			b0[u] = 0;
+			proto[u] = 0;
+			if (need_hdr && pk[u].ok && span > 0) {
+				b0[u] = *gbl_at<const uint8_t>(a0);
+				if (span > 9)
+					proto[u] = *gbl_at<const uint8_t>(a0 + 9);
+			}
+			const uint4 *c0 = reinterpret_cast<const uint4 *>(a0 & ~(uint64_t)15);
+			if (!__any(nch[u] == 0)) {
+				// clamped: chunks past the packet re-read its last chunk;
+				// eat() masks them out by position
+#pragma unroll
+				for (int s = 0; s < S; ++s)
+					v[u][s] = ldc<NT>(c0, s * G + gl, nch[u]);
+			} else {
+#pragma unroll
+				for (int s = 0; s < S; ++s) {
+					const int k = s * G + gl;
+					v[u][s] = k < nch[u] ? ld<NT>(c0 + k) : make_uint4(0, 0, 0, 0);
+				}
+			}
+		}
+#pragma unroll
+		for (int u = 0; u < U; ++u) {
+			const int q = (int)(pk[u].a0 & 15);
+			const int len = (int)pk[u].len;
+			const int hl = (int)(b0[u] & 15) * 4;
+			const int fo = (need_hdr && (flags & (CGCK_L4)) && len >= 20 && len >= hl &&
+					l4_field(proto[u], flags) >= 0 &&
+					hl + l4_field(proto[u], flags) + 2 <= len)
+					       ? l4_field(proto[u], flags)
+					       : -1;
+			Part pt = {0, 0, 0, 0};
+#pragma unroll
+			for (int s = 0; s < S; ++s) {
+				const int k = s * G + gl;
+				if (need_hdr && s * G * 16 < 96)
+					eat<true>(pt, v[u][s], k, q, len, hl, fo, flags);
+				else
+					eat<false>(pt, v[u][s], k, q, len, hl, fo, flags);
+			}
+			// Steps beyond the unrolled S (long packets): one at a time.
+			const uint4 *c0 = reinterpret_cast<const uint4 *>(pk[u].a0 & ~(uint64_t)15);
+			for (int s = S; __any(s * G < nch[u]); ++s) {
+				const int k = s * G + gl;
+				uint4 w = k < nch[u] ? ld<NT>(c0 + k) : make_uint4(0, 0, 0, 0);
+				if (need_hdr && s * G * 16 < 96)
+					eat<true>(pt, w, k, q, len, hl, fo, flags);
+				else
+					eat<false>(pt, w, k, q, len, hl, fo, flags);
+				pt.tot = (pt.tot & 0xffffu) + (pt.tot >> 16); // keep u32 headroom
+			}
+
+			uint32_t tot = gsum<G>(pt.tot);
+			uint32_t ip = 0, ps = 0, fld = 0;
+			if (need_hdr) {
+				ip = gsum<(G < 8 ? G : 8)>(pt.ip);
+				ps = gsum<(G < 8 ? G : 8)>(pt.ps);
+				fld = gsum<(G < 8 ? G : 8)>(pt.fld);
+			}
+			if (gl != 0 || !pk[u].ok)
+				continue; // lane 0 of the group finishes the packet
+
+			const uint64_t k = blk * PPB + (uint64_t)u * GPB + gib;
+			const bool odd = q & 1;
+			uint32_t lo = 0, hi = 0, verdict = 0;
+			if (raw) {
+				uint32_t f = fold16(tot);
+				lo = finish(odd ? bswap16(f) : f);
+			} else if (!(flags & kFlagNoLenCheck) && (len < 20 || len < hl)) {
+				verdict = CGCK_BAD_LEN;
+			} else {
+				if (flags & CGCK_IP) {
+					uint32_t f = fold16(ip);
+					lo = finish(odd ? bswap16(f) : f);
+				}
+				if (flags & CGCK_L4) {
+					const uint32_t l4len = (uint32_t)(len - hl);
+					// L4 region = datagram minus header: one's-complement
+					// subtraction, tot + ~ip (mod 65535).
+					const uint32_t l4 = fold16(tot) + (0xffffu - fold16(ip));
+					if (flags & CGCK_L4_NOPSEUDO) {
+						uint32_t f = fold16(l4);
+						hi = finish(odd ? bswap16(f) : f);
+					} else {
+						uint32_t f = fold16(l4 + ps);
+						f = odd ? bswap16(f) : f;
+						f += (proto[u] << 8) + bswap16(l4len & 0xffffu);
+						hi = finish(fold16(f));
+					}
+				}
+				if (flags & CGCK_VERIFY) {
+					uint32_t sip = fld & 0xffffu, sl4 = fld >> 16;
+					if (odd) {
+						sip = bswap16(sip);
+						sl4 = bswap16(sl4);
+					}
+					uint32_t want = sip;
+					if ((flags & CGCK_V_IP_ZERO_IS_FFFF) && want == 0)
+						want = 0xffffu;
+					if ((flags & CGCK_IP) && lo != want)
+						verdict |= CGCK_BAD_IP;
+					if ((flags & CGCK_L4) && fo >= 0 &&
+					    !((flags & CGCK_V_UDP_ZERO_SKIP) && proto[u] == 17 && sl4 == 0) &&
+					    hi != sl4)
+						verdict |= CGCK_BAD_L4;
+				}
+				if (flags & CGCK_STORE) {
+					uint8_t *ipp = reinterpret_cast<uint8_t *>(pk[u].a0);
+					if (flags & CGCK_IP)
+						store16(ipp + 10, lo);
+					if ((flags & CGCK_L4) && fo >= 0)
+						store16(ipp + hl + fo, hi);
+				}
+			}
+			if (p.out)
+				gbl(p.out)[k] = lo | (hi << 16);
+			if (p.verdict)
+				gbl(p.verdict)[k] = (uint8_t)verdict;
+			if (p.bad) {
+				if (verdict & CGCK_BAD_IP)
+					atomicAdd(p.bad + 0, 1u);
+				if (verdict & CGCK_BAD_L4)
+					atomicAdd(p.bad + 1, 1u);
+			}
+		}
+	}
+}
+
+template <int G, int S, int U, bool DESC>
+static hipError_t launch_t(const KParams &p, int max_blocks, bool nt, hipStream_t st)
+{
+	constexpr uint64_t PPB = (256 / G) * U;
+	uint64_t want = (p.n + PPB - 1) / PPB;
+	int blocks = (int)(want < (uint64_t)max_blocks ? want : (uint64_t)max_blocks);
+	if (blocks < 1)
+		blocks = 1;
+	if (nt)
+		hipLaunchKernelGGL((cksum_kernel<G, S, U, DESC, true>), dim3(blocks), dim3(256), 0, st, p);
+	else
+		hipLaunchKernelGGL((cksum_kernel<G, S, U, DESC, false>), dim3(blocks), dim3(256), 0, st, p);
+	return hipGetLastError();
+}
+
+hipError_t launch_group(const KParams &p, uint32_t max_len, int num_cus, bool nt, hipStream_t st)
+{
+	const int max_blocks = num_cus * 16;
+	const bool d = p.desc != nullptr;
+	if (max_len <= 80) // <= 6 chunks at any alignment: two steps of 4 lanes
+		return d ? launch_t<4, 2, 4, true>(p, max_blocks, nt, st)
+			 : launch_t<4, 2, 4, false>(p, max_blocks, nt, st);
+	if (max_len <= 256)
+		return d ? launch_t<16, 2, 2, true>(p, max_blocks, nt, st)
+			 : launch_t<16, 2, 2, false>(p, max_blocks, nt, st);
+	if (max_len <= 1600)
+		return d ? launch_t<16, 6, 1, true>(p, max_blocks, nt, st)
+			 : launch_t<16, 6, 1, false>(p, max_blocks, nt, st);
+	return d ? launch_t<64, 4, 1, true>(p, max_blocks, nt, st)
+		 : launch_t<64, 4, 1, false>(p, max_blocks, nt, st);
+}
+
+} // namespace cgck

@@ -28,17 +28,18 @@ struct KParams {
 	uint32_t contig; // set by the launcher: contiguous block ranges
 };
 
-// Kernel selection flags (see launch_cksum) and the measured defaults.
+// Kernel selection flags (see cgck_dispatch.cpp) and the measured defaults
+// (tools/sweep.py; profiles/r01).  The group kernel streams whole lines per
+// wave-instruction, so nontemporal loads + contiguous block ranges win
+// (1500 B: 5.79 -> 6.18 TB/s); the lane kernels re-touch each line from
+// several instructions, so they want cached loads (NT: -30..-50 %).
 constexpr int kNT = 16, kContig = 32, kExplicit = 64;
-constexpr int kDefaultLpp = 5;
-// Measured (tools/sweep.py, profiles/r01): the group kernel streams whole
-// lines per wave-instruction, so nontemporal loads + contiguous block ranges
-// win (1500 B: 5.79 -> 6.18 TB/s); the lane-per-packet kernel re-touches each
-// line from several instructions, so it wants cached loads (NT: -30..-50 %).
+constexpr uint32_t kGroupFromLen = 1024; // typical length from which the group kernel is used
+constexpr uint32_t kLppUpToLen = 128;    // lane-per-packet up to here, lane-per-slot above
 constexpr bool kDefaultGroupNT = true, kDefaultGroupContig = true;
-constexpr bool kDefaultLppNT = false, kDefaultLppContig = false;
+constexpr bool kDefaultLaneNT = false, kDefaultLaneContig = false;
 
-hipError_t launch_cksum(const KParams &p, uint32_t max_len, int num_cus, int family, hipStream_t st);
+hipError_t launch_cksum(const KParams &p, uint32_t len_hint, int num_cus, int kernel, hipStream_t st);
 hipError_t launch_synth_fill(uint8_t *base, uint64_t nbytes, uint64_t seed, int num_cus, hipStream_t st);
 hipError_t launch_synth_stamp(uint8_t *base, uint64_t n, uint64_t stride, uint32_t len, int num_cus,
 			      hipStream_t st);

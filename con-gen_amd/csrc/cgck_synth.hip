@@ -1,0 +1,275 @@
+// cgck_synth.hip — device-side synthetic batches and the
+// streaming-read diagnostics probes.
+#include "cgck_device.h"
+
+namespace cgck {
+
+// --------------------------------------------------------------------------
+// Synthetic input: byte j of the stream = byte j&7 of
+// splitmix64(seed, j>>3); then per-packet header stamps.
+// --------------------------------------------------------------------------
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t seed, uint64_t j)
+{
+	uint64_t z = seed + (j + 1) * 0x9e3779b97f4a7c15ull;
+	z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+	z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+	return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(256) void synth_fill_kernel(uint8_t *base, uint64_t nbytes, uint64_t seed)
+{
+	const uint64_t nw = nbytes >> 3;
+	uint64_t *w = reinterpret_cast<uint64_t *>(base);
+	for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; 2 * i < nw;
+	     i += (uint64_t)gridDim.x * 256) {
+		uint64_t j = 2 * i;
+		if (j + 1 < nw) {
+			ulonglong2 x = make_ulonglong2(splitmix64(seed, j), splitmix64(seed, j + 1));
+			*reinterpret_cast<ulonglong2 *>(w + j) = x;
+		} else {
+			w[j] = splitmix64(seed, j);
+		}
+	}
+	if (blockIdx.x == 0 && threadIdx.x < (nbytes & 7)) {
+		uint64_t b = (nw << 3) + threadIdx.x;
+		base[b] = (uint8_t)(splitmix64(seed, b >> 3) >> (8 * (b & 7)));
+	}
+}
+
+__device__ __forceinline__ void stamp(uint8_t *ip, uint32_t len)
+{
+	ip[0] = 0x45;
+	ip[1] = 0;
+	ip[2] = (uint8_t)(len >> 8);
+	ip[3] = (uint8_t)len;
+	ip[9] = 6;
+	ip[10] = 0;
+	ip[11] = 0;
+	if (len >= 38) {
+		ip[36] = 0;
+		ip[37] = 0;
+	}
+}
+
+__global__ __launch_bounds__(256) void synth_stamp_strided_kernel(uint8_t *base, uint64_t n,
+								  uint64_t stride, uint32_t len)
+{
+	for (uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x; k < n;
+	     k += (uint64_t)gridDim.x * 256)
+		stamp(base + k * stride, len);
+}
+
+__constant__ uint16_t c_imix_len[12] = {64, 576, 64, 64, 576, 64, 1500, 64, 576, 64, 64, 576};
+__constant__ uint16_t c_imix_off[12] = {0, 64, 640, 704, 768, 1344, 1408, 2908, 2972, 3548, 3612, 3676};
+
+__global__ __launch_bounds__(256) void synth_imix_kernel(uint8_t *base, uint32_t *desc, uint64_t n)
+{
+	for (uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x; k < n;
+	     k += (uint64_t)gridDim.x * 256) {
+		uint64_t off = (k / 12) * (uint64_t)kImixCycleBytes + c_imix_off[k % 12];
+		uint32_t len = c_imix_len[k % 12];
+		stamp(base + off, len);
+		desc[3 * k + 0] = (uint32_t)off;
+		desc[3 * k + 1] = (uint32_t)(off >> 32);
+		desc[3 * k + 2] = len << 16; // l3_off 0, ip_len
+	}
+}
+
+// --------------------------------------------------------------------------
+// Diagnostics: streaming-read probe (what this box's HBM delivers to a plain
+// coalesced uint4 read with minimal arithmetic) — the practical ceiling the
+// checksum kernels are compared against in DESIGN.md.
+// --------------------------------------------------------------------------
+
+template <int UN, bool NT>
+__global__ __launch_bounds__(256) void probe_read_kernel(const uint4 *src, uint64_t n16, uint32_t *sink)
+{
+	uint32_t acc = 0;
+	const uint64_t stride = (uint64_t)gridDim.x * 256;
+	uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+	for (; i + (UN - 1) * stride < n16; i += UN * stride) {
+		uint4 w[UN];
+#pragma unroll
+		for (int j = 0; j < UN; ++j)
+			w[j] = ld<NT>(src + i + j * stride);
+#pragma unroll
+		for (int j = 0; j < UN; ++j)
+			acc = sum4(w[j], acc);
+	}
+	for (; i < n16; i += stride)
+		acc = sum4(src[i], acc);
+	if (acc == 0x12345678u) // keeps the loads live; practically never stores
+		sink[0] = acc;
+}
+
+// Contiguous-per-block variant: block b streams [b*per, (b+1)*per).
+template <int UN>
+__global__ __launch_bounds__(256) void probe_block_kernel(const uint4 *src, uint64_t n16, uint32_t *sink)
+{
+	uint32_t acc = 0;
+	const uint64_t per = (n16 + gridDim.x - 1) / gridDim.x;
+	const uint64_t b0 = (uint64_t)blockIdx.x * per, b1 = b0 + per < n16 ? b0 + per : n16;
+	uint64_t i = b0 + threadIdx.x;
+	for (; i + (UN - 1) * 256 < b1; i += UN * 256) {
+		uint4 w[UN];
+#pragma unroll
+		for (int j = 0; j < UN; ++j)
+			w[j] = src[i + j * 256];
+#pragma unroll
+		for (int j = 0; j < UN; ++j)
+			acc = sum4(w[j], acc);
+	}
+	for (; i < b1; i += 256)
+		acc = sum4(src[i], acc);
+	if (acc == 0x12345678u)
+		sink[0] = acc;
+}
+
+// Lane-strided variant: lane reads CH consecutive uint4 (one "packet" of
+// 16*CH bytes), lanes 16*CH bytes apart — the lane-per-packet access shape.
+template <int CH>
+__global__ __launch_bounds__(256) void probe_lane_kernel(const uint4 *src, uint64_t n16, uint32_t *sink)
+{
+	uint32_t acc = 0;
+	const uint64_t npk = n16 / CH;
+	for (uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x; k < npk; k += (uint64_t)gridDim.x * 256) {
+		uint4 w[CH];
+#pragma unroll
+		for (int j = 0; j < CH; ++j)
+			w[j] = src[k * CH + j];
+#pragma unroll
+		for (int j = 0; j < CH; ++j)
+			acc = sum4(w[j], acc);
+	}
+	if (acc == 0x12345678u)
+		sink[0] = acc;
+}
+
+// Latency-structure probe: lane reads 4 uint4 (64 B) per iteration, then
+// runs K dependent VALU ops on them; PIPE prefetches the next iteration's
+// chunks before the ALU work (software pipelining).
+template <int K, bool PIPE>
+__global__ __launch_bounds__(256) void probe_alu_kernel(const uint4 *src, uint64_t n16, uint32_t *sink)
+{
+	uint32_t acc = 0;
+	const uint64_t npk = n16 / 4;
+	const uint64_t stride = (uint64_t)gridDim.x * 256;
+	uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+	uint4 w[4], nx[4];
+	if (PIPE && k < npk) {
+#pragma unroll
+		for (int j = 0; j < 4; ++j)
+			nx[j] = src[k * 4 + j];
+	}
+	for (; k < npk; k += stride) {
+#pragma unroll
+		for (int j = 0; j < 4; ++j)
+			w[j] = PIPE ? nx[j] : src[k * 4 + j];
+		if (PIPE && k + stride < npk) {
+#pragma unroll
+			for (int j = 0; j < 4; ++j)
+				nx[j] = src[(k + stride) * 4 + j];
+		}
+		uint32_t x = 0;
+#pragma unroll
+		for (int j = 0; j < 4; ++j)
+			x = sum4(w[j], x);
+#pragma unroll
+		for (int i = 0; i < K; ++i)
+			x = __builtin_amdgcn_alignbyte(x, x ^ (uint32_t)i, 1u) + (uint32_t)i;
+		acc += x;
+	}
+	if (acc == 0x12345678u)
+		sink[0] = acc;
+}
+
+hipError_t launch_probe_read(const void *src, uint64_t bytes, uint32_t *sink, int num_cus, int variant,
+			     hipStream_t st)
+{
+	const uint4 *s = reinterpret_cast<const uint4 *>(src);
+	const uint64_t n = bytes / 16;
+	switch (variant) {
+	case 1:
+		hipLaunchKernelGGL((probe_read_kernel<8, true>), dim3(num_cus * 8), dim3(256), 0, st, s, n, sink);
+		break;
+	case 2:
+		hipLaunchKernelGGL((probe_read_kernel<16, false>), dim3(num_cus * 4), dim3(256), 0, st, s, n, sink);
+		break;
+	case 3:
+		hipLaunchKernelGGL((probe_read_kernel<4, false>), dim3(num_cus * 16), dim3(256), 0, st, s, n, sink);
+		break;
+	case 4:
+		hipLaunchKernelGGL((probe_block_kernel<8>), dim3(num_cus * 8), dim3(256), 0, st, s, n, sink);
+		break;
+	case 5:
+		hipLaunchKernelGGL((probe_read_kernel<8, false>), dim3(num_cus * 32), dim3(256), 0, st, s, n, sink);
+		break;
+	case 6:
+		hipLaunchKernelGGL((probe_lane_kernel<4>), dim3(num_cus * 8), dim3(256), 0, st, s, n, sink);
+		break;
+	case 7:
+		hipLaunchKernelGGL((probe_lane_kernel<8>), dim3(num_cus * 8), dim3(256), 0, st, s, n, sink);
+		break;
+	case 8:
+		hipLaunchKernelGGL((probe_lane_kernel<2>), dim3(num_cus * 8), dim3(256), 0, st, s, n, sink);
+		break;
+	case 9:
+		hipLaunchKernelGGL((probe_alu_kernel<100, false>), dim3(num_cus * 8), dim3(256), 0, st, s, n, sink);
+		break;
+	case 10:
+		hipLaunchKernelGGL((probe_alu_kernel<300, false>), dim3(num_cus * 8), dim3(256), 0, st, s, n, sink);
+		break;
+	case 11:
+		hipLaunchKernelGGL((probe_alu_kernel<600, false>), dim3(num_cus * 8), dim3(256), 0, st, s, n, sink);
+		break;
+	case 12:
+		hipLaunchKernelGGL((probe_alu_kernel<100, true>), dim3(num_cus * 8), dim3(256), 0, st, s, n, sink);
+		break;
+	case 13:
+		hipLaunchKernelGGL((probe_alu_kernel<300, true>), dim3(num_cus * 8), dim3(256), 0, st, s, n, sink);
+		break;
+	case 14:
+		hipLaunchKernelGGL((probe_alu_kernel<600, true>), dim3(num_cus * 8), dim3(256), 0, st, s, n, sink);
+		break;
+	case 15:
+		hipLaunchKernelGGL((probe_alu_kernel<0, false>), dim3(num_cus * 8), dim3(256), 0, st, s, n, sink);
+		break;
+	default:
+		hipLaunchKernelGGL((probe_read_kernel<8, false>), dim3(num_cus * 8), dim3(256), 0, st, s, n, sink);
+	}
+	return hipGetLastError();
+}
+
+hipError_t launch_synth_fill(uint8_t *base, uint64_t nbytes, uint64_t seed, int num_cus, hipStream_t st)
+{
+	uint64_t want = (nbytes / 16 + 255) / 256;
+	int blocks = (int)(want < (uint64_t)num_cus * 8 ? want : (uint64_t)num_cus * 8);
+	if (blocks < 1)
+		blocks = 1;
+	hipLaunchKernelGGL(synth_fill_kernel, dim3(blocks), dim3(256), 0, st, base, nbytes, seed);
+	return hipGetLastError();
+}
+
+hipError_t launch_synth_stamp(uint8_t *base, uint64_t n, uint64_t stride, uint32_t len, int num_cus,
+			      hipStream_t st)
+{
+	uint64_t want = (n + 255) / 256;
+	int blocks = (int)(want < (uint64_t)num_cus * 8 ? want : (uint64_t)num_cus * 8);
+	if (blocks < 1)
+		blocks = 1;
+	hipLaunchKernelGGL(synth_stamp_strided_kernel, dim3(blocks), dim3(256), 0, st, base, n, stride, len);
+	return hipGetLastError();
+}
+
+hipError_t launch_synth_imix(uint8_t *base, uint32_t *desc, uint64_t n, int num_cus, hipStream_t st)
+{
+	uint64_t want = (n + 255) / 256;
+	int blocks = (int)(want < (uint64_t)num_cus * 8 ? want : (uint64_t)num_cus * 8);
+	if (blocks < 1)
+		blocks = 1;
+	hipLaunchKernelGGL(synth_imix_kernel, dim3(blocks), dim3(256), 0, st, base, desc, n);
+	return hipGetLastError();
+}
+
+} // namespace cgck

@@ -16,7 +16,7 @@ sizes = [int(x) << 20 for x in os.environ.get("PROBE_MB", "64,256,1024,4096,2400
 variants = [int(x) for x in os.environ.get("PROBE_VARIANTS", "0,1,2,3,4,5").split(",")]
 engines = {}
 for v in variants:
-    os.environ["CGCK_KERNEL"] = f"lpp{v}" if v else "auto"
+    os.environ["CGCK_KERNEL"] = str(v)
     e = cgck.Engine(0)
     engines[v] = e
 L = cgck.load()
