@@ -66,6 +66,7 @@ struct cgck_ctx {
 	size_t d_bytes_cap;
 	uint8_t *d_aux; // descriptors | out | verdict
 	size_t d_aux_cap;
+	void *d_zero; // 64 zero bytes (KParams.zero)
 };
 
 struct cgck_event {
@@ -138,6 +139,11 @@ extern "C" int cgck_ctx_create(int device, cgck_ctx_t **out)
 		free(c);
 		return set_err(-EIO, "hipStreamCreate: %s", hipGetErrorString(e));
 	}
+	if ((e = hipMalloc(&c->d_zero, 64)) != hipSuccess || (e = hipMemset(c->d_zero, 0, 64)) != hipSuccess) {
+		(void)hipStreamDestroy(c->stream);
+		free(c);
+		return set_err(-EIO, "zero chunk: %s", hipGetErrorString(e));
+	}
 	*out = c;
 	return 0;
 }
@@ -157,6 +163,8 @@ extern "C" int cgck_ctx_destroy(cgck_ctx_t *c)
 		(void)hipFree(c->d_bytes);
 	if (c->d_aux)
 		(void)hipFree(c->d_aux);
+	if (c->d_zero)
+		(void)hipFree(c->d_zero);
 	free(c);
 	return 0;
 }
@@ -201,9 +209,11 @@ static int check_flags(uint32_t flags)
 	return 0;
 }
 
-static int run(cgck_ctx *c, const KParams &p, uint32_t max_len, hipStream_t st)
+static int run(cgck_ctx *c, const KParams &p0, uint32_t max_len, hipStream_t st)
 {
 	HIP_TRY(hipSetDevice(c->device));
+	KParams p = p0;
+	p.zero = c->d_zero;
 	hipError_t e = launch_cksum(p, max_len, c->num_cus, c->family, st);
 	if (e != hipSuccess)
 		return set_err(-EIO, "cksum launch: %s", hipGetErrorString(e));
@@ -223,7 +233,7 @@ extern "C" int cgck_strided(cgck_ctx_t *c, void *base, uint64_t n, uint64_t stri
 		return set_err(-EINVAL, "cgck_strided: NULL base");
 	if (ip_len > 0x7fffffffu)
 		return set_err(-EINVAL, "cgck_strided: ip_len too large");
-	KParams p = {(const uint8_t *)base, nullptr, n, stride, l3_off, ip_len, flags, out, verdict, bad, 0};
+	KParams p = {(const uint8_t *)base, nullptr, n, stride, l3_off, ip_len, flags, out, verdict, bad, 0, nullptr};
 	return run(c, p, ip_len, pick(c, stream));
 }
 
@@ -239,7 +249,7 @@ extern "C" int cgck_desc(cgck_ctx_t *c, void *base, const cgck_desc_t *desc, uin
 		return set_err(-EINVAL, "cgck_desc: NULL base or descriptors");
 	if (((uintptr_t)desc & 3) != 0)
 		return set_err(-EINVAL, "cgck_desc: descriptors must be 4-byte aligned");
-	KParams p = {(const uint8_t *)base, desc, n, 0, 0, 0, flags, out, verdict, bad, 0};
+	KParams p = {(const uint8_t *)base, desc, n, 0, 0, 0, flags, out, verdict, bad, 0, nullptr};
 	return run(c, p, c->desc_len_hint, pick(c, stream));
 }
 
@@ -271,7 +281,7 @@ extern "C" int cgck_desc_host(cgck_ctx_t *c, void *base, size_t bytes, const cgc
 	hipStream_t st = c->stream;
 	HIP_TRY(hipMemcpyAsync(c->d_bytes, base, bytes, hipMemcpyHostToDevice, st));
 	HIP_TRY(hipMemcpyAsync(d_desc, desc, dbytes, hipMemcpyHostToDevice, st));
-	KParams p = {c->d_bytes, (const cgck_desc_t *)d_desc, n, 0, 0, 0, flags, d_out, d_ver, nullptr, 0};
+	KParams p = {c->d_bytes, (const cgck_desc_t *)d_desc, n, 0, 0, 0, flags, d_out, d_ver, nullptr, 0, nullptr};
 	if ((rc = run(c, p, c->desc_len_hint, st)))
 		return rc;
 	if (out)
@@ -345,7 +355,7 @@ uint32_t one_packet(const void *src, uint32_t span, uint32_t ip_len, uint32_t fl
 		die("staging allocation");
 	if (span)
 		memcpy(c->h_stage, src, span);
-	KParams p = {c->h_stage, nullptr, 1, 0, 0, ip_len, flags, c->h_out, nullptr, nullptr, 0};
+	KParams p = {c->h_stage, nullptr, 1, 0, 0, ip_len, flags, c->h_out, nullptr, nullptr, 0, nullptr};
 	if (run(c, p, ip_len, c->stream) != 0)
 		die("kernel launch");
 	if (hipStreamSynchronize(c->stream) != hipSuccess) {
@@ -449,7 +459,7 @@ extern "C" int cgck_tx_flush(void)
 	// entries for the segment checksum; both read their fields as zero, as
 	// the reference's callers have just stored them (ip_output.c:61,
 	// tcp_subr.c:75 / gbtcp/tcp.c:426,436).
-	KParams p = {c->h_stage, d, n, 0, 0, 0, CGCK_IP | CGCK_L4 | CGCK_ZERO_FIELDS, o, nullptr, nullptr, 0};
+	KParams p = {c->h_stage, d, n, 0, 0, 0, CGCK_IP | CGCK_L4 | CGCK_ZERO_FIELDS, o, nullptr, nullptr, 0, nullptr};
 	if ((rc = run(c, p, 1500, c->stream)))
 		return rc;
 	HIP_TRY(hipStreamSynchronize(c->stream));

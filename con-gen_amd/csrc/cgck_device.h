@@ -156,27 +156,15 @@ __device__ __forceinline__ uint4 ld(const uint4 *p)
 	return make_uint4(x[0], x[1], x[2], x[3]);
 }
 
-// Branch-free chunk load for chunk i of a run of nch >= 1 chunks: indices
-// past the run re-read the run's last chunk (same cache line, no extra HBM
-// traffic) and the caller drops their contribution.  Keeping loads out of
-// exec-masked branches keeps vmcnt counting precise.
+// Branch-free chunk load: chunk i of a run of nch chunks starting at c0;
+// indices past the run re-read its last chunk (same cache line, no extra HBM
+// traffic) and lanes without chunks read the context's zero chunk, so no
+// load sits in an exec-masked branch and vmcnt counting stays precise.  The
+// caller drops the contribution of indices >= nch.
 template <bool NT>
-__device__ __forceinline__ uint4 ldc(const uint4 *c0, int i, int nch)
+__device__ __forceinline__ uint4 ldc(const uint4 *c0, int i, int nch, const void *zero)
 {
-	return ld<NT>(c0 + min(i, nch - 1));
-}
-
-// Chunk i of a run of n chunks, or zero when !ok.  Wave-uniform forms: all
-// lanes valid -> plain load (no exec mask, precise vmcnt); none -> no load;
-// mixed -> predicated load.
-template <bool NT>
-__device__ __forceinline__ uint4 ldz(const uint4 *c, bool ok)
-{
-	if (__all(ok))
-		return ld<NT>(c);
-	if (!__any(ok))
-		return make_uint4(0, 0, 0, 0);
-	return ok ? ld<NT>(c) : make_uint4(0, 0, 0, 0);
+	return ld<NT>(nch > 0 ? c0 + min(i, nch - 1) : reinterpret_cast<const uint4 *>(zero));
 }
 
 template <bool NT>

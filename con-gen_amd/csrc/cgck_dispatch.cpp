@@ -4,15 +4,16 @@
 namespace cgck {
 
 hipError_t launch_group(const KParams &p, uint32_t max_len, int num_cus, bool nt, hipStream_t st);
-hipError_t launch_lpp(const KParams &p, int num_cus, bool nt, bool occ, hipStream_t st);
-hipError_t launch_slot(const KParams &p, int num_cus, bool nt, bool occ, hipStream_t st);
+hipError_t launch_lpp(const KParams &p, int num_cus, bool nt, int shape, hipStream_t st);
+hipError_t launch_slot(const KParams &p, int num_cus, bool nt, hipStream_t st);
 hipError_t launch_lppp(const KParams &p, int num_cus, bool nt, hipStream_t st);
 
 // `kernel` = variant | flags (include/cgck.h is agnostic of this; $CGCK_KERNEL
 // overrides it for A/B runs):
 //   variant (bits 0-3): 0 auto, 1 group (G lanes per packet), 2 lane per
 //     packet, 3 lane per 128-byte slot, 4 software-pipelined lane per packet,
-//     5 / 6 = 2 / 3 compiled for 8 / 6 waves per SIMD;
+//     5..8 lane per packet shapes 1..3, 0 (6 clamped, 6 predicated,
+//     4 predicated, 4 clamped chunks up front);
 //   kNT (bit 4) nontemporal loads, kContig (bit 5) contiguous block ranges,
 //   kExplicit (bit 6) take bits 4-5 as given instead of the measured defaults.
 // len_hint = the batch's packet length (strided) or typical length (descriptors).
@@ -41,13 +42,17 @@ hipError_t launch_cksum(const KParams &p0, uint32_t len_hint, int num_cus, int k
 	p.contig = contig;
 	switch (variant) {
 	case 2:
-		return launch_lpp(p, num_cus, nt, false, st);
+		return launch_lpp(p, num_cus, nt, kDefaultLppShape, st);
 	case 3:
-		return launch_slot(p, num_cus, nt, false, st);
+		return launch_slot(p, num_cus, nt, st);
 	case 5:
-		return launch_lpp(p, num_cus, nt, true, st);
+		return launch_lpp(p, num_cus, nt, 1, st);
 	case 6:
-		return launch_slot(p, num_cus, nt, true, st);
+		return launch_lpp(p, num_cus, nt, 2, st);
+	case 7:
+		return launch_lpp(p, num_cus, nt, 3, st);
+	case 8:
+		return launch_lpp(p, num_cus, nt, 0, st);
 	case 4:
 		return launch_lppp(p, num_cus, nt, st);
 	default:

@@ -79,19 +79,11 @@ __global__ __launch_bounds__(256) void cksum_kernel(KParams p)
 					proto[u] = *gbl_at<const uint8_t>(a0 + 9);
 			}
 			const uint4 *c0 = reinterpret_cast<const uint4 *>(a0 & ~(uint64_t)15);
-			if (!__any(nch[u] == 0)) {
-				// clamped: chunks past the packet re-read its last chunk;
-				// eat() masks them out by position
+			// clamped: chunks past the packet re-read its last chunk and
+			// eat() masks them out by position (zero-chunk lanes read zeros)
 #pragma unroll
-				for (int s = 0; s < S; ++s)
-					v[u][s] = ldc<NT>(c0, s * G + gl, nch[u]);
-			} else {
-#pragma unroll
-				for (int s = 0; s < S; ++s) {
-					const int k = s * G + gl;
-					v[u][s] = k < nch[u] ? ld<NT>(c0 + k) : make_uint4(0, 0, 0, 0);
-				}
-			}
+			for (int s = 0; s < S; ++s)
+				v[u][s] = ldc<NT>(c0, s * G + gl, nch[u], p.zero);
 		}
 #pragma unroll
 		for (int u = 0; u < U; ++u) {

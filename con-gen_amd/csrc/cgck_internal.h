@@ -26,6 +26,7 @@ struct KParams {
 	uint8_t *verdict;
 	uint32_t *bad;
 	uint32_t contig; // set by the launcher: contiguous block ranges
+	const void *zero; // 64 zero bytes of device memory (safe target for clamped loads)
 };
 
 // Kernel selection flags (see cgck_dispatch.cpp) and the measured defaults
@@ -36,6 +37,7 @@ struct KParams {
 constexpr int kNT = 16, kContig = 32, kExplicit = 64;
 constexpr uint32_t kGroupFromLen = 1024; // typical length from which the group kernel is used
 constexpr uint32_t kLppUpToLen = 128;    // lane-per-packet up to here, lane-per-slot above
+constexpr int kDefaultLppShape = 0;       // see launch_lpp
 constexpr bool kDefaultGroupNT = true, kDefaultGroupContig = true;
 constexpr bool kDefaultLaneNT = false, kDefaultLaneContig = false;
 

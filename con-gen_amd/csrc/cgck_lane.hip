@@ -66,17 +66,22 @@ __device__ __forceinline__ uint32_t rdw(const uint32_t (&D)[24], int i, const Al
 
 // Header facts of the packet whose chunk run starts with v[0..5]; `act`
 // marks the lanes whose result is used (wave-uniform paths consult only them).
-template <int NV>
-__device__ __forceinline__ Hdr header(const uint4 (&v)[NV], int q, int len, uint32_t flags, bool act)
+// The header zone spans chunks 0..5; with NV = 4 loaded chunks, chunks 4..5
+// are fetched (from c0, nch) only when some active packet has ip_hl != 5 —
+// ip_hl 5 with both fields stays within bytes [q, q + 40) <= chunk 3.
+template <int NV, bool NT>
+__device__ __forceinline__ Hdr header(const uint4 (&v)[NV], const uint4 *c0, int nch, int q, int len,
+				      uint32_t flags, bool act)
 {
-	static_assert(NV >= 6, "the header zone spans chunks 0..5");
+	static_assert(NV >= 4, "ip_hl 5 needs chunks 0..3");
 	uint32_t D[24];
 #pragma unroll
 	for (int i = 0; i < 6; ++i) {
-		D[4 * i + 0] = v[i].x;
-		D[4 * i + 1] = v[i].y;
-		D[4 * i + 2] = v[i].z;
-		D[4 * i + 3] = v[i].w;
+		const uint4 c = i < NV ? v[i < NV ? i : 0] : make_uint4(0, 0, 0, 0);
+		D[4 * i + 0] = c.x;
+		D[4 * i + 1] = c.y;
+		D[4 * i + 2] = c.z;
+		D[4 * i + 3] = c.w;
 	}
 	Align a;
 	const int qd = q >> 2;
@@ -95,6 +100,16 @@ __device__ __forceinline__ Hdr header(const uint4 (&v)[NV], int q, int len, uint
 	h.ps = hsum(R4, hsum(R3, 0));
 	const bool all5 = !__any(act && h.hd != 5);
 	uint32_t hor = 5;
+	if (!all5 && NV < 6) {
+#pragma unroll
+		for (int i = NV; i < 6; ++i) {
+			const uint4 c = act && i < nch ? ld<NT>(c0 + i) : make_uint4(0, 0, 0, 0);
+			D[4 * i + 0] = c.x;
+			D[4 * i + 1] = c.y;
+			D[4 * i + 2] = c.z;
+			D[4 * i + 3] = c.w;
+		}
+	}
 	if (all5) {
 		h.ip = hsum(R4, hsum(R3, hsum(R2, hsum(R1, hsum(R0, 0)))));
 	} else {
@@ -250,10 +265,9 @@ __device__ __forceinline__ int nchunks(uint64_t a0, uint32_t len)
 // Lane per packet
 // --------------------------------------------------------------------------
 
-template <bool DESC, bool NT, int W>
-__global__ __launch_bounds__(256, W) void lpp_kernel(KParams p)
+template <bool DESC, bool NT, int S0, bool CLAMP>
+__global__ __launch_bounds__(256) void lpp_kernel(KParams p)
 {
-	constexpr int S0 = 6;
 	const bool raw = p.flags & CGCK_RAW;
 	const Sched sc = sched((p.n + 255) / 256, p.contig);
 	for (uint64_t it = sc.it; it < sc.end; it += sc.step) {
@@ -262,37 +276,47 @@ __global__ __launch_bounds__(256, W) void lpp_kernel(KParams p)
 		const uint64_t a0 = pk.a0;
 		const int len = (int)pk.len, q = (int)(a0 & 15), nch = nchunks(a0, pk.len);
 		const uint4 *c0 = reinterpret_cast<const uint4 *>(a0 & ~(uint64_t)15);
+		// first S0 chunks: clamped and branch-free (precise vmcnt) or
+		// predicated per lane (no duplicate loads)
 		uint4 v[S0];
 #pragma unroll
 		for (int i = 0; i < S0; ++i)
-			v[i] = ldz<NT>(c0 + i, i < nch);
-		const uint4 last = ldz<NT>(c0 + nch - 1, nch > S0);
+			v[i] = CLAMP ? ldc<NT>(c0, i, nch, p.zero) : (i < nch ? ld<NT>(c0 + i) : make_uint4(0, 0, 0, 0));
+		const bool more = __any(nch > S0);
+		uint4 last = make_uint4(0, 0, 0, 0);
+		if (CLAMP) {
+			if (more)
+				last = ldc<NT>(c0, nch - 1, nch, p.zero);
+		} else {
+			last = nch > S0 ? ld<NT>(c0 + nch - 1) : make_uint4(0, 0, 0, 0);
+		}
 
 		uint32_t tot = 0;
 #pragma unroll
 		for (int i = 0; i < S0; ++i)
-			if (__any(i < nch))
-				tot = sum4(v[i], tot);
+			tot = i < nch ? sum4(v[i], tot) : tot;
 		Hdr h{};
 		if (!raw)
-			h = header(v, q, len, p.flags, pk.ok);
-		// chunks S0 .. nch-2 (the last one is `last`), 8 per step
-		for (int t = S0; __any(t < nch - 1); t += 8) {
-			uint4 w[8];
+			h = header<S0, NT>(v, c0, nch, q, len, p.flags, pk.ok);
+		if (more) {
+			// chunks S0 .. nch-2 (the last one is `last`), 8 per step
+			for (int t = S0; __any(t < nch - 1); t += 8) {
+				uint4 w[8];
 #pragma unroll
-			for (int i = 0; i < 8; ++i)
-				w[i] = ldz<NT>(c0 + t + i, t + i < nch - 1);
-			uint32_t s = 0;
+				for (int i = 0; i < 8; ++i)
+					w[i] = t + i < nch - 1 ? ld<NT>(c0 + t + i) : make_uint4(0, 0, 0, 0);
+				uint32_t s = 0;
 #pragma unroll
-			for (int i = 0; i < 8; ++i)
-				s = sum4(w[i], s);
-			tot = fold16(tot) + fold16(s);
+				for (int i = 0; i < 8; ++i)
+					s = sum4(w[i], s);
+				tot = fold16(tot) + fold16(s);
+			}
 		}
 		const bool dw = !__any(((q | len) & 3) != 0);
 		if (__any(q != 0))
 			tot = fold16(tot) + (0xffffu - fold16(lead_sum(v[0], q, dw)));
 		const int e = q + len - 16 * (nch - 1); // bytes of the last chunk inside
-		if (__any(nch > S0))
+		if (more)
 			tot = fold16(tot) + fold16(nch > S0 ? sum4(last, 0) - trail_sum(last, e, dw) : 0u);
 		if (__any(nch > 0 && nch <= S0 && e != 16)) {
 			uint4 lc = make_uint4(0, 0, 0, 0);
@@ -330,8 +354,8 @@ __global__ __launch_bounds__(256) void lppp_kernel(KParams p)
 		const uint4 *c0 = reinterpret_cast<const uint4 *>(pk.a0 & ~(uint64_t)15);
 #pragma unroll
 		for (int i = 0; i < S0; ++i)
-			v[i] = ldz<NT>(c0 + i, i < nch);
-		last = ldz<NT>(c0 + nch - 1, nch > S0);
+			v[i] = ldc<NT>(c0, i, nch, p.zero);
+		last = ldc<NT>(c0, nch - 1, nch, p.zero);
 	}
 	for (; it < sc.end; it += sc.step) {
 		const uint64_t k = it * 256 + threadIdx.x;
@@ -343,8 +367,8 @@ __global__ __launch_bounds__(256) void lppp_kernel(KParams p)
 			const uint4 *c0 = reinterpret_cast<const uint4 *>(pkn.a0 & ~(uint64_t)15);
 #pragma unroll
 			for (int i = 0; i < S0; ++i)
-				vn[i] = ldz<NT>(c0 + i, i < nch);
-			lastn = ldz<NT>(c0 + nch - 1, nch > S0);
+				vn[i] = ldc<NT>(c0, i, nch, p.zero);
+			lastn = ldc<NT>(c0, nch - 1, nch, p.zero);
 		}
 		pk2 = get_pkt<DESC>(p, (it + 2 * sc.step) * 256 + threadIdx.x);
 
@@ -354,16 +378,15 @@ __global__ __launch_bounds__(256) void lppp_kernel(KParams p)
 		uint32_t tot = 0;
 #pragma unroll
 		for (int i = 0; i < S0; ++i)
-			if (__any(i < nch))
-				tot = sum4(v[i], tot);
+			tot = i < nch ? sum4(v[i], tot) : tot;
 		Hdr h{};
 		if (!raw)
-			h = header(v, q, len, p.flags, pk.ok);
+			h = header<S0, NT>(v, c0, nch, q, len, p.flags, pk.ok);
 		for (int t = S0; __any(t < nch - 1); t += 8) {
 			uint4 w[8];
 #pragma unroll
 			for (int i = 0; i < 8; ++i)
-				w[i] = ldz<NT>(c0 + t + i, t + i < nch - 1);
+				w[i] = t + i < nch - 1 ? ld<NT>(c0 + t + i) : make_uint4(0, 0, 0, 0);
 			uint32_t s = 0;
 #pragma unroll
 			for (int i = 0; i < 8; ++i)
@@ -432,8 +455,8 @@ __device__ __forceinline__ uint32_t jumbo_window(const uint4 *c0, int nch, int s
 	return r;
 }
 
-template <bool DESC, bool NT, int W>
-__global__ __launch_bounds__(256, W) void slot_kernel(KParams p)
+template <bool DESC, bool NT>
+__global__ __launch_bounds__(256) void slot_kernel(KParams p)
 {
 	__shared__ uint32_t mark[4][64];
 	const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
@@ -468,7 +491,7 @@ __global__ __launch_bounds__(256, W) void slot_kernel(KParams p)
 				uint4 w[8];
 				uint32_t r = jumbo_window<NT>(c0, nch, s, w);
 				if (wbase == 0 && !raw)
-					h = header(w, q, len, p.flags, l == 0);
+					h = header<8, NT>(w, c0, nch, q, len, p.flags, l == 0);
 				const int j = (nch - 1) - 8 * s; // last chunk's position in this slot
 				const int e = q + len - 16 * (nch - 1);
 				uint32_t corr = 0;
@@ -510,20 +533,21 @@ __global__ __launch_bounds__(256, W) void slot_kernel(KParams p)
 		const int q = (int)(a0 & 15);
 		const uint4 *c0 = reinterpret_cast<const uint4 *>(a0 & ~(uint64_t)15);
 
+		// clamped, branch-free: slot tails and idle lanes re-read the
+		// packet's last chunk (or the zero chunk) and are dropped below
 		uint4 w[8];
 #pragma unroll
 		for (int i = 0; i < 8; ++i)
-			w[i] = ldz<NT>(c0 + 8 * s + i, act && 8 * s + i < nch);
+			w[i] = ldc<NT>(c0, 8 * s + i, act ? nch : 0, p.zero);
 		uint32_t r = 0;
 #pragma unroll
 		for (int i = 0; i < 8; ++i)
-			if (__any(act && 8 * s + i < nch))
-				r = sum4(w[i], r);
+			r = act && 8 * s + i < nch ? sum4(w[i], r) : r;
 
 		const bool head = act && s == 0;
 		Hdr h{};
 		if (!raw)
-			h = header(w, q, len, p.flags, head);
+			h = header<8, NT>(w, c0, nch, q, len, p.flags, head);
 
 		// edges: lead on the head lane, trail on the lane holding chunk nch-1
 		const bool dw = !__any(act && ((q | len) & 3) != 0);
@@ -561,7 +585,7 @@ __global__ __launch_bounds__(256, W) void slot_kernel(KParams p)
 // Launchers
 // --------------------------------------------------------------------------
 
-template <bool DESC, int W>
+template <bool DESC, int S0, bool CLAMP>
 static hipError_t launch_lpp_t(const KParams &p, int max_blocks, bool nt, hipStream_t st)
 {
 	uint64_t want = (p.n + 255) / 256;
@@ -569,13 +593,13 @@ static hipError_t launch_lpp_t(const KParams &p, int max_blocks, bool nt, hipStr
 	if (blocks < 1)
 		blocks = 1;
 	if (nt)
-		hipLaunchKernelGGL((lpp_kernel<DESC, true, W>), dim3(blocks), dim3(256), 0, st, p);
+		hipLaunchKernelGGL((lpp_kernel<DESC, true, S0, CLAMP>), dim3(blocks), dim3(256), 0, st, p);
 	else
-		hipLaunchKernelGGL((lpp_kernel<DESC, false, W>), dim3(blocks), dim3(256), 0, st, p);
+		hipLaunchKernelGGL((lpp_kernel<DESC, false, S0, CLAMP>), dim3(blocks), dim3(256), 0, st, p);
 	return hipGetLastError();
 }
 
-template <bool DESC, int W>
+template <bool DESC>
 static hipError_t launch_slot_t(const KParams &p, int max_blocks, bool nt, hipStream_t st)
 {
 	// each wave owns a contiguous packet range of >= ~64 packets
@@ -584,9 +608,9 @@ static hipError_t launch_slot_t(const KParams &p, int max_blocks, bool nt, hipSt
 	if (blocks < 1)
 		blocks = 1;
 	if (nt)
-		hipLaunchKernelGGL((slot_kernel<DESC, true, W>), dim3(blocks), dim3(256), 0, st, p);
+		hipLaunchKernelGGL((slot_kernel<DESC, true>), dim3(blocks), dim3(256), 0, st, p);
 	else
-		hipLaunchKernelGGL((slot_kernel<DESC, false, W>), dim3(blocks), dim3(256), 0, st, p);
+		hipLaunchKernelGGL((slot_kernel<DESC, false>), dim3(blocks), dim3(256), 0, st, p);
 	return hipGetLastError();
 }
 
@@ -609,18 +633,27 @@ hipError_t launch_lppp(const KParams &p, int num_cus, bool nt, hipStream_t st)
 	return p.desc ? launch_lppp_t<true>(p, num_cus * 8, nt, st) : launch_lppp_t<false>(p, num_cus * 8, nt, st);
 }
 
-hipError_t launch_lpp(const KParams &p, int num_cus, bool nt, bool occ, hipStream_t st)
+// shape: 0 = 4 chunks up front, clamped; 1 = 6 clamped; 2 = 6 predicated;
+// 3 = 4 predicated
+hipError_t launch_lpp(const KParams &p, int num_cus, bool nt, int shape, hipStream_t st)
 {
-	if (occ)
-		return p.desc ? launch_lpp_t<true, 8>(p, num_cus * 8, nt, st) : launch_lpp_t<false, 8>(p, num_cus * 8, nt, st);
-	return p.desc ? launch_lpp_t<true, 1>(p, num_cus * 8, nt, st) : launch_lpp_t<false, 1>(p, num_cus * 8, nt, st);
+	const int mb = num_cus * 8;
+	const bool d = p.desc != nullptr;
+	switch (shape) {
+	case 1:
+		return d ? launch_lpp_t<true, 6, true>(p, mb, nt, st) : launch_lpp_t<false, 6, true>(p, mb, nt, st);
+	case 2:
+		return d ? launch_lpp_t<true, 6, false>(p, mb, nt, st) : launch_lpp_t<false, 6, false>(p, mb, nt, st);
+	case 3:
+		return d ? launch_lpp_t<true, 4, false>(p, mb, nt, st) : launch_lpp_t<false, 4, false>(p, mb, nt, st);
+	default:
+		return d ? launch_lpp_t<true, 4, true>(p, mb, nt, st) : launch_lpp_t<false, 4, true>(p, mb, nt, st);
+	}
 }
 
-hipError_t launch_slot(const KParams &p, int num_cus, bool nt, bool occ, hipStream_t st)
+hipError_t launch_slot(const KParams &p, int num_cus, bool nt, hipStream_t st)
 {
-	if (occ)
-		return p.desc ? launch_slot_t<true, 6>(p, num_cus * 8, nt, st) : launch_slot_t<false, 6>(p, num_cus * 8, nt, st);
-	return p.desc ? launch_slot_t<true, 1>(p, num_cus * 8, nt, st) : launch_slot_t<false, 1>(p, num_cus * 8, nt, st);
+	return p.desc ? launch_slot_t<true>(p, num_cus * 8, nt, st) : launch_slot_t<false>(p, num_cus * 8, nt, st);
 }
 
 } // namespace cgck

@@ -184,9 +184,50 @@ __global__ __launch_bounds__(256) void probe_alu_kernel(const uint4 *src, uint64
 		sink[0] = acc;
 }
 
+// Factor-isolation probe for the 64 B lane-per-packet shape: 4 uint4 per
+// lane per iteration, then K dependent VALU, optionally one u32 store per
+// lane per iteration (STORE) and an LDS reservation that caps occupancy.
+template <int K, bool STORE>
+__global__ __launch_bounds__(256) void probe_iso_kernel(const uint4 *src, uint64_t n16, uint32_t *out)
+{
+	extern __shared__ uint32_t cap[]; // occupancy cap only
+	uint32_t acc = 0;
+	const uint64_t npk = n16 / 4;
+	for (uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x; k < npk; k += (uint64_t)gridDim.x * 256) {
+		uint4 w[4];
+#pragma unroll
+		for (int j = 0; j < 4; ++j)
+			w[j] = ld<false>(src + k * 4 + j);
+		uint32_t x = 0;
+#pragma unroll
+		for (int j = 0; j < 4; ++j)
+			x = sum4(w[j], x);
+#pragma unroll
+		for (int i = 0; i < K; ++i)
+			x = __builtin_amdgcn_alignbyte(x, x ^ (uint32_t)i, 1u) + (uint32_t)i;
+		if (STORE)
+			gbl(out)[k] = x;
+		acc += x;
+	}
+	if (acc == 0x12345678u)
+		cap[threadIdx.x] = acc;
+}
+
 hipError_t launch_probe_read(const void *src, uint64_t bytes, uint32_t *sink, int num_cus, int variant,
 			     hipStream_t st)
 {
+	const uint64_t n16 = bytes / 16;
+	const uint4 *sp = reinterpret_cast<const uint4 *>(src);
+	const dim3 g(num_cus * 8), b(256);
+	switch (variant) {
+	case 16: hipLaunchKernelGGL((probe_iso_kernel<0, true>), g, b, 0, st, sp, n16, sink); return hipGetLastError();
+	case 17: hipLaunchKernelGGL((probe_iso_kernel<60, false>), g, b, 0, st, sp, n16, sink); return hipGetLastError();
+	case 18: hipLaunchKernelGGL((probe_iso_kernel<0, false>), g, b, 32768, st, sp, n16, sink); return hipGetLastError();
+	case 19: hipLaunchKernelGGL((probe_iso_kernel<60, true>), g, b, 32768, st, sp, n16, sink); return hipGetLastError();
+	case 20: hipLaunchKernelGGL((probe_iso_kernel<60, true>), g, b, 0, st, sp, n16, sink); return hipGetLastError();
+	case 21: hipLaunchKernelGGL((probe_iso_kernel<0, true>), g, b, 32768, st, sp, n16, sink); return hipGetLastError();
+	default: break;
+	}
 	const uint4 *s = reinterpret_cast<const uint4 *>(src);
 	const uint64_t n = bytes / 16;
 	switch (variant) {

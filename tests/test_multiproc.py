@@ -1,0 +1,57 @@
+"""N > 1 path of bench.py on the CPU (gloo, world size 2): the batch split
+has no data-path collective; ranks own disjoint contiguous packet ranges with
+their own generator seeds, and timing is the max over ranks behind barriers
+(SURVEY §8(e))."""
+import os
+import socket
+
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import bench
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, q):
+    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port),
+                       "RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank)})
+    d = bench.Dist()
+    plan = bench.shard_plan(d.rank, d.world, 1000)
+    d.barrier()
+    m = d.max(float(rank + 1) * 0.5)   # per-rank "elapsed": max must win
+    q.put((rank, plan, m))
+    d.close()
+
+
+def test_two_rank_shard_plan_and_max():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (r0, p0, m0), (r1, p1, m1) = res
+    assert (p0["first"], p0["n"]) == (0, 1000) and (p1["first"], p1["n"]) == (1000, 1000)
+    assert p0["seed"] != p1["seed"]                      # independent shards
+    assert m0 == m1 == 1.0                               # max over ranks
+
+
+def test_single_rank_is_noop():
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        os.environ.pop(k, None)
+    d = bench.Dist()
+    assert d.world == 1 and d.max(3.0) == 3.0
+    d.barrier()
+    d.close()

@@ -24,7 +24,7 @@ for v, e in engines.items():   # family field carries the probe variant
     pass
 buf = cgck.DeviceBuffer(max(sizes))
 engines[variants[0]].synth_strided(buf.ptr, max(sizes) // 1500, 1500, 1500, 7)
-sink = cgck.DeviceBuffer(4)
+sink = cgck.DeviceBuffer(max(4, max(sizes) // 16))   # iso variants store a u32 per 64 B
 engines[variants[0]].sync()
 a, b = cgck.Event(), cgck.Event()
 res = {}
