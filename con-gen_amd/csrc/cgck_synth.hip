@@ -213,6 +213,96 @@ __global__ __launch_bounds__(256) void probe_iso_kernel(const uint4 *src, uint64
 		cap[threadIdx.x] = acc;
 }
 
+// Store-shape probes (64 B lane shape): NTS = nontemporal output stores;
+// V4 = each lane takes 4 consecutive packets over 4 iterations and writes
+// one 16-byte store; CONTIG = block-contiguous packet ranges.
+template <bool NTS, bool V4, bool CONTIG>
+__global__ __launch_bounds__(256) void probe_store_kernel(const uint4 *src, uint64_t n16, uint32_t *out)
+{
+	uint32_t acc = 0;
+	const uint64_t npk = n16 / 4;
+	const uint64_t nit = (npk + 255) / 256;
+	const Sched sc = sched(V4 ? (nit + 3) / 4 : nit, CONTIG);
+	for (uint64_t it = sc.it; it < sc.end; it += sc.step) {
+		if (V4) {
+			uint32_t x4[4];
+#pragma unroll
+			for (int j = 0; j < 4; ++j) {
+				const uint64_t k = it * 1024 + threadIdx.x * 4 + j;
+				uint4 w[4];
+#pragma unroll
+				for (int c = 0; c < 4; ++c)
+					w[c] = k < npk ? ld<false>(src + k * 4 + c) : make_uint4(0, 0, 0, 0);
+				uint32_t x = 0;
+#pragma unroll
+				for (int c = 0; c < 4; ++c)
+					x = sum4(w[c], x);
+				x4[j] = x;
+			}
+			const uint64_t k0 = it * 1024 + threadIdx.x * 4;
+			if (k0 + 3 < npk) {
+				u32x4_t v = {x4[0], x4[1], x4[2], x4[3]};
+				if (NTS)
+					__builtin_nontemporal_store(v, (CGCK_GLOBAL u32x4_t *)(out + k0));
+				else
+					*(CGCK_GLOBAL u32x4_t *)(out + k0) = v;
+			}
+			acc += x4[0];
+		} else {
+			const uint64_t k = it * 256 + threadIdx.x;
+			if (k >= npk)
+				continue;
+			uint4 w[4];
+#pragma unroll
+			for (int c = 0; c < 4; ++c)
+				w[c] = ld<false>(src + k * 4 + c);
+			uint32_t x = 0;
+#pragma unroll
+			for (int c = 0; c < 4; ++c)
+				x = sum4(w[c], x);
+			if (NTS)
+				__builtin_nontemporal_store(x, (CGCK_GLOBAL uint32_t *)(out + k));
+			else
+				gbl(out)[k] = x;
+			acc += x;
+		}
+	}
+	if (acc == 0x12345678u)
+		out[0] = acc;
+}
+
+// Delayed-store probe: iteration i's u32 is stored AFTER iteration i+1's
+// loads are issued, so the wait for those loads does not include the store's
+// acknowledgement (vmcnt retires in order).
+template <int K>
+__global__ __launch_bounds__(256) void probe_dstore_kernel(const uint4 *src, uint64_t n16, uint32_t *out)
+{
+	const uint64_t npk = n16 / 4;
+	const uint64_t stride = (uint64_t)gridDim.x * 256;
+	uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+	if (k >= npk)
+		return;
+	uint64_t kprev = k;
+	uint32_t xprev = 0;
+	for (; k < npk; k += stride) {
+		uint4 w[4];
+#pragma unroll
+		for (int c = 0; c < 4; ++c)
+			w[c] = ld<false>(src + k * 4 + c);
+		gbl(out)[kprev] = xprev;
+		uint32_t x = 0;
+#pragma unroll
+		for (int c = 0; c < 4; ++c)
+			x = sum4(w[c], x);
+#pragma unroll
+		for (int i = 0; i < K; ++i)
+			x = __builtin_amdgcn_alignbyte(x, x ^ (uint32_t)i, 1u) + (uint32_t)i;
+		kprev = k;
+		xprev = x;
+	}
+	gbl(out)[kprev] = xprev;
+}
+
 hipError_t launch_probe_read(const void *src, uint64_t bytes, uint32_t *sink, int num_cus, int variant,
 			     hipStream_t st)
 {
@@ -226,6 +316,15 @@ hipError_t launch_probe_read(const void *src, uint64_t bytes, uint32_t *sink, in
 	case 19: hipLaunchKernelGGL((probe_iso_kernel<60, true>), g, b, 32768, st, sp, n16, sink); return hipGetLastError();
 	case 20: hipLaunchKernelGGL((probe_iso_kernel<60, true>), g, b, 0, st, sp, n16, sink); return hipGetLastError();
 	case 21: hipLaunchKernelGGL((probe_iso_kernel<0, true>), g, b, 32768, st, sp, n16, sink); return hipGetLastError();
+	case 22: hipLaunchKernelGGL((probe_store_kernel<true, false, false>), g, b, 0, st, sp, n16, sink); return hipGetLastError();
+	case 23: hipLaunchKernelGGL((probe_store_kernel<false, true, false>), g, b, 0, st, sp, n16, sink); return hipGetLastError();
+	case 24: hipLaunchKernelGGL((probe_store_kernel<true, true, false>), g, b, 0, st, sp, n16, sink); return hipGetLastError();
+	case 25: hipLaunchKernelGGL((probe_store_kernel<false, false, true>), g, b, 0, st, sp, n16, sink); return hipGetLastError();
+	case 26: hipLaunchKernelGGL((probe_store_kernel<false, true, true>), g, b, 0, st, sp, n16, sink); return hipGetLastError();
+	case 27: hipLaunchKernelGGL((probe_store_kernel<true, true, true>), g, b, 0, st, sp, n16, sink); return hipGetLastError();
+	case 28: hipLaunchKernelGGL((probe_store_kernel<false, false, false>), g, b, 0, st, sp, n16, sink); return hipGetLastError();
+	case 29: hipLaunchKernelGGL((probe_dstore_kernel<0>), g, b, 0, st, sp, n16, sink); return hipGetLastError();
+	case 30: hipLaunchKernelGGL((probe_dstore_kernel<60>), g, b, 0, st, sp, n16, sink); return hipGetLastError();
 	default: break;
 	}
 	const uint4 *s = reinterpret_cast<const uint4 *>(src);

@@ -1,0 +1,118 @@
+#!/usr/bin/env python3
+"""End-to-end (host-resident) checksum rate: packets start in pinned host
+memory (the netmap/XDP ring case) and the
+two u16 results come back to host memory.
+
+Modes, per layout (dense 1500 B records, and 2048 B ring slots with the IPv4
+header at +14 as in netmap):
+  * copy  — chunked hipMemcpyAsync H2D of the packet bytes, kernel, D2H of
+            4 B/packet, two contexts (streams) alternating so copies overlap
+            kernels;
+  * zcopy — the kernel reads the pinned host buffer directly over the
+            fabric (no staging copy), outputs to device memory, D2H 4 B/pkt.
+
+Prints one JSON line; numbers go to DESIGN.md (never bench.py's value).
+"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "con-gen_amd"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+import cgck  # noqa: E402
+
+L = cgck.load()
+
+
+def host_alloc(nbytes):
+    import ctypes
+    p = ctypes.c_void_p()
+    cgck._check(L.cgck_host_alloc(nbytes, ctypes.byref(p)), "host_alloc")
+    return p.value
+
+
+def run(layout, n, chunk, reps):
+    stride, l3 = (1500, 0) if layout == "dense" else (2048, 14)
+    ln = 1500
+    nbytes = n * stride
+    e0, e1 = cgck.Engine(0), cgck.Engine(0)
+    # build the batch on the device, copy it to pinned host memory
+    dev_all = cgck.DeviceBuffer(nbytes)
+    if layout == "dense":
+        e0.synth_strided(dev_all.ptr, n, stride, ln, 0xC0C0)
+    else:
+        e0.synth_strided(dev_all.ptr, n, stride, stride - 16, 0xC0C0)
+        # (ring slots: the IPv4 datagram is the first 1500 B after +14)
+    host = host_alloc(nbytes)
+    L.cgck_memcpy(host, dev_all.ptr, nbytes, e0.stream)
+    e0.sync()
+    dev_all.free()
+    outs = np.zeros(n, np.uint32)
+    # reference: device-resident run over the same bytes for parity
+    ref_dev = cgck.DeviceBuffer(nbytes)
+    L.cgck_memcpy(ref_dev.ptr, host, nbytes, e0.stream)
+    refo = cgck.DeviceBuffer(4 * n)
+    e0.strided(ref_dev.ptr, n, stride, l3, ln, cgck.FILL_BOTH & ~cgck.STORE, refo.ptr)
+    ref = np.zeros(n, np.uint32)
+    refo.download(ref, stream=e0.stream)
+    e0.sync()
+    ref_dev.free()
+    refo.free()
+
+    res = {}
+    # --- copy mode ---
+    bufs = [cgck.DeviceBuffer(chunk * stride) for _ in range(2)]
+    obufs = [cgck.DeviceBuffer(4 * chunk) for _ in range(2)]
+    engs = [e0, e1]
+    flags = cgck.FILL_BOTH & ~cgck.STORE
+    best = None
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        for ci, k0 in enumerate(range(0, n, chunk)):
+            m = min(chunk, n - k0)
+            e, b, o = engs[ci & 1], bufs[ci & 1], obufs[ci & 1]
+            L.cgck_memcpy(b.ptr, host + k0 * stride, m * stride, e.stream)
+            e.strided(b.ptr, m, stride, l3, ln, flags, o.ptr)
+            L.cgck_memcpy(outs.ctypes.data + 4 * k0, o.ptr, 4 * m, e.stream)
+        e0.sync()
+        e1.sync()
+        dt = time.perf_counter() - t0
+        best = dt if best is None else min(best, dt)
+    ok = bool(np.array_equal(outs, ref))
+    res["copy"] = {"mpkt_s": n / best / 1e6, "wire_gb_s": n * ln / best / 1e9,
+                   "h2d_gb_s": nbytes / best / 1e9, "parity": ok}
+    # --- zero-copy mode: kernel reads pinned host memory directly ---
+    outs[:] = 0
+    o = cgck.DeviceBuffer(4 * n)
+    best = None
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        e0.strided(host, n, stride, l3, ln, flags, o.ptr)
+        o.download(outs, stream=e0.stream)
+        e0.sync()
+        dt = time.perf_counter() - t0
+        best = dt if best is None else min(best, dt)
+    res["zcopy"] = {"mpkt_s": n / best / 1e6, "wire_gb_s": n * ln / best / 1e9,
+                    "parity": bool(np.array_equal(outs, ref))}
+    for b in bufs + obufs + [o]:
+        b.free()
+    L.cgck_host_free(host)
+    return res
+
+
+def main():
+    n = int(os.environ.get("E2E_PACKETS", 1 << 20))
+    chunk = int(os.environ.get("E2E_CHUNK", 1 << 16))
+    out = {"packets": n, "chunk": chunk}
+    for layout in ("dense", "ring2048"):
+        out[layout] = run(layout, n, chunk, 3)
+        print(layout, out[layout], flush=True)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
