@@ -191,9 +191,15 @@ __device__ __forceinline__ uint4 pick8(const uint4 (&w)[8], int j)
 	return r;
 }
 
+// One packet's outputs: the u32 (ip | l4 << 16) and the verdict byte.
+struct Res {
+	uint32_t out, verdict;
+};
+
 // Finish one packet: T = folded sum over [ip, ip+len) in the ABSOLUTE frame.
-__device__ __forceinline__ void finish(const KParams &p, uint64_t k, uint64_t a0, int len, uint32_t T,
-				       const Hdr &h)
+// In-place field stores (CGCK_STORE) and the bad counters happen here; the
+// per-packet outputs are returned for the caller to emit (or stage).
+__device__ __forceinline__ Res result(const KParams &p, uint64_t a0, int len, uint32_t T, const Hdr &h)
 {
 	const uint32_t flags = p.flags;
 	if (a0 & 1)
@@ -244,16 +250,81 @@ __device__ __forceinline__ void finish(const KParams &p, uint64_t k, uint64_t a0
 				store16(ipp + hl + h.fo, hi);
 		}
 	}
-	if (p.out)
-		gbl(p.out)[k] = lo | (hi << 16);
-	if (p.verdict)
-		gbl(p.verdict)[k] = (uint8_t)verdict;
 	if (p.bad) {
 		if (verdict & CGCK_BAD_IP)
 			atomicAdd(p.bad + 0, 1u);
 		if (verdict & CGCK_BAD_L4)
 			atomicAdd(p.bad + 1, 1u);
 	}
+	return Res{lo | (hi << 16), verdict};
+}
+
+__device__ __forceinline__ void emit(const KParams &p, uint64_t k, const Res &r)
+{
+	if (p.out)
+		gbl(p.out)[k] = r.out;
+	if (p.verdict)
+		gbl(p.verdict)[k] = (uint8_t)r.verdict;
+}
+
+__device__ __forceinline__ void finish(const KParams &p, uint64_t k, uint64_t a0, int len, uint32_t T,
+				       const Hdr &h)
+{
+	emit(p, k, result(p, a0, len, T, h));
+}
+
+// --------------------------------------------------------------------------
+// Output staging
+// --------------------------------------------------------------------------
+//
+// On gfx9 vmcnt counts stores as well as loads and retires in order, so a
+// per-iteration output store makes the NEXT iteration's wait for its loads
+// also wait for that store's write acknowledgement — measured at -20% of
+// the stream rate on 64 B packets and IMIX for ~1% of the bytes.  Outputs
+// of the slot kernels (scattered head-lane stores, ~20 per iteration) are
+// therefore staged in LDS and written in coalesced bursts: one exposed store
+// latency per window instead of per iteration.  (For grid-stride lane per
+// packet, whose stores are already coalesced, a burst of 8 measured worse
+// than one store per iteration: 58.5% vs 65.5% of HBM peak on 64 B.)
+
+// Lane per slot: a window of kWaveStage consecutive packets of the wave's
+// range [sb, sb + kWaveStage), written by head lanes, flushed by all lanes.
+constexpr int kWaveStage = 256;
+
+struct WaveStage {
+	uint32_t *so;
+	uint8_t *sv;
+	uint64_t sb;
+};
+
+__device__ __forceinline__ void wave_stage_flush(const KParams &p, WaveStage &s, uint64_t e)
+{
+	const int l = threadIdx.x & 63;
+	__builtin_amdgcn_wave_barrier();
+	asm volatile("" ::: "memory");
+	const int c = (int)(e - s.sb);
+	for (int i = l; i < c; i += 64) {
+		if (p.out)
+			gbl(p.out)[s.sb + i] = s.so[i];
+		if (p.verdict)
+			gbl(p.verdict)[s.sb + i] = s.sv[i];
+	}
+	__builtin_amdgcn_wave_barrier();
+	asm volatile("" ::: "memory");
+	s.sb = e;
+}
+
+// make room for packets [cur, cur + m)
+__device__ __forceinline__ void wave_stage_reserve(const KParams &p, WaveStage &s, uint64_t cur, int m)
+{
+	if (cur + m > s.sb + kWaveStage)
+		wave_stage_flush(p, s, cur);
+}
+
+__device__ __forceinline__ void wave_stage_put(WaveStage &s, uint64_t k, const Res &r)
+{
+	s.so[k - s.sb] = r.out;
+	s.sv[k - s.sb] = (uint8_t)r.verdict;
 }
 
 __device__ __forceinline__ int nchunks(uint64_t a0, uint32_t len)
@@ -459,13 +530,16 @@ template <bool DESC, bool NT>
 __global__ __launch_bounds__(256) void slot_kernel(KParams p)
 {
 	__shared__ uint32_t mark[4][64];
-	const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
+	__shared__ uint32_t so[4][kWaveStage];
+	__shared__ uint8_t sv[4][kWaveStage];
+	const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63; // wave-uniform (SGPR)
 	const bool raw = p.flags & CGCK_RAW;
 	const uint64_t nwaves = (uint64_t)gridDim.x * 4;
 	const uint64_t wid = (uint64_t)blockIdx.x * 4 + wv;
 	const uint64_t per = (p.n + nwaves - 1) / nwaves;
 	const uint64_t r0 = wid * per;
 	const uint64_t r1 = r0 + per < p.n ? r0 + per : p.n;
+	WaveStage ws{so[wv], sv[wv], r0};
 
 	for (uint64_t cur = r0; cur < r1;) {
 		// -- this iteration's packets and their slots --
@@ -502,8 +576,9 @@ __global__ __launch_bounds__(256) void slot_kernel(KParams p)
 				r = fold16(r) + (0xffffu - fold16(corr));
 				acc = fold16(acc) + fold16(gsum<64>(r));
 			}
+			wave_stage_reserve(p, ws, cur, 1);
 			if (l == 0)
-				finish(p, cur, a0, len, fold16(acc), h);
+				wave_stage_put(ws, cur, result(p, a0, len, fold16(acc), h));
 			cur += 1;
 			continue;
 		}
@@ -575,10 +650,290 @@ __global__ __launch_bounds__(256) void slot_kernel(KParams p)
 			if (l + d < send)
 				r += y;
 		}
+		wave_stage_reserve(p, ws, cur, m);
 		if (head)
-			finish(p, cur + owner, a0, len, fold16(r), h);
+			wave_stage_put(ws, cur + owner, result(p, a0, len, fold16(r), h));
 		cur += m;
 	}
+	if (r0 < r1)
+		wave_stage_flush(p, ws, r1);
+}
+
+// --------------------------------------------------------------------------
+// Lane per 128-byte slot, software-pipelined two deep
+// --------------------------------------------------------------------------
+//
+// Same slot mapping as slot_kernel, but a wave keeps TWO iterations of chunk
+// loads in flight: while iteration i is reduced, the chunks of i+1 are
+// loading and the descriptors of i+2 too.  In-order vmcnt retirement shapes
+// the issue order of each phase:
+//
+//   map(i+1) [waits only for desc(i+1), issued before chunks(i)]
+//   issue desc(i+2); issue chunks(i+1)
+//   reduce(i) [waits for chunks(i): desc(i+2) + chunks(i+1) stay in flight]
+//
+// The A/B buffers are explicit (the loop body is unrolled twice) so no
+// register holding an in-flight load is ever copied — a copy would force a
+// vmcnt(0) at the back edge.  Every load is branch-free (clamped to the
+// packet's chunks or the context's zero chunk) so vmcnt counting stays exact.
+
+struct DescW {
+	uint32_t lo, hi, w2;
+};
+
+// descriptor words of packet k (k past the wave's range reads packet 0)
+template <bool DESC>
+__device__ __forceinline__ DescW load_desc(const KParams &p, uint64_t k, uint64_t r1)
+{
+	DescW d{0, 0, 0};
+	if (DESC) {
+		const CGCK_GLOBAL uint32_t *q = (const CGCK_GLOBAL uint32_t *)p.desc + 3 * (k < r1 ? k : 0);
+		d.lo = q[0];
+		d.hi = q[1];
+		d.w2 = q[2];
+	}
+	return d;
+}
+
+template <bool DESC>
+__device__ __forceinline__ Pkt decode(const KParams &p, uint64_t k, uint64_t r1, const DescW &d)
+{
+	Pkt r;
+	r.ok = k < r1;
+	if (DESC) {
+		r.a0 = reinterpret_cast<uint64_t>(p.base) + (((uint64_t)d.hi << 32) | d.lo) + (d.w2 & 0xffffu);
+		r.len = d.w2 >> 16;
+	} else {
+		r.a0 = reinterpret_cast<uint64_t>(p.base) + (r.ok ? k : 0) * p.stride + p.l3_off;
+		r.len = p.ip_len;
+	}
+	if (!r.ok)
+		r.len = 0;
+	return r;
+}
+
+// inclusive prefix sum over the wave in DPP (row shifts, then the row
+// broadcasts of lanes 15 and 31); no LDS round trips
+__device__ __forceinline__ uint32_t wave_scan_dpp(uint32_t x)
+{
+	x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false); // row_shr:1
+	x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false); // row_shr:2
+	x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false); // row_shr:4
+	x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false); // row_shr:8
+	x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false); // row_bcast:15
+	x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false); // row_bcast:31
+	return x;
+}
+
+// One iteration's lane -> (packet, slot) mapping.
+struct SMap {
+	uint64_t a0;   // owner packet's IPv4 header (jumbo: lane 0's packet)
+	int len, nch;  // owner packet
+	int s;         // slot index inside the owner packet
+	int st, ns;    // owner's first slot (lane) and slot count
+	int owner;     // owner's packet index relative to the iteration
+	int m;         // packets placed this iteration (0: jumbo or empty)
+	bool act;      // lane holds a slot
+};
+
+template <bool DESC>
+__device__ __forceinline__ SMap smap(const KParams &p, uint64_t cur, uint64_t r1, const DescW &d,
+				     uint32_t (&mark)[64])
+{
+	const int l = threadIdx.x & 63;
+	const Pkt pk = decode<DESC>(p, cur + l, r1, d);
+	const int nch_l = nchunks(pk.a0, pk.len);
+	const uint32_t ns = pk.ok ? (uint32_t)max(1, (nch_l + 7) >> 3) : 0u;
+	const uint32_t P = wave_scan_dpp(ns);
+	const uint64_t fit = __ballot(pk.ok && P <= 64);
+	SMap M;
+	M.m = __popcll(fit);
+	const int T = M.m ? (int)__builtin_amdgcn_readlane(P, M.m - 1) : 0; // slots in use
+	mark[l] = 0;
+	__builtin_amdgcn_wave_barrier();
+	asm volatile("" ::: "memory");
+	if (l < M.m)
+		mark[P - ns] = 1;
+	__builtin_amdgcn_wave_barrier();
+	asm volatile("" ::: "memory");
+	const uint64_t heads = __ballot(mark[l] != 0 && l < T);
+	const uint64_t le = l == 63 ? ~0ull : ((2ull << l) - 1);
+	const uint64_t below = heads & le, above = heads & ~le;
+	M.act = l < T;
+	M.owner = below ? __popcll(below) - 1 : 0;
+	M.st = below ? 63 - __clzll(below) : 0;
+	M.ns = (above ? __ffsll((long long)above) - 1 : T) - M.st;
+	M.s = l - M.st;
+	M.a0 = shfl64(pk.a0, M.owner);
+	M.len = __shfl((int)pk.len, M.owner, 64);
+	M.nch = nchunks(M.a0, (uint32_t)M.len);
+	return M;
+}
+
+template <bool NT>
+__device__ __forceinline__ void slot_issue(const KParams &p, const SMap &M, uint4 (&w)[8])
+{
+	const uint4 *c0 = reinterpret_cast<const uint4 *>(M.a0 & ~(uint64_t)15);
+#pragma unroll
+	for (int i = 0; i < 8; ++i)
+		w[i] = ldc<NT>(c0, 8 * M.s + i, M.act ? M.nch : 0, p.zero);
+}
+
+template <bool NT>
+__device__ __forceinline__ void slot_reduce(const KParams &p, uint64_t cur, const SMap &M, const uint4 (&w)[8],
+					    WaveStage &ws)
+{
+	const int l = threadIdx.x & 63;
+	const bool raw = p.flags & CGCK_RAW;
+	const uint64_t a0 = M.a0;
+	const int len = M.len, nch = M.nch, s = M.s;
+	const int q = (int)(a0 & 15);
+	const uint4 *c0 = reinterpret_cast<const uint4 *>(a0 & ~(uint64_t)15);
+	// All of w[] counts as consumed here, on every path: a chunk whose use
+	// sits in a skippable branch (or the jumbo path, which ignores w[]) would
+	// leave its load "maybe pending" and degrade later waits to vmcnt(0).
+#pragma unroll
+	for (int i = 0; i < 8; ++i)
+		asm volatile("" ::"v"(w[i].x), "v"(w[i].y), "v"(w[i].z), "v"(w[i].w));
+	if (M.m == 0) {
+		// jumbo packet (> 64 slots): windows of 64 slots, whole-wave sums
+		const int nsj = (nch + 7) >> 3;
+		uint32_t acc = 0;
+		Hdr h{};
+		for (int wbase = 0; wbase < nsj; wbase += 64) {
+			const int sj = wbase + l;
+			uint4 v[8];
+			uint32_t r = jumbo_window<NT>(c0, nch, sj, v);
+			if (wbase == 0 && !raw)
+				h = header<8, NT>(v, c0, nch, q, len, p.flags, l == 0);
+			const int j = (nch - 1) - 8 * sj;
+			const int e = q + len - 16 * (nch - 1);
+			uint32_t corr = 0;
+			if (sj == 0 && q != 0)
+				corr += lead_sum(v[0], q, false);
+			if (j >= 0 && j < 8 && e != 16)
+				corr += trail_sum(pick8(v, j), e, false);
+			r = fold16(r) + (0xffffu - fold16(corr));
+			acc = fold16(acc) + fold16(gsum<64>(r));
+		}
+		wave_stage_reserve(p, ws, cur, 1);
+		if (l == 0)
+			wave_stage_put(ws, cur, result(p, a0, len, fold16(acc), h));
+		// drain this rare path completely so the wait state merged after it
+		// holds no "maybe pending" loads (they would cost a vmcnt(0) later)
+		__builtin_amdgcn_s_waitcnt(0);
+		return;
+	}
+	const bool act = M.act;
+	uint32_t r = 0;
+#pragma unroll
+	for (int i = 0; i < 8; ++i)
+		r = act && 8 * s + i < nch ? sum4(w[i], r) : r;
+	const bool head = act && s == 0;
+	Hdr h{};
+	if (!raw)
+		h = header<8, NT>(w, c0, nch, q, len, p.flags, head);
+	const bool dw = !__any(act && ((q | len) & 3) != 0);
+	uint32_t corr = 0;
+	if (__any(head && q != 0))
+		corr = head && q != 0 ? lead_sum(w[0], q, dw) : 0u;
+	const int j = (nch - 1) - 8 * s;
+	const int e = q + len - 16 * (nch - 1);
+	const bool tail = act && nch > 0 && j >= 0 && j < 8 && e != 16;
+	if (__any(tail))
+		corr += tail ? trail_sum(pick8(w, j), e, dw) : 0u;
+	r = fold16(r) + (0xffffu - fold16(corr));
+	// segmented suffix sum towards the head lane
+	uint32_t nso = 0; // wave-uniform bound on segment length (OR >= max)
+#pragma unroll
+	for (int b = 0; b < 7; ++b)
+		nso |= __any(act && ((M.ns >> b) & 1)) ? (1u << b) : 0u;
+	const int send = M.st + M.ns;
+#pragma unroll
+	for (int d = 1; d < 64; d <<= 1) {
+		if ((uint32_t)d >= nso)
+			break;
+		const uint32_t y = __shfl_down(r, d, 64);
+		if (l + d < send)
+			r += y;
+	}
+	wave_stage_reserve(p, ws, cur, M.m);
+	if (head)
+		wave_stage_put(ws, cur + M.owner, result(p, a0, len, fold16(r), h));
+}
+
+// DEPTH 1: one chunk buffer, only the descriptors of the next iteration are
+// prefetched (keeps the VGPR budget of slot_kernel: 4 waves per SIMD).
+template <bool DESC, bool NT>
+__device__ __forceinline__ void slot_loop1(const KParams &p, uint64_t r0, uint64_t r1, uint32_t (&mark)[64],
+					   WaveStage &ws)
+{
+	const int l = threadIdx.x & 63;
+	uint64_t cur = r0;
+	DescW d = load_desc<DESC>(p, cur + l, r1);
+	for (;;) {
+		const SMap M = smap<DESC>(p, cur, r1, d, mark);
+		const uint64_t nxt = cur + (M.m ? M.m : 1);
+		d = load_desc<DESC>(p, nxt + l, r1);
+		uint4 w[8];
+		slot_issue<NT>(p, M, w);
+		slot_reduce<NT>(p, cur, M, w, ws);
+		if (nxt >= r1)
+			break;
+		cur = nxt;
+	}
+}
+
+template <bool DESC, bool NT, int DEPTH, int WPE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void slot2_kernel(KParams p)
+{
+	__shared__ uint32_t mark[4][64];
+	__shared__ uint32_t so[4][kWaveStage];
+	__shared__ uint8_t sv[4][kWaveStage];
+	const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63; // wave-uniform (SGPR)
+	const uint64_t nwaves = (uint64_t)gridDim.x * 4;
+	const uint64_t wid = (uint64_t)blockIdx.x * 4 + wv;
+	const uint64_t per = (p.n + nwaves - 1) / nwaves;
+	const uint64_t r0 = wid * per;
+	const uint64_t r1 = r0 + per < p.n ? r0 + per : p.n;
+	if (r0 >= r1)
+		return;
+	WaveStage ws{so[wv], sv[wv], r0};
+	if (DEPTH == 1) {
+		slot_loop1<DESC, NT>(p, r0, r1, mark[wv], ws);
+		wave_stage_flush(p, ws, r1);
+		return;
+	}
+
+	// prologue: map A, desc of B, chunks of A
+	uint64_t curA = r0;
+	SMap mA = smap<DESC>(p, curA, r1, load_desc<DESC>(p, curA + l, r1), mark[wv]);
+	uint64_t curB = curA + (mA.m ? mA.m : 1);
+	DescW dB = load_desc<DESC>(p, curB + l, r1);
+	uint4 wA[8], wB[8];
+	slot_issue<NT>(p, mA, wA);
+	for (;;) {
+		// phase A: map B, prefetch desc C, issue chunks B, reduce A
+		const SMap mB = smap<DESC>(p, curB, r1, dB, mark[wv]);
+		const uint64_t curC = curB + (mB.m ? mB.m : 1);
+		const DescW dC = load_desc<DESC>(p, curC + l, r1);
+		slot_issue<NT>(p, mB, wB);
+		slot_reduce<NT>(p, curA, mA, wA, ws);
+		if (curB >= r1)
+			break;
+		// phase B: map C, prefetch desc D, issue chunks C (into A), reduce B
+		const SMap mC = smap<DESC>(p, curC, r1, dC, mark[wv]);
+		const uint64_t curD = curC + (mC.m ? mC.m : 1);
+		dB = load_desc<DESC>(p, curD + l, r1);
+		slot_issue<NT>(p, mC, wA);
+		slot_reduce<NT>(p, curB, mB, wB, ws);
+		if (curC >= r1)
+			break;
+		curA = curC;
+		mA = mC;
+		curB = curD;
+	}
+	wave_stage_flush(p, ws, r1);
 }
 
 // --------------------------------------------------------------------------
@@ -648,6 +1003,36 @@ hipError_t launch_lpp(const KParams &p, int num_cus, bool nt, int shape, hipStre
 		return d ? launch_lpp_t<true, 4, false>(p, mb, nt, st) : launch_lpp_t<false, 4, false>(p, mb, nt, st);
 	default:
 		return d ? launch_lpp_t<true, 4, true>(p, mb, nt, st) : launch_lpp_t<false, 4, true>(p, mb, nt, st);
+	}
+}
+
+template <bool DESC, int DEPTH, int WPE>
+static hipError_t launch_slot2_t(const KParams &p, int max_blocks, bool nt, hipStream_t st)
+{
+	uint64_t want = (p.n + 4 * 64 - 1) / (4 * 64);
+	int blocks = (int)(want < (uint64_t)max_blocks ? want : (uint64_t)max_blocks);
+	if (blocks < 1)
+		blocks = 1;
+	if (nt)
+		hipLaunchKernelGGL((slot2_kernel<DESC, true, DEPTH, WPE>), dim3(blocks), dim3(256), 0, st, p);
+	else
+		hipLaunchKernelGGL((slot2_kernel<DESC, false, DEPTH, WPE>), dim3(blocks), dim3(256), 0, st, p);
+	return hipGetLastError();
+}
+
+// depth 1: descriptor prefetch only; depth 2: chunks of the next iteration too
+hipError_t launch_slot2(const KParams &p, int num_cus, int depth, bool nt, hipStream_t st)
+{
+	const int mb = num_cus * 8;
+	switch (depth) {
+	case 1:
+		return p.desc ? launch_slot2_t<true, 1, 1>(p, mb, nt, st) : launch_slot2_t<false, 1, 1>(p, mb, nt, st);
+	case 3: // depth 2, >= 3 waves per SIMD
+		return p.desc ? launch_slot2_t<true, 2, 3>(p, mb, nt, st) : launch_slot2_t<false, 2, 3>(p, mb, nt, st);
+	case 4: // depth 2, >= 4 waves per SIMD
+		return p.desc ? launch_slot2_t<true, 2, 4>(p, mb, nt, st) : launch_slot2_t<false, 2, 4>(p, mb, nt, st);
+	default:
+		return p.desc ? launch_slot2_t<true, 2, 1>(p, mb, nt, st) : launch_slot2_t<false, 2, 1>(p, mb, nt, st);
 	}
 }
 

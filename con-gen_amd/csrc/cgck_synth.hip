@@ -303,6 +303,55 @@ __global__ __launch_bounds__(256) void probe_dstore_kernel(const uint4 *src, uin
 	gbl(out)[kprev] = xprev;
 }
 
+// Wave-contiguous 64-B-per-lane reads, 4 x 64 packets per wave step (16
+// loads in flight per lane).  MODE 0: u32 store per packet; 1: results
+// transposed through LDS, one 16-B store per lane per step; 2: u32 store for
+// a quarter of the packets (a quarter of the bytes); 3: no store.
+template <int MODE>
+__global__ __launch_bounds__(256) void probe_wave4_kernel(const uint4 *src, uint64_t n16, uint32_t *out)
+{
+	__shared__ uint32_t lds[4][256];
+	const uint64_t npk = n16 / 4;
+	const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+	const uint64_t nw = (uint64_t)gridDim.x * 4;
+	for (uint64_t base = ((uint64_t)blockIdx.x * 4 + wid) * 256; base + 256 <= npk; base += nw * 256) {
+		uint4 w[4][4];
+#pragma unroll
+		for (int j = 0; j < 4; ++j)
+#pragma unroll
+			for (int c = 0; c < 4; ++c)
+				w[j][c] = ld<false>(src + (base + j * 64 + lane) * 4 + c);
+		uint32_t r[4];
+#pragma unroll
+		for (int j = 0; j < 4; ++j) {
+			uint32_t x = 0;
+#pragma unroll
+			for (int c = 0; c < 4; ++c)
+				x = sum4(w[j][c], x);
+			r[j] = x;
+		}
+		if (MODE == 0) {
+#pragma unroll
+			for (int j = 0; j < 4; ++j)
+				gbl(out)[base + j * 64 + lane] = r[j];
+		} else if (MODE == 1) {
+#pragma unroll
+			for (int j = 0; j < 4; ++j)
+				lds[wid][j * 64 + lane] = r[j];
+			__builtin_amdgcn_wave_barrier();
+			const u32x4_t v = *reinterpret_cast<const u32x4_t *>(&lds[wid][4 * lane]);
+			__builtin_amdgcn_wave_barrier();
+			*(CGCK_GLOBAL u32x4_t *)(gbl(out) + base + 4 * lane) = v;
+		} else if (MODE == 2) {
+			gbl(out)[base / 4 + lane] = r[0] + r[1] + r[2] + r[3];
+		} else {
+			const uint32_t x = r[0] + r[1] + r[2] + r[3];
+			if (x == 0x12345678u)
+				gbl(out)[lane] = x;
+		}
+	}
+}
+
 hipError_t launch_probe_read(const void *src, uint64_t bytes, uint32_t *sink, int num_cus, int variant,
 			     hipStream_t st)
 {
@@ -325,6 +374,10 @@ hipError_t launch_probe_read(const void *src, uint64_t bytes, uint32_t *sink, in
 	case 28: hipLaunchKernelGGL((probe_store_kernel<false, false, false>), g, b, 0, st, sp, n16, sink); return hipGetLastError();
 	case 29: hipLaunchKernelGGL((probe_dstore_kernel<0>), g, b, 0, st, sp, n16, sink); return hipGetLastError();
 	case 30: hipLaunchKernelGGL((probe_dstore_kernel<60>), g, b, 0, st, sp, n16, sink); return hipGetLastError();
+	case 31: hipLaunchKernelGGL((probe_wave4_kernel<0>), g, b, 0, st, sp, n16, sink); return hipGetLastError();
+	case 32: hipLaunchKernelGGL((probe_wave4_kernel<1>), g, b, 0, st, sp, n16, sink); return hipGetLastError();
+	case 33: hipLaunchKernelGGL((probe_wave4_kernel<2>), g, b, 0, st, sp, n16, sink); return hipGetLastError();
+	case 34: hipLaunchKernelGGL((probe_wave4_kernel<3>), g, b, 0, st, sp, n16, sink); return hipGetLastError();
 	default: break;
 	}
 	const uint4 *s = reinterpret_cast<const uint4 *>(src);

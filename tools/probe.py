@@ -42,4 +42,4 @@ for r in range(6):
                 res.setdefault((sz, v), []).append(ms)
 for (sz, v), xs in sorted(res.items()):
     ms = statistics.median(xs)
-    print(f"{sz >> 20:6d} MB variant {v}: {ms * 1e3:9.1f} us  {sz / ms / 1e9:8.1f} GB/s")
+    print(f"{sz >> 20:6d} MB variant {v}: {ms * 1e3:9.1f} us  {sz / ms / 1e9:8.2f} TB/s")

@@ -28,10 +28,13 @@ def main():
     ap.add_argument("--launches", type=int, default=10)
     ap.add_argument("--variants", default="group,lpp")
     ap.add_argument("--workloads", default="1500,64,imix")
-    ap.add_argument("--flags", default="GEN_BOTH")
+    ap.add_argument("--flags", default="GEN_BOTH",
+                    help="comma list of cgck flag names; each is a separate cell")
+    ap.add_argument("--outs", default="out", help="comma list of out (u32 per packet) | none")
     args = ap.parse_args()
     n = args.packets
-    flags = getattr(cgck, args.flags)
+    flag_list = args.flags.split(",")
+    out_list = args.outs.split(",")
     engines = {}
     for v in args.variants.split(","):
         os.environ["CGCK_KERNEL"] = v
@@ -45,34 +48,41 @@ def main():
             buf = cgck.DeviceBuffer(nbytes)
             desc = cgck.DeviceBuffer(12 * n)
             e0.synth_imix(buf.ptr, desc.ptr, n, 0xC0C0)
-            algo = nbytes + 16 * n
+            algo = nbytes + 12 * n + (4 * n if "out" in out_list else 0)
             for e in engines.values():
                 e.set_desc_len_hint(nbytes // n)
-            work[w] = (lambda e, buf=buf, desc=desc: e.desc(buf.ptr, desc.ptr, n, flags, out.ptr), algo,
+            work[w] = (lambda e, f, o, buf=buf, desc=desc: e.desc(buf.ptr, desc.ptr, n, f, o), algo,
                        [buf, desc])
         else:
             L = int(w)
             buf = cgck.DeviceBuffer(n * L)
             e0.synth_strided(buf.ptr, n, L, L, 0xC0C0)
-            work[w] = (lambda e, buf=buf, L=L: e.strided(buf.ptr, n, L, 0, L, flags, out.ptr),
-                       n * (L + 4), [buf])
+            work[w] = (lambda e, f, o, buf=buf, L=L: e.strided(buf.ptr, n, L, 0, L, f, o),
+                       n * L + (4 * n if "out" in out_list else 0), [buf])
     out = cgck.DeviceBuffer(4 * n)
     # streaming-read ceiling on the 1500 B buffer (or the first one)
     pb = work.get("1500", next(iter(work.values())))[2][0]
     sink = cgck.DeviceBuffer(4)
-    work["probe"] = (lambda e, pb=pb: e.probe_read(pb.ptr, pb.nbytes, sink.ptr), pb.nbytes, [pb])
+    work["probe"] = (lambda e, f, o, pb=pb: e.probe_read(pb.ptr, pb.nbytes, sink.ptr), pb.nbytes, [pb])
     e0.sync()
-    res = {(w, v): [] for w in work for v in engines if w != "probe" or v == next(iter(engines))}
+    cells = {}
+    for v, e in engines.items():
+        for fl in flag_list:
+            for o in out_list:
+                tag = v if (len(flag_list) == 1 and len(out_list) == 1) else f"{v}:{fl}:{o}"
+                cells[tag] = (e, getattr(cgck, fl), out.ptr if o == "out" else 0)
+    first = next(iter(cells))
+    res = {(w, v): [] for w in work for v in cells if w != "probe" or v == first}
     a, b = cgck.Event(), cgck.Event()
     for r in range(args.rounds + 1):
         for w, (fn, algo, _) in work.items():
-            for v, e in engines.items():
+            for v, (e, fl, o) in cells.items():
                 if (w, v) not in res:
                     continue
-                fn(e)  # warm
+                fn(e, fl, o)  # warm
                 e.record(a)
                 for _ in range(args.launches):
-                    fn(e)
+                    fn(e, fl, o)
                 e.record(b)
                 ms = cgck.Engine.elapsed_ms(a, b) / args.launches
                 if r > 0:
@@ -82,7 +92,7 @@ def main():
         med, best = statistics.median(xs), max(xs)
         table[f"{w}/{v}"] = {"median_GBs": med / 1e9, "best_GBs": best / 1e9,
                              "median_frac": med / HBM}
-        print(f"{w:>5} {v:>6}: median {med / 1e9:8.1f} GB/s ({med / HBM:6.1%})  best {best / 1e9:8.1f}",
+        print(f"{w:>5} {v:>22}: median {med / 1e9:8.1f} GB/s ({med / HBM:6.1%})  best {best / 1e9:8.1f}",
               flush=True)
     print(json.dumps(table))
 
