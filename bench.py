@@ -169,7 +169,8 @@ def cpu_baseline(seconds):
     finally:
         os.sched_setaffinity(0, old)
     rate = n * reps / sec
-    allc = min(len(cpus), 64)
+    # the box's CPU share for one GPU (OMP_NUM_THREADS is 16 there)
+    allc = min(len(cpus), int(os.environ.get("OMP_NUM_THREADS", "16") or 16), 16)
     sec_all, _ = P.cpu_bench(fin, fudp, buf, n, 1500, 1500, threads=allc, reps=max(1, reps // 4))
     rate_all = n * max(1, reps // 4) / sec_all
     return {

@@ -28,7 +28,7 @@ hipError_t launch_cksum(const KParams &p0, uint32_t len_hint, int num_cus, int k
 	const bool lane_ok = !(p.flags & kFlagNoLenCheck);
 	int variant = kernel & 15;
 	if (variant == 0)
-		variant = !lane_ok ? 1 : len_hint >= kGroupFromLen ? 1 : len_hint <= kLppUpToLen ? 2 : 3;
+		variant = !lane_ok ? 1 : len_hint >= kGroupFromLen ? 1 : len_hint <= kLppUpToLen ? 2 : 9;
 	if (variant >= 2 && !lane_ok)
 		variant = 1;
 	bool nt, contig;

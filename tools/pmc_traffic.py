@@ -14,10 +14,13 @@ import sys
 
 KERNELS = {
     "1500": "cksum_kernel<16, 6, 1, false, true>",
-    "64": "lpp_kernel<false, 1, 6, false>",
-    "imix": "lpp_kernel<true, 1, 6, false>",
+    "64": "lpp_kernel<false, false, 6, false>",
+    "imix": "slot2_kernel<true, false, 2, 1>",
 }
-ALGO = {"1500": (16 << 20) * 1504, "64": (16 << 20) * 68, "imix": None}
+# bench.py's batches: 16M packets; reads + 12 B descriptor (IMIX) + 4 B output
+N = 16 << 20
+IMIX_BYTES = 5944726220   # cgck_imix_bytes(16M)
+ALGO = {"1500": N * 1504, "64": N * 68, "imix": IMIX_BYTES + 16 * N}
 
 
 def per_kernel(path, counter):
