@@ -7,7 +7,7 @@ hipError_t launch_group(const KParams &p, uint32_t max_len, int num_cus, bool nt
 hipError_t launch_lpp(const KParams &p, int num_cus, bool nt, int shape, hipStream_t st);
 hipError_t launch_slot(const KParams &p, int num_cus, bool nt, hipStream_t st);
 hipError_t launch_lppp(const KParams &p, int num_cus, bool nt, hipStream_t st);
-hipError_t launch_slot2(const KParams &p, int num_cus, int depth, bool nt, hipStream_t st);
+hipError_t launch_slot2(const KParams &p, int num_cus, bool nt, hipStream_t st);
 
 // `kernel` = variant | flags (include/cgck.h is agnostic of this; $CGCK_KERNEL
 // overrides it for A/B runs):
@@ -15,8 +15,7 @@ hipError_t launch_slot2(const KParams &p, int num_cus, int depth, bool nt, hipSt
 //     packet, 3 lane per 128-byte slot, 4 software-pipelined lane per packet,
 //     5..8 lane per packet shapes 1..3, 0 (6 clamped, 6 predicated,
 //     4 predicated, 4 clamped chunks up front), 9 lane per 128-byte slot
-//     pipelined two deep, 10 lane per slot with descriptor prefetch,
-//     11/12 = 9 held to >= 3/4 waves per SIMD;
+//     pipelined two deep (the default for mid-size packets);
 //   kNT (bit 4) nontemporal loads, kContig (bit 5) contiguous block ranges,
 //   kExplicit (bit 6) take bits 4-5 as given instead of the measured defaults.
 // len_hint = the batch's packet length (strided) or typical length (descriptors).
@@ -59,13 +58,7 @@ hipError_t launch_cksum(const KParams &p0, uint32_t len_hint, int num_cus, int k
 	case 4:
 		return launch_lppp(p, num_cus, nt, st);
 	case 9:
-		return launch_slot2(p, num_cus, 2, nt, st);
-	case 10:
-		return launch_slot2(p, num_cus, 1, nt, st);
-	case 11:
-		return launch_slot2(p, num_cus, 3, nt, st);
-	case 12:
-		return launch_slot2(p, num_cus, 4, nt, st);
+		return launch_slot2(p, num_cus, nt, st);
 	default:
 		return launch_group(p, len_hint, num_cus, nt, st);
 	}

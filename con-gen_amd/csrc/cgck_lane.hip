@@ -25,6 +25,8 @@
 //    pseudo-header, reduce() (subr.c:137-156), verdicts, stores, outputs.
 #include "cgck_device.h"
 
+#include <stdlib.h>
+
 namespace cgck {
 
 // --------------------------------------------------------------------------
@@ -613,7 +615,7 @@ __global__ __launch_bounds__(256) void slot_kernel(KParams p)
 		uint4 w[8];
 #pragma unroll
 		for (int i = 0; i < 8; ++i)
-			w[i] = ldc<NT>(c0, 8 * s + i, act ? nch : 0, p.zero);
+			w[i] = ldc<NT>(c0, 8 * s + i, nch, p.zero);
 		uint32_t r = 0;
 #pragma unroll
 		for (int i = 0; i < 8; ++i)
@@ -773,14 +775,18 @@ __device__ __forceinline__ SMap smap(const KParams &p, uint64_t cur, uint64_t r1
 template <bool NT>
 __device__ __forceinline__ void slot_issue(const KParams &p, const SMap &M, uint4 (&w)[8])
 {
+	// Idle lanes (past the slots in use) clamp into the last placed packet's
+	// final chunk, a line its own tail lane reads anyway: pointing them all
+	// at the context's one zero chunk made every wave of the grid hit the
+	// same address (one L2 channel).  Their chunks are excluded from sums.
 	const uint4 *c0 = reinterpret_cast<const uint4 *>(M.a0 & ~(uint64_t)15);
 #pragma unroll
 	for (int i = 0; i < 8; ++i)
-		w[i] = ldc<NT>(c0, 8 * M.s + i, M.act ? M.nch : 0, p.zero);
+		w[i] = ldc<NT>(c0, 8 * M.s + i, M.nch, p.zero);
 }
 
 template <bool NT>
-__device__ __forceinline__ void slot_reduce(const KParams &p, uint64_t cur, const SMap &M, const uint4 (&w)[8],
+__device__ __forceinline__ void slot_reduce(const KParams &p, uint64_t cur, const SMap &M, uint4 (&w)[8],
 					    WaveStage &ws)
 {
 	const int l = threadIdx.x & 63;
@@ -802,8 +808,15 @@ __device__ __forceinline__ void slot_reduce(const KParams &p, uint64_t cur, cons
 		Hdr h{};
 		for (int wbase = 0; wbase < nsj; wbase += 64) {
 			const int sj = wbase + l;
-			uint4 v[8];
-			uint32_t r = jumbo_window<NT>(c0, nch, sj, v);
+			// the window reuses w[] (dead here) with clamped, branch-free loads
+			uint4 (&v)[8] = w;
+#pragma unroll
+			for (int i = 0; i < 8; ++i)
+				v[i] = ldc<NT>(c0, 8 * sj + i, nch, p.zero);
+			uint32_t r = 0;
+#pragma unroll
+			for (int i = 0; i < 8; ++i)
+				r = 8 * sj + i < nch ? sum4(v[i], r) : r;
 			if (wbase == 0 && !raw)
 				h = header<8, NT>(v, c0, nch, q, len, p.flags, l == 0);
 			const int j = (nch - 1) - 8 * sj;
@@ -862,30 +875,8 @@ __device__ __forceinline__ void slot_reduce(const KParams &p, uint64_t cur, cons
 		wave_stage_put(ws, cur + M.owner, result(p, a0, len, fold16(r), h));
 }
 
-// DEPTH 1: one chunk buffer, only the descriptors of the next iteration are
-// prefetched (keeps the VGPR budget of slot_kernel: 4 waves per SIMD).
 template <bool DESC, bool NT>
-__device__ __forceinline__ void slot_loop1(const KParams &p, uint64_t r0, uint64_t r1, uint32_t (&mark)[64],
-					   WaveStage &ws)
-{
-	const int l = threadIdx.x & 63;
-	uint64_t cur = r0;
-	DescW d = load_desc<DESC>(p, cur + l, r1);
-	for (;;) {
-		const SMap M = smap<DESC>(p, cur, r1, d, mark);
-		const uint64_t nxt = cur + (M.m ? M.m : 1);
-		d = load_desc<DESC>(p, nxt + l, r1);
-		uint4 w[8];
-		slot_issue<NT>(p, M, w);
-		slot_reduce<NT>(p, cur, M, w, ws);
-		if (nxt >= r1)
-			break;
-		cur = nxt;
-	}
-}
-
-template <bool DESC, bool NT, int DEPTH, int WPE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void slot2_kernel(KParams p)
+__global__ __launch_bounds__(256) void slot2_kernel(KParams p)
 {
 	__shared__ uint32_t mark[4][64];
 	__shared__ uint32_t so[4][kWaveStage];
@@ -899,11 +890,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 	if (r0 >= r1)
 		return;
 	WaveStage ws{so[wv], sv[wv], r0};
-	if (DEPTH == 1) {
-		slot_loop1<DESC, NT>(p, r0, r1, mark[wv], ws);
-		wave_stage_flush(p, ws, r1);
-		return;
-	}
 
 	// prologue: map A, desc of B, chunks of A
 	uint64_t curA = r0;
@@ -1006,7 +992,7 @@ hipError_t launch_lpp(const KParams &p, int num_cus, bool nt, int shape, hipStre
 	}
 }
 
-template <bool DESC, int DEPTH, int WPE>
+template <bool DESC>
 static hipError_t launch_slot2_t(const KParams &p, int max_blocks, bool nt, hipStream_t st)
 {
 	uint64_t want = (p.n + 4 * 64 - 1) / (4 * 64);
@@ -1014,26 +1000,22 @@ static hipError_t launch_slot2_t(const KParams &p, int max_blocks, bool nt, hipS
 	if (blocks < 1)
 		blocks = 1;
 	if (nt)
-		hipLaunchKernelGGL((slot2_kernel<DESC, true, DEPTH, WPE>), dim3(blocks), dim3(256), 0, st, p);
+		hipLaunchKernelGGL((slot2_kernel<DESC, true>), dim3(blocks), dim3(256), 0, st, p);
 	else
-		hipLaunchKernelGGL((slot2_kernel<DESC, false, DEPTH, WPE>), dim3(blocks), dim3(256), 0, st, p);
+		hipLaunchKernelGGL((slot2_kernel<DESC, false>), dim3(blocks), dim3(256), 0, st, p);
 	return hipGetLastError();
 }
 
-// depth 1: descriptor prefetch only; depth 2: chunks of the next iteration too
-hipError_t launch_slot2(const KParams &p, int num_cus, int depth, bool nt, hipStream_t st)
+hipError_t launch_slot2(const KParams &p, int num_cus, bool nt, hipStream_t st)
 {
-	const int mb = num_cus * 8;
-	switch (depth) {
-	case 1:
-		return p.desc ? launch_slot2_t<true, 1, 1>(p, mb, nt, st) : launch_slot2_t<false, 1, 1>(p, mb, nt, st);
-	case 3: // depth 2, >= 3 waves per SIMD
-		return p.desc ? launch_slot2_t<true, 2, 3>(p, mb, nt, st) : launch_slot2_t<false, 2, 3>(p, mb, nt, st);
-	case 4: // depth 2, >= 4 waves per SIMD
-		return p.desc ? launch_slot2_t<true, 2, 4>(p, mb, nt, st) : launch_slot2_t<false, 2, 4>(p, mb, nt, st);
-	default:
-		return p.desc ? launch_slot2_t<true, 2, 1>(p, mb, nt, st) : launch_slot2_t<false, 2, 1>(p, mb, nt, st);
-	}
+	// 8 blocks per CU requested; 2 waves per SIMD are resident (178 VGPRs).
+	// $CGCK_BPC overrides the blocks per CU for A/B runs.
+	static const int bpc = [] {
+		const char *e = getenv("CGCK_BPC");
+		return e && atoi(e) > 0 ? atoi(e) : 8;
+	}();
+	const int mb = num_cus * bpc;
+	return p.desc ? launch_slot2_t<true>(p, mb, nt, st) : launch_slot2_t<false>(p, mb, nt, st);
 }
 
 hipError_t launch_slot(const KParams &p, int num_cus, bool nt, hipStream_t st)
