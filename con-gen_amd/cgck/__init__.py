@@ -37,6 +37,21 @@ BAD_IP = 1
 BAD_L4 = 2
 BAD_LEN = 4
 
+# cgck_dst_entry_t (include/cgck.h): the struct ip_socket fields con-gen.c:344-349 fills.
+DST_DTYPE = np.dtype([("laddr", "<u4"), ("faddr", "<u4"), ("lport", "<u2"), ("fport", "<u2"),
+                      ("hash", "<u4")])
+assert DST_DTYPE.itemsize == 16
+
+
+class DstParams(ctypes.Structure):
+    """cgck_dst_params_t: the struct thread fields thread_init_dst_cache reads."""
+    _fields_ = [("laddr_min", ctypes.c_uint32), ("laddr_max", ctypes.c_uint32),
+                ("faddr_min", ctypes.c_uint32), ("faddr_max", ctypes.c_uint32),
+                ("fport", ctypes.c_uint16), ("rss_queue_num", ctypes.c_uint8),
+                ("rss_queue_id", ctypes.c_uint8), ("rss_key", ctypes.c_void_p),
+                ("rss_key_size", ctypes.c_int)]
+
+
 DESC_DTYPE = np.dtype([("frame_off", "<u8"), ("l3_off", "<u2"), ("ip_len", "<u2")], align=False)
 assert DESC_DTYPE.itemsize == 12
 
@@ -49,6 +64,7 @@ EXPORTS = (
     "cgck_synth_imix", "cgck_imix_bytes", "cgck_device_count", "cgck_dev_alloc", "cgck_dev_free",
     "cgck_host_alloc", "cgck_host_free", "cgck_memcpy", "cgck_memset", "cgck_event_create",
     "cgck_event_destroy", "cgck_event_record", "cgck_event_elapsed_ms", "cgck_probe_read",
+    "toeplitz_hash", "rss_hash4", "cgck_toeplitz", "cgck_dst_cache", "cgck_dst_cache_host",
 )
 
 
@@ -104,6 +120,14 @@ def load(path=None):
     L.cgck_event_record.argtypes = [_vp, _vp, _vp]
     L.cgck_event_elapsed_ms.argtypes = [_vp, _vp, ctypes.POINTER(ctypes.c_float)]
     L.cgck_probe_read.argtypes = [_vp, _vp, _u64, _vp, _vp]
+    L.toeplitz_hash.restype = _u32
+    L.toeplitz_hash.argtypes = [_vp, ctypes.c_int, _vp, ctypes.c_int]
+    L.rss_hash4.restype = _u32
+    L.rss_hash4.argtypes = [_u32, _u32, ctypes.c_uint16, ctypes.c_uint16, _vp, ctypes.c_int]
+    L.cgck_toeplitz.argtypes = [_vp, _vp, _u64, _u64, _u32, _vp, ctypes.c_int, _u32, _vp, _vp]
+    L.cgck_dst_cache.argtypes = [_vp, ctypes.POINTER(DstParams), _vp, _u32, _vp, _vp]
+    L.cgck_dst_cache_host.argtypes = [_vp, ctypes.POINTER(DstParams), _vp, _u32,
+                                      ctypes.POINTER(_u32)]
     _lib = L
     return L
 
@@ -147,6 +171,26 @@ tcp_cksum = udp_cksum
 def ip_cksum(buf, ip_off=0):
     """ip_cksum(ip) = in_cksum(ip, ip->ip_hl << 2) — subr.h:176."""
     return in_cksum(buf, ip_off, (int(buf[ip_off]) & 0x0F) << 2)
+
+
+def _u8(a):
+    return np.ascontiguousarray(np.frombuffer(bytes(a), np.uint8) if isinstance(a, (bytes, bytearray))
+                                else a, np.uint8)
+
+
+def toeplitz_hash(data, key, cnt=None, key_size=None):
+    """toeplitz_hash(data, cnt, key, key_size) — subr.c:482-502, on the GPU."""
+    d, k = _u8(data), _u8(key)
+    return load().toeplitz_hash(d.ctypes.data, len(d) if cnt is None else cnt, k.ctypes.data,
+                                len(k) if key_size is None else key_size)
+
+
+def rss_hash4(laddr, faddr, lport, fport, key, key_size=None):
+    """rss_hash4(laddr, faddr, lport, fport, key, key_size) — subr.c:506-530
+    (arguments in network order, as con-gen.c:338 passes them), on the GPU."""
+    k = _u8(key)
+    return load().rss_hash4(laddr, faddr, lport, fport, k.ctypes.data,
+                            len(k) if key_size is None else key_size)
 
 
 def tx_begin():
@@ -263,6 +307,37 @@ class Engine:
 
     def synth_imix(self, base, desc, n, seed, stream=None):
         _check(load().cgck_synth_imix(self.ctx, base, desc, n, seed, stream), "cgck_synth_imix")
+
+    def toeplitz(self, data, n, stride, cnt, key, out, mask=0xFFFFFFFF, key_size=None, stream=None):
+        """cgck_toeplitz: device data/out, host key.  Asynchronous."""
+        k = _u8(key)
+        _check(load().cgck_toeplitz(self.ctx, data, n, stride, cnt, k.ctypes.data,
+                                    len(k) if key_size is None else key_size, mask, out, stream),
+               "cgck_toeplitz")
+
+    @staticmethod
+    def dst_params(laddr, faddr, fport, queue_num, queue_id, key=None, key_size=None):
+        """laddr/faddr = (min, max) host order; fport network order.  The key
+        array must stay alive while the params are used."""
+        k = None if key is None else _u8(key)
+        p = DstParams(laddr[0], laddr[1], faddr[0], faddr[1], fport, queue_num, queue_id,
+                      None if k is None else k.ctypes.data,
+                      0 if k is None else (len(k) if key_size is None else key_size))
+        p._key_ref = k
+        return p
+
+    def dst_cache(self, params, out, cap, count, stream=None):
+        """cgck_dst_cache: device out/count, asynchronous."""
+        _check(load().cgck_dst_cache(self.ctx, ctypes.byref(params), out, cap, count, stream),
+               "cgck_dst_cache")
+
+    def dst_cache_host(self, params, cap):
+        """cgck_dst_cache_host: returns the DST_DTYPE entries written."""
+        out = np.zeros(cap, DST_DTYPE)
+        got = _u32()
+        _check(load().cgck_dst_cache_host(self.ctx, ctypes.byref(params), out.ctypes.data, cap,
+                                          ctypes.byref(got)), "cgck_dst_cache_host")
+        return out[:got.value]
 
     def probe_read(self, src, nbytes, sink, stream=None):
         _check(load().cgck_probe_read(self.ctx, src, nbytes, sink, stream), "cgck_probe_read")

@@ -67,6 +67,19 @@ struct cgck_ctx {
 	uint8_t *d_aux; // descriptors | out | verdict
 	size_t d_aux_cap;
 	void *d_zero; // 64 zero bytes (KParams.zero)
+	// Toeplitz byte tables of the last key used (cgck_rss.hip)
+	uint32_t *d_rss_tab;
+	size_t d_rss_tab_cap;
+	uint32_t *h_rss_tab; // host copy (malloc)
+	size_t h_rss_tab_cap;
+	uint8_t *rss_key; // the key the tables were built from (malloc)
+	int rss_key_len;
+	uint32_t rss_cnt;
+	bool rss_valid;
+	hipStream_t rss_stream; // stream of the last launch that read d_rss_tab
+	// dst-cache scratch: control words + look-back status (zeroed per launch)
+	uint8_t *d_dst;
+	size_t d_dst_cap;
 };
 
 struct cgck_event {
@@ -166,6 +179,12 @@ extern "C" int cgck_ctx_destroy(cgck_ctx_t *c)
 		(void)hipFree(c->d_aux);
 	if (c->d_zero)
 		(void)hipFree(c->d_zero);
+	if (c->d_rss_tab)
+		(void)hipFree(c->d_rss_tab);
+	if (c->d_dst)
+		(void)hipFree(c->d_dst);
+	free(c->h_rss_tab);
+	free(c->rss_key);
 	free(c);
 	return 0;
 }
@@ -479,6 +498,240 @@ extern "C" int cgck_tx_flush(void)
 		written++;
 	}
 	return written;
+}
+
+// --------------------------------------------------------------------------
+// Toeplitz RSS hash and the dst-cache build
+// --------------------------------------------------------------------------
+
+static constexpr uint32_t kRssMaxCnt = 65536;
+
+// Byte tables of a key: T[i][v] = XOR of W(8i+b) over the set bits b of v
+// (MSB first), where W(p) is the 32-bit window of the key bit stream at bit
+// p.  toeplitz_hash (subr.c:482-502) starts its window at key[0..3]
+// unconditionally (:489) and shifts in key[i+4] only while i+4 < key_size
+// (:496), so stream byte b is key[b] for b < max(4, key_size), else 0.
+static void rss_tables(const uint8_t *key, int key_size, uint32_t cnt, uint32_t *T)
+{
+	const uint64_t kb = key_size > 4 ? (uint64_t)key_size : 4;
+	auto kbyte = [&](uint64_t b) -> uint64_t { return b < kb ? key[b] : 0; };
+	for (uint32_t i = 0; i < cnt; i++) {
+		uint32_t W[8];
+		const uint64_t b = i;
+		const uint64_t x = kbyte(b) << 32 | kbyte(b + 1) << 24 | kbyte(b + 2) << 16 | kbyte(b + 3) << 8 |
+				   kbyte(b + 4);
+		for (int s = 0; s < 8; s++)
+			W[s] = (uint32_t)(x >> (8 - s));
+		for (uint32_t v = 0; v < 256; v++) {
+			uint32_t h = 0;
+			for (int s = 0; s < 8; s++)
+				if (v & (0x80u >> s))
+					h ^= W[s];
+			T[i * 256 + v] = h;
+		}
+	}
+}
+
+// Make d_rss_tab hold the tables of (key, key_size) for `cnt` bytes.  A key
+// change waits for the last launch that read the old tables.
+static int rss_prepare(cgck_ctx *c, const uint8_t *key, int key_size, uint32_t cnt, hipStream_t st)
+{
+	const int klen = key_size > 4 ? key_size : 4;
+	if (c->rss_valid && c->rss_key_len == klen && c->rss_cnt >= cnt && !memcmp(c->rss_key, key, klen))
+		return 0;
+	const uint32_t tcnt = cnt < 12 ? 12 : cnt; // rss_hash4's 12 bytes are always there
+	const size_t tbytes = (size_t)tcnt * 256 * 4;
+	if (c->rss_valid && c->rss_stream)
+		HIP_TRY(hipStreamSynchronize(c->rss_stream));
+	c->rss_valid = false;
+	if (tbytes > c->h_rss_tab_cap) {
+		free(c->h_rss_tab);
+		c->h_rss_tab = (uint32_t *)malloc(tbytes);
+		c->h_rss_tab_cap = c->h_rss_tab ? tbytes : 0;
+		if (!c->h_rss_tab)
+			return set_err(-ENOMEM, "rss tables: out of memory");
+	}
+	int rc;
+	if ((rc = grow_dev((void **)&c->d_rss_tab, &c->d_rss_tab_cap, tbytes)))
+		return rc;
+	uint8_t *nk = (uint8_t *)realloc(c->rss_key, klen);
+	if (!nk)
+		return set_err(-ENOMEM, "rss key: out of memory");
+	c->rss_key = nk;
+	memcpy(c->rss_key, key, klen);
+	c->rss_key_len = klen;
+	rss_tables(key, key_size, tcnt, c->h_rss_tab);
+	HIP_TRY(hipMemcpyAsync(c->d_rss_tab, c->h_rss_tab, tbytes, hipMemcpyHostToDevice, st));
+	HIP_TRY(hipStreamSynchronize(st)); // h_rss_tab is pageable and reused
+	c->rss_cnt = tcnt;
+	c->rss_valid = true;
+	return 0;
+}
+
+extern "C" int cgck_toeplitz(cgck_ctx_t *c, const void *data, uint64_t n, uint64_t stride, uint32_t cnt,
+			     const unsigned char *key, int key_size, uint32_t mask, uint32_t *out, void *stream)
+{
+	if (!c)
+		return set_err(-EINVAL, "cgck_toeplitz: NULL context");
+	if (n && (!data || !out))
+		return set_err(-EINVAL, "cgck_toeplitz: NULL data or out");
+	if (!key)
+		return set_err(-EINVAL, "cgck_toeplitz: NULL key");
+	if (cnt > kRssMaxCnt)
+		return set_err(-EINVAL, "cgck_toeplitz: cnt %u above %u", cnt, kRssMaxCnt);
+	if (n == 0)
+		return 0;
+	HIP_TRY(hipSetDevice(c->device));
+	hipStream_t st = pick(c, stream);
+	int rc = rss_prepare(c, key, key_size, cnt, st);
+	if (rc)
+		return rc;
+	RssParams p = {(const uint8_t *)data, n, stride, cnt, mask, c->d_rss_tab, out};
+	HIP_TRY(launch_toeplitz(p, c->num_cus, st));
+	c->rss_stream = st;
+	return 0;
+}
+
+extern "C" int cgck_dst_cache(cgck_ctx_t *c, const cgck_dst_params_t *prm, cgck_dst_entry_t *out, uint32_t cap,
+			      uint32_t *count, void *stream)
+{
+	if (!c || !prm || !out || !count)
+		return set_err(-EINVAL, "cgck_dst_cache: NULL argument");
+	if (cap == 0 || cap > 0x7fffffffu)
+		return set_err(-EINVAL, "cgck_dst_cache: cap must be in 1..INT_MAX (t_dst_cache_size)");
+	const bool filter = prm->rss_queue_id < 128 && prm->rss_queue_num > 1; // con-gen.c:337
+	if (filter && !prm->rss_key)
+		return set_err(-EINVAL, "cgck_dst_cache: RSS filter on but rss_key is NULL");
+	// scan_ip_range (con-gen.c:131-133) never yields min > max.
+	if (prm->laddr_min > prm->laddr_max || prm->faddr_min > prm->faddr_max)
+		return set_err(-EINVAL, "cgck_dst_cache: address range with min > max");
+	HIP_TRY(hipSetDevice(c->device));
+	hipStream_t st = pick(c, stream);
+	// con-gen.c:314-315: the product is formed in 32-bit unsigned arithmetic.
+	const uint32_t nl = prm->laddr_max - prm->laddr_min + 1u;
+	const uint32_t nf = prm->faddr_max - prm->faddr_min + 1u;
+	const uint32_t n = nl * nf * (uint32_t)(65535 - 5000 + 1);
+	if (n == 0) {
+		HIP_TRY(hipMemsetAsync(count, 0, 4, st));
+		return 0;
+	}
+	const uint32_t ntiles = (uint32_t)(((uint64_t)n + 4095) / 4096);
+	const size_t sbytes = 16 + (size_t)ntiles * 8;
+	int rc;
+	if ((rc = grow_dev((void **)&c->d_dst, &c->d_dst_cap, sbytes)))
+		return rc;
+	DstParams p = {};
+	p.laddr_min = prm->laddr_min;
+	p.faddr_min = prm->faddr_min;
+	p.nf = nf;
+	p.n = n;
+	p.q64 = 64 / nf;
+	p.r64 = 64 % nf;
+	p.fport_be = prm->fport;
+	p.filter = filter;
+	p.cap = cap;
+	p.ntiles = ntiles;
+	if (filter) {
+		if ((rc = rss_prepare(c, prm->rss_key, prm->rss_key_size, 12, st)))
+			return rc;
+		// rss_hash4 stores fport as given (subr.c:519): bytes 8, 9 of the data.
+		p.hconst = c->h_rss_tab[8 * 256 + (prm->fport & 255u)] ^ c->h_rss_tab[9 * 256 + (prm->fport >> 8)];
+		for (uint32_t h = 0; h < 128; h++)
+			if (h % prm->rss_queue_num == prm->rss_queue_id)
+				(h < 64 ? p.pass_lo : p.pass_hi) |= 1ull << (h & 63);
+		p.tab = c->d_rss_tab;
+	}
+	p.out = out;
+	p.ctl = (uint32_t *)c->d_dst;
+	p.count = count;
+	p.status = (uint64_t *)(c->d_dst + 16);
+	HIP_TRY(hipMemsetAsync(c->d_dst, 0, sbytes, st));
+	HIP_TRY(launch_dst_cache(p, c->num_cus, st));
+	if (filter)
+		c->rss_stream = st;
+	return 0;
+}
+
+extern "C" int cgck_dst_cache_host(cgck_ctx_t *c, const cgck_dst_params_t *prm, cgck_dst_entry_t *out,
+				   uint32_t cap, uint32_t *count)
+{
+	if (!c || !prm || !out || !count)
+		return set_err(-EINVAL, "cgck_dst_cache_host: NULL argument");
+	if (cap == 0 || cap > 0x7fffffffu)
+		return set_err(-EINVAL, "cgck_dst_cache_host: cap must be in 1..INT_MAX (t_dst_cache_size)");
+	HIP_TRY(hipSetDevice(c->device));
+	int rc;
+	const size_t obytes = (size_t)cap * sizeof(cgck_dst_entry_t);
+	if ((rc = grow_dev((void **)&c->d_bytes, &c->d_bytes_cap, obytes + 64)))
+		return rc;
+	if ((rc = grow_host((void **)&c->h_out, &c->h_out_cap, 64)))
+		return rc;
+	uint32_t *d_count = (uint32_t *)(c->d_bytes + obytes);
+	if ((rc = cgck_dst_cache(c, prm, (cgck_dst_entry_t *)c->d_bytes, cap, d_count, c->stream)))
+		return rc;
+	// count, then the control words (timeout flag) when the launch ran
+	HIP_TRY(hipMemcpyAsync(c->h_out, d_count, 4, hipMemcpyDeviceToHost, c->stream));
+	HIP_TRY(hipMemcpyAsync(c->h_out + 1, c->d_dst, 16, hipMemcpyDeviceToHost, c->stream));
+	HIP_TRY(hipStreamSynchronize(c->stream));
+	if (c->h_out[1 + 2])
+		return set_err(-ETIMEDOUT, "cgck_dst_cache: look-back spin limit reached");
+	const uint32_t got = c->h_out[0];
+	if (got > cap)
+		return set_err(-EIO, "cgck_dst_cache: count %u above cap %u", got, cap);
+	if (got)
+		HIP_TRY(hipMemcpy(out, c->d_bytes, (size_t)got * sizeof(cgck_dst_entry_t), hipMemcpyDeviceToHost));
+	*count = got;
+	return 0;
+}
+
+namespace {
+
+// One toeplitz_hash on the calling thread's context: the data is staged in
+// pinned memory, which the kernel reads over the fabric.
+uint32_t one_toeplitz(const uint8_t *data, uint32_t cnt, const uint8_t *key, int key_size, uint32_t mask)
+{
+	cgck_ctx *c = tls_ctx();
+	if (grow_host((void **)&c->h_stage, &c->h_stage_cap, cnt + 16) ||
+	    grow_host((void **)&c->h_out, &c->h_out_cap, 64))
+		die("staging allocation");
+	if (cnt)
+		memcpy(c->h_stage, data, cnt);
+	if (hipSetDevice(c->device) != hipSuccess || rss_prepare(c, key, key_size, cnt, c->stream) != 0)
+		die("rss tables");
+	RssParams p = {c->h_stage, 1, 0, cnt, mask, c->d_rss_tab, c->h_out};
+	hipError_t e = launch_toeplitz(p, c->num_cus, c->stream);
+	if (e == hipSuccess)
+		e = hipStreamSynchronize(c->stream);
+	if (e != hipSuccess) {
+		set_err(-EIO, "toeplitz: %s", hipGetErrorString(e));
+		die("toeplitz kernel");
+	}
+	c->rss_stream = c->stream;
+	return c->h_out[0];
+}
+
+} // namespace
+
+extern "C" uint32_t toeplitz_hash(const unsigned char *data, int cnt, const unsigned char *key, int key_size)
+{
+	if (cnt > (int)kRssMaxCnt) {
+		set_err(-EINVAL, "toeplitz_hash: cnt %d above %u", cnt, kRssMaxCnt);
+		die("toeplitz_hash");
+	}
+	// cnt <= 0: the reference's loop does not run and returns 0 (subr.c:490).
+	return one_toeplitz(data, cnt > 0 ? (uint32_t)cnt : 0, key, key_size, 0xffffffffu);
+}
+
+extern "C" uint32_t rss_hash4(uint32_t laddr, uint32_t faddr, uint16_t lport, uint16_t fport, unsigned char *key,
+			      int key_size)
+{
+	// subr.c:513-521: faddr, laddr, fport, lport as stored (network order).
+	uint8_t d[12];
+	memcpy(d + 0, &faddr, 4);
+	memcpy(d + 4, &laddr, 4);
+	memcpy(d + 8, &fport, 2);
+	memcpy(d + 10, &lport, 2);
+	return one_toeplitz(d, 12, key, key_size, 0x7Fu); // subr.c:523
 }
 
 // --------------------------------------------------------------------------

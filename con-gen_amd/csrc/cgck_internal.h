@@ -41,6 +41,42 @@ constexpr int kDefaultLppShape = 2;       // see launch_lpp (6 chunks up front, 
 constexpr bool kDefaultGroupNT = true, kDefaultGroupContig = true;
 constexpr bool kDefaultLaneNT = false, kDefaultLaneContig = false;
 
+// Toeplitz RSS hash (cgck_rss.hip; subr.c:482-530).  `tab` = cnt x 256 u32
+// byte tables derived from the key on the host (rss_tables in cgck_api.cpp).
+constexpr uint32_t kRssLdsMaxCnt = 36; // tables up to 36 KiB are staged in LDS
+
+struct RssParams {
+	const uint8_t *data;
+	uint64_t n;
+	uint64_t stride;
+	uint32_t cnt;
+	uint32_t mask;
+	const uint32_t *tab;
+	uint32_t *out;
+};
+
+// dst-cache build (cgck_rss.hip; con-gen.c:291-360).
+struct DstParams {
+	uint32_t laddr_min, faddr_min;
+	uint32_t nf;             // faddr count (t_ip_faddr_max - t_ip_faddr_min + 1), nonzero
+	uint32_t n;              // tuple count, u32 as con-gen.c:314-315 computes it
+	uint32_t q64, r64;       // 64 / nf, 64 % nf
+	uint32_t fport_be;       // t_port as stored (network order)
+	uint32_t hconst;         // the fport bytes' share of the hash
+	uint32_t filter;         // RSS filter on (con-gen.c:337)
+	uint32_t cap;            // t_dst_cache_size (> 0)
+	uint32_t ntiles;         // ceil(n / 4096)
+	uint64_t pass_lo, pass_hi; // bit h set: (h % t_rss_queue_num) == t_rss_queue_id, h in 0..127
+	const uint32_t *tab;     // 12 x 256 byte tables of the key
+	void *out;               // cgck_dst_entry_t[cap]
+	uint32_t *ctl;           // [0] ticket, [1] done, [2] timeout; zeroed per launch
+	uint32_t *count;         // entries written (con-gen.c:356); set by the kernel when n > 0
+	uint64_t *status;        // one look-back word per tile; zeroed per launch
+};
+
+hipError_t launch_toeplitz(const RssParams &p, int num_cus, hipStream_t st);
+hipError_t launch_dst_cache(const DstParams &p, int num_cus, hipStream_t st);
+
 hipError_t launch_cksum(const KParams &p, uint32_t len_hint, int num_cus, int kernel, hipStream_t st);
 hipError_t launch_synth_fill(uint8_t *base, uint64_t nbytes, uint64_t seed, int num_cus, hipStream_t st);
 hipError_t launch_synth_stamp(uint8_t *base, uint64_t n, uint64_t stride, uint32_t len, int num_cus,

@@ -166,6 +166,62 @@ int cgck_synth_imix(cgck_ctx_t *ctx, void *base, cgck_desc_t *desc, uint64_t n,
 		    uint64_t seed, void *stream);
 uint64_t cgck_imix_bytes(uint64_t n); /* bytes an n-packet IMIX batch occupies */
 
+/* ------------------------------------------------------------------------ */
+/* 3. Toeplitz RSS hash (subr.c:482-530, subr.h:370-371) */
+/*    and the dst-cache build that calls it (con-gen.c:291-360).             */
+/* ------------------------------------------------------------------------ */
+
+/* Drop-in symbols, prototypes of subr.h:370-371.  Synchronous, on the calling
+ * thread's context (like in_cksum).  toeplitz_hash: subr.c:482-502 over
+ * `cnt` bytes (cnt <= 65536; reads key[0..3] and key[4..key_size-1] as the
+ * reference does).  rss_hash4: subr.c:506-530, the hash of the 12 bytes
+ * {faddr, laddr, fport, lport} masked to 7 bits.  Caller: con-gen.c:338. */
+uint32_t toeplitz_hash(const unsigned char *data, int cnt, const unsigned char *key, int key_size);
+uint32_t rss_hash4(uint32_t laddr, uint32_t faddr, uint16_t lport, uint16_t fport,
+		   unsigned char *key, int key_size);
+
+/* Batched hash, device-resident: out[k] = toeplitz_hash(data + k*stride, cnt,
+ * key, key_size) & mask (mask 0x7F = rss_hash4 on {faddr, laddr, fport,
+ * lport} records of 12 bytes).  `key` is host memory (the context derives
+ * and caches its byte tables).  Asynchronous. */
+int cgck_toeplitz(cgck_ctx_t *ctx, const void *data, uint64_t n, uint64_t stride, uint32_t cnt,
+		  const unsigned char *key, int key_size, uint32_t mask, uint32_t *out, void *stream);
+
+/* One dst-cache entry: the fields thread_init_dst_cache fills in struct
+ * ip_socket (con-gen.c:344-349; subr.h:218-228).  16 bytes. */
+typedef struct cgck_dst_entry {
+	uint32_t laddr; /* ipso_laddr, network order */
+	uint32_t faddr; /* ipso_faddr, network order */
+	uint16_t lport; /* ipso_lport, network order */
+	uint16_t fport; /* ipso_fport, network order */
+	uint32_t hash;  /* ipso_hash = SO_HASH(faddr, lport, fport) (subr.h:179-180) */
+} cgck_dst_entry_t;
+
+/* The struct thread fields the loop reads (subr.h:274-279, 325-328). */
+typedef struct cgck_dst_params {
+	uint32_t laddr_min, laddr_max; /* t_ip_laddr_min/max, host order */
+	uint32_t faddr_min, faddr_max; /* t_ip_faddr_min/max, host order */
+	uint16_t fport;                /* t_port, network order */
+	uint8_t rss_queue_num;         /* t_rss_queue_num */
+	uint8_t rss_queue_id;          /* t_rss_queue_id; the filter runs only when
+	                                  id < 128 (RSS_QUEUE_ID_MAX) and num > 1 */
+	const unsigned char *rss_key;  /* t_rss_key (host memory; unused without the filter) */
+	int rss_key_size;              /* t_rss_key_size */
+} cgck_dst_params_t;
+
+/* Enumerate the candidate tuples in the reference's loop order (faddr
+ * fastest, then the ephemeral lport 5000..65535, then laddr; the tuple count
+ * is computed in 32-bit arithmetic as con-gen.c:314-315 does), keep those
+ * whose rss_hash4 % queue_num == queue_id, and write the first `cap`
+ * (t_dst_cache_size, >= 1) in order.  `*count` = entries written
+ * (con-gen.c:356; the caller panics below t_concurrency, :357-358).
+ * cgck_dst_cache: `out` and `count` are device memory, asynchronous.
+ * cgck_dst_cache_host: host memory, synchronous. */
+int cgck_dst_cache(cgck_ctx_t *ctx, const cgck_dst_params_t *prm, cgck_dst_entry_t *out, uint32_t cap,
+		   uint32_t *count, void *stream);
+int cgck_dst_cache_host(cgck_ctx_t *ctx, const cgck_dst_params_t *prm, cgck_dst_entry_t *out,
+			uint32_t cap, uint32_t *count);
+
 /* Plumbing for callers without their own runtime (tests, bench, C users). */
 int cgck_device_count(void);
 int cgck_dev_alloc(size_t bytes, void **ptr);

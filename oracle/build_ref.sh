@@ -31,3 +31,22 @@ sed -n 119,223p "$REF/subr.c" | $CC -O2 -DNDEBUG -finline-functions -falign-func
 	-std=gnu99 -pipe -pthread -fPIC -Wall -Wstrict-prototypes \
 	-I"$REF" -include "$REF/subr.h" -x c - -shared -o "$OUT/libref_cksum.so"
 echo "build_ref: $OUT/libref_cksum.so"
+
+# The Toeplitz RSS hash: freebsd_rss_key (subr.c:29-35),
+# toeplitz_hash (subr.c:482-502) and rss_hash4 (subr.c:506-530), read in place
+# the same way.  Line 504, `#include <rte_thash.h>`, sits between the two
+# functions and is not part of either, so it is left out of the range.
+k0=$(sed -n 29p "$REF/subr.c")
+t0=$(sed -n 482,483p "$REF/subr.c" | tr -d '\n')
+r0=$(sed -n 506,507p "$REF/subr.c" | cut -c1-9 | tr -d '\n')
+r1=$(sed -n 530p "$REF/subr.c")
+if [ "$k0" != "uint8_t freebsd_rss_key[RSS_KEY_SIZE] = {" ] || \
+   [ "$t0" != "uint32_ttoeplitz_hash(const u_char *data, int cnt, const u_char *key, int key_size)" ] || \
+   [ "$r0" != "uint32_trss_hash4" ] || [ "$r1" != "}" ]; then
+	echo "build_ref: subr.c:29-35/482-502/506-530 are not the RSS unit this recipe expects" >&2
+	exit 1
+fi
+sed -n '29,35p;482,502p;506,530p' "$REF/subr.c" | $CC -O2 -DNDEBUG -finline-functions -falign-functions=16 \
+	-std=gnu99 -pipe -pthread -fPIC -Wall -Wstrict-prototypes \
+	-I"$REF" -include "$REF/subr.h" -x c - -shared -o "$OUT/libref_rss.so"
+echo "build_ref: $OUT/libref_rss.so"

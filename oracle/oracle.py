@@ -18,6 +18,10 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 PORT_SO = os.path.join(HERE, "liboracle.so")
 REF_SO = os.path.join(HERE, "_ref", "libref_cksum.so")
+REF_RSS_SO = os.path.join(HERE, "_ref", "libref_rss.so")
+
+DST_DTYPE = np.dtype([("laddr", "<u4"), ("faddr", "<u4"), ("lport", "<u2"), ("fport", "<u2"),
+                      ("hash", "<u4")])   # cgck_dst_entry_t
 
 _u8p = ctypes.POINTER(ctypes.c_uint8)
 _u32p = ctypes.POINTER(ctypes.c_uint32)
@@ -83,6 +87,20 @@ class Port:
                                               ctypes.POINTER(ctypes.c_uint64)]
         L.oracle_fn_in_cksum.restype = ctypes.c_void_p
         L.oracle_fn_udp_cksum.restype = ctypes.c_void_p
+        # Toeplitz RSS (oracle/rss_oracle.c)
+        L.oracle_toeplitz_hash.restype = ctypes.c_uint32
+        L.oracle_toeplitz_hash.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
+        L.oracle_rss_hash4.restype = ctypes.c_uint32
+        L.oracle_rss_hash4.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint16,
+                                       ctypes.c_uint16, ctypes.c_void_p, ctypes.c_int]
+        L.oracle_toeplitz_batch.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
+                                            ctypes.c_uint32, ctypes.c_void_p, ctypes.c_int,
+                                            ctypes.c_uint32, ctypes.c_void_p]
+        L.oracle_dst_cache.restype = ctypes.c_uint32
+        L.oracle_dst_cache.argtypes = [ctypes.c_uint32] * 4 + [ctypes.c_uint16, ctypes.c_uint8,
+                                       ctypes.c_uint8, ctypes.c_void_p, ctypes.c_int,
+                                       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32]
+        L.oracle_fn_rss_hash4.restype = ctypes.c_void_p
 
     # -- pure functions (subr.c:186-195, 212-223) --
     def in_cksum(self, buf, off=0, n=None):
@@ -145,6 +163,41 @@ class Port:
                                                ctypes.byref(chk))
         return bad, chk.value
 
+    # -- Toeplitz RSS (subr.c:482-530, con-gen.c:291-360) --
+    def toeplitz_hash(self, data, key, cnt=None, key_size=None):
+        data = np.ascontiguousarray(data, np.uint8)
+        key = np.ascontiguousarray(key, np.uint8)
+        return self.lib.oracle_toeplitz_hash(data.ctypes.data, len(data) if cnt is None else cnt,
+                                             key.ctypes.data, len(key) if key_size is None else key_size)
+
+    def rss_hash4(self, laddr, faddr, lport, fport, key, key_size=None):
+        key = np.ascontiguousarray(key, np.uint8)
+        return self.lib.oracle_rss_hash4(laddr, faddr, lport, fport, key.ctypes.data,
+                                         len(key) if key_size is None else key_size)
+
+    def toeplitz_batch(self, data, n, stride, cnt, key, mask=0xFFFFFFFF, key_size=None):
+        key = np.ascontiguousarray(key, np.uint8)
+        out = np.zeros(n, np.uint32)
+        self.lib.oracle_toeplitz_batch(data.ctypes.data, n, stride, cnt, key.ctypes.data,
+                                       len(key) if key_size is None else key_size, mask,
+                                       out.ctypes.data)
+        return out
+
+    def dst_cache(self, laddr_min, laddr_max, faddr_min, faddr_max, fport, queue_num, queue_id,
+                  key, cap, hash_fn=None, key_size=None):
+        """con-gen.c:291-360 restated; hash_fn = a C rss_hash4 pointer (None:
+        this file's).  Returns a DST_DTYPE array of the entries written."""
+        key = np.ascontiguousarray(key, np.uint8)
+        out = np.zeros(cap, DST_DTYPE)
+        got = self.lib.oracle_dst_cache(laddr_min, laddr_max, faddr_min, faddr_max, fport,
+                                        queue_num, queue_id, key.ctypes.data,
+                                        len(key) if key_size is None else key_size, hash_fn,
+                                        out.ctypes.data, cap)
+        return out[:got]
+
+    def fn_rss_hash4(self):
+        return self.lib.oracle_fn_rss_hash4()
+
     def cpu_bench(self, fin, fudp, base, n, stride, ip_len, threads=1, reps=1):
         sink = ctypes.c_uint64()
         sec = self.lib.oracle_cpu_bench(fin, fudp, base.ctypes.data, n, stride, ip_len,
@@ -174,6 +227,42 @@ class Reference:
     def fn_pointers(self):
         return (ctypes.cast(self.lib.in_cksum, ctypes.c_void_p).value,
                 ctypes.cast(self.lib.udp_cksum, ctypes.c_void_p).value)
+
+
+class ReferenceRss:
+    """The reference's own Toeplitz unit: freebsd_rss_key, toeplitz_hash and
+    rss_hash4 (subr.c:29-35, 482-530), built into oracle/_ref/libref_rss.so."""
+
+    def __init__(self, path=REF_RSS_SO):
+        L = ctypes.CDLL(path)
+        self.lib = L
+        L.toeplitz_hash.restype = ctypes.c_uint32
+        L.toeplitz_hash.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
+        L.rss_hash4.restype = ctypes.c_uint32
+        L.rss_hash4.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint16, ctypes.c_uint16,
+                                ctypes.c_void_p, ctypes.c_int]
+        self.key = np.frombuffer((ctypes.c_uint8 * 40).in_dll(L, "freebsd_rss_key"), np.uint8).copy()
+
+    def toeplitz_hash(self, data, key, cnt=None, key_size=None):
+        data = np.ascontiguousarray(data, np.uint8)
+        key = np.ascontiguousarray(key, np.uint8)
+        return self.lib.toeplitz_hash(data.ctypes.data, len(data) if cnt is None else cnt,
+                                      key.ctypes.data, len(key) if key_size is None else key_size)
+
+    def rss_hash4(self, laddr, faddr, lport, fport, key, key_size=None):
+        key = np.ascontiguousarray(key, np.uint8)
+        return self.lib.rss_hash4(laddr, faddr, lport, fport, key.ctypes.data,
+                                  len(key) if key_size is None else key_size)
+
+    def fn_rss_hash4(self):
+        return ctypes.cast(self.lib.rss_hash4, ctypes.c_void_p).value
+
+
+def reference_rss():
+    """The reference's RSS build, or None where it was not built."""
+    if not os.path.exists(REF_RSS_SO):
+        return None
+    return ReferenceRss()
 
 
 _port = None

@@ -214,5 +214,119 @@ def main():
     print("golden fixtures written to", HERE)
 
 
-if __name__ == "__main__":
+if __name__ == "__main__" and len(sys.argv) == 1:
     main()
+    rss_main()
+
+
+# ---------------------------------------------------------------------------
+# Toeplitz RSS fixtures: tests/golden/rss.json.
+#     python tests/golden/make_golden.py rss
+# Expected hashes come from the reference's own toeplitz_hash / rss_hash4
+# (oracle/_ref/libref_rss.so, built from subr.c:29-35, 482-530).  The
+# dst-cache sets run the loop of con-gen.c:291-360 (restated in
+# oracle/rss_oracle.c) with the REFERENCE's rss_hash4 as its hash, and store
+# the count, a SHA-256 of the entries and the first/last 32 entries.
+# ---------------------------------------------------------------------------
+
+MS_RSS = [  # Microsoft RSS verification suite, default key: (dst, dport, src, sport, ipv4, ipv4+tcp)
+    ("161.142.100.80", 1766, "66.9.149.187", 2794, 0x323e8fc2, 0x51ccc178),
+    ("65.69.140.83", 4739, "199.92.111.2", 14230, 0xd718262a, 0xc626b0ea),
+    ("12.22.207.184", 38024, "24.19.198.95", 12898, 0xd2d0a5de, 0x5c2b394a),
+    ("209.142.163.6", 2217, "38.27.205.30", 48228, 0x82989176, 0xafc7327f),
+    ("202.188.127.2", 1303, "153.39.163.191", 44251, 0x5d1809c5, 0x10e828a2),
+]
+
+
+def ip4(s):
+    a, b, c, d = (int(x) for x in s.split("."))
+    return (a << 24) | (b << 16) | (c << 8) | d
+
+
+def htonl(x):
+    return int.from_bytes(x.to_bytes(4, "big"), "little")
+
+
+def htons(x):
+    return int.from_bytes(x.to_bytes(2, "big"), "little")
+
+
+DST_SETS = [  # name, laddr range, faddr range, port, queue_num, queue_id, key, cap
+    ("default_q4", "10.0.0.1", "10.0.0.1", "10.1.0.1", "10.1.0.1", 80, 4, 1, "freebsd", 100000),
+    ("straddle_q8", "10.0.0.1", "10.0.0.2", "10.1.0.1", "10.1.0.3", 8080, 8, 7, "freebsd", 5000),
+    ("no_filter_id128", "10.0.0.1", "10.0.0.1", "10.1.0.1", "10.1.0.2", 80, 4, 128, "freebsd", 70000),
+    ("no_filter_num1", "10.0.0.1", "10.0.0.1", "10.1.0.1", "10.1.0.9", 443, 1, 0, "freebsd", 1000),
+    ("id_above_num", "10.0.0.1", "10.0.0.1", "10.1.0.1", "10.1.0.1", 80, 4, 5, "freebsd", 100000),
+    ("many_tiles_q16", "10.0.0.1", "10.0.0.1", "10.2.0.0", "10.2.0.199", 80, 16, 3, "freebsd", 100000),
+    ("nf63_q2", "192.168.0.1", "192.168.0.2", "172.16.0.1", "172.16.0.63", 80, 2, 0, "freebsd", 1 << 22),
+    ("nf64_q3", "192.168.0.1", "192.168.0.1", "172.16.0.0", "172.16.0.63", 80, 3, 2, "freebsd", 1 << 22),
+    ("nf65_q5", "192.168.0.1", "192.168.0.1", "172.16.0.0", "172.16.0.64", 53, 5, 4, "freebsd", 1 << 22),
+    ("nf130_q7", "192.168.0.1", "192.168.0.1", "172.16.0.0", "172.16.0.129", 53, 7, 0, "freebsd", 1 << 22),
+    ("key52_q3", "10.0.0.1", "10.0.0.3", "10.1.0.1", "10.1.0.4", 80, 3, 2, "random52", 300000),
+    ("key16_q12", "10.0.0.1", "10.0.0.1", "10.1.0.1", "10.1.0.4", 80, 12, 11, "random16", 20000),
+    ("cap1", "10.0.0.1", "10.0.0.1", "10.1.0.1", "10.1.0.1", 80, 4, 1, "freebsd", 1),
+    ("full_range_zero_n", "0.0.0.0", "255.255.255.255", "10.1.0.1", "10.1.0.1", 80, 4, 1, "freebsd", 100),
+    ("wrapped_n", "10.0.0.0", "10.0.255.255", "10.1.0.0", "10.1.0.255", 80, 2, 1, "freebsd", 200000),
+]
+
+
+def rss_main():
+    import hashlib
+    RR = oracle.reference_rss()
+    if RR is None:
+        sys.exit("make_golden: oracle/_ref/libref_rss.so missing (run make -C oracle)")
+    P = oracle.port()
+    key = RR.key
+    rng = np.random.default_rng(23)
+    keys = {"freebsd": key, "random52": rng.integers(0, 256, 52, dtype=np.uint8),
+            "random16": rng.integers(0, 256, 16, dtype=np.uint8)}
+    out = {"freebsd_rss_key": key.tobytes().hex(),
+           "keys": {k: v.tobytes().hex() for k, v in keys.items()}}
+
+    # Published vectors, checked against the reference build here.
+    ms = []
+    for dst, dp, src, sp, h2, h4 in MS_RSS:
+        d4 = np.frombuffer(ip4(src).to_bytes(4, "big") + ip4(dst).to_bytes(4, "big")
+                           + sp.to_bytes(2, "big") + dp.to_bytes(2, "big"), np.uint8)
+        assert RR.toeplitz_hash(d4, key) == h4 and RR.toeplitz_hash(d4[:8], key) == h2
+        r4 = RR.rss_hash4(htonl(ip4(dst)), htonl(ip4(src)), htons(dp), htons(sp), key)
+        ms.append({"data_hex": d4.tobytes().hex(), "ipv4": h2, "ipv4_tcp": h4, "rss_hash4": r4,
+                   "laddr": htonl(ip4(dst)), "faddr": htonl(ip4(src)), "lport": htons(dp),
+                   "fport": htons(sp)})
+    out["ms_vectors"] = ms
+
+    # toeplitz_hash over random data: every cnt 0..48 and 100, 1500 for a set
+    # of key sizes (key_size < 4 still reads key[0..3], subr.c:489).
+    buf = rng.integers(0, 256, 1600, dtype=np.uint8)
+    kbuf = rng.integers(0, 256, 64, dtype=np.uint8)
+    cnts = list(range(49)) + [100, 1500]
+    ksz = [2, 4, 5, 12, 16, 40, 52, 64]
+    grid = [[RR.toeplitz_hash(buf, kbuf, c, ks) for c in cnts] for ks in ksz]
+    out["toeplitz_grid"] = {"data_hex": buf.tobytes().hex(), "key_hex": kbuf.tobytes().hex(),
+                            "cnts": cnts, "key_sizes": ksz, "hash": grid}
+
+    # 4096 random 12-byte tuples (dense records) with the default key.
+    tup = rng.integers(0, 256, 4096 * 12, dtype=np.uint8)
+    out["tuples12"] = {"data_hex": tup.tobytes().hex(),
+                       "hash": [RR.toeplitz_hash(tup[12 * k:12 * k + 12], key) for k in range(4096)]}
+
+    dsets = []
+    ref_fn = RR.fn_rss_hash4()
+    for name, l0, l1, f0, f1, port, qn, qi, kname, cap in DST_SETS:
+        k = keys[kname]
+        ents = P.dst_cache(ip4(l0), ip4(l1), ip4(f0), ip4(f1), htons(port), qn, qi, k, cap,
+                           hash_fn=ref_fn)
+        dsets.append({"name": name, "laddr": [ip4(l0), ip4(l1)], "faddr": [ip4(f0), ip4(f1)],
+                      "fport": htons(port), "queue_num": qn, "queue_id": qi, "key": kname,
+                      "cap": cap, "count": len(ents),
+                      "sha256": hashlib.sha256(ents.tobytes()).hexdigest(),
+                      "head": ents[:32].tobytes().hex(), "tail": ents[-32:].tobytes().hex()})
+        print(f"  dst set {name}: {len(ents)} entries")
+    out["dst_sets"] = dsets
+    with open(os.path.join(HERE, "rss.json"), "w") as f:
+        json.dump(out, f, separators=(",", ":"))
+    print("rss fixtures written to", HERE)
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "rss":
+    rss_main()

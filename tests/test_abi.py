@@ -40,6 +40,24 @@ def test_drop_in_prototypes_match_reference():
         assert "uint16_t udp_cksum(struct ip *, int);" in ref
 
 
+def test_rss_drop_in_prototypes_match_reference():
+    """toeplitz_hash/rss_hash4 keep subr.h:370-371's prototypes (u_char is
+    unsigned char, be32_t/be16_t are uint32_t/uint16_t, subr.h:183-184)."""
+    hdr = open(os.path.join(ROOT, "include", "cgck.h")).read()
+    assert ("uint32_t toeplitz_hash(const unsigned char *data, int cnt, const unsigned char *key, "
+            "int key_size);") in hdr
+    assert "uint32_t rss_hash4(uint32_t laddr, uint32_t faddr, uint16_t lport, uint16_t fport," in hdr
+    if os.path.exists("/root/reference/subr.h"):
+        ref = open("/root/reference/subr.h").read()
+        assert "uint32_t toeplitz_hash(const u_char *, int, const u_char *, int);" in ref
+        assert "uint32_t rss_hash4(be32_t, be32_t, be16_t, be16_t, u_char *, int);" in ref
+
+
+def test_dst_layout():
+    assert cgck.DST_DTYPE.itemsize == 16
+    assert ctypes.sizeof(cgck.DstParams) == 40   # 16 + 2 + 1 + 1, pad, pointer, int, pad
+
+
 def test_desc_layout():
     assert cgck.DESC_DTYPE.itemsize == 12
     assert cgck.DESC_DTYPE.fields["l3_off"][1] == 8
