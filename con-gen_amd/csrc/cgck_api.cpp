@@ -615,11 +615,7 @@ extern "C" int cgck_dst_cache(cgck_ctx_t *c, const cgck_dst_params_t *prm, cgck_
 		HIP_TRY(hipMemsetAsync(count, 0, 4, st));
 		return 0;
 	}
-	const uint32_t ntiles = (uint32_t)(((uint64_t)n + 4095) / 4096);
-	const size_t sbytes = 16 + (size_t)ntiles * 8;
 	int rc;
-	if ((rc = grow_dev((void **)&c->d_dst, &c->d_dst_cap, sbytes)))
-		return rc;
 	DstParams p = {};
 	p.laddr_min = prm->laddr_min;
 	p.faddr_min = prm->faddr_min;
@@ -630,7 +626,6 @@ extern "C" int cgck_dst_cache(cgck_ctx_t *c, const cgck_dst_params_t *prm, cgck_
 	p.fport_be = prm->fport;
 	p.filter = filter;
 	p.cap = cap;
-	p.ntiles = ntiles;
 	if (filter) {
 		if ((rc = rss_prepare(c, prm->rss_key, prm->rss_key_size, 12, st)))
 			return rc;
@@ -641,6 +636,12 @@ extern "C" int cgck_dst_cache(cgck_ctx_t *c, const cgck_dst_params_t *prm, cgck_
 				(h < 64 ? p.pass_lo : p.pass_hi) |= 1ull << (h & 63);
 		p.tab = c->d_rss_tab;
 	}
+	p.iters = dst_iters(n, cap, filter, p.pass_lo, p.pass_hi, c->num_cus);
+	const uint64_t tile = 256ull * p.iters;
+	p.ntiles = (uint32_t)(((uint64_t)n + tile - 1) / tile);
+	const size_t sbytes = 16 + (size_t)p.ntiles * 8;
+	if ((rc = grow_dev((void **)&c->d_dst, &c->d_dst_cap, sbytes)))
+		return rc;
 	p.out = out;
 	p.ctl = (uint32_t *)c->d_dst;
 	p.count = count;

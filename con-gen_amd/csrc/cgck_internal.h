@@ -65,7 +65,8 @@ struct DstParams {
 	uint32_t hconst;         // the fport bytes' share of the hash
 	uint32_t filter;         // RSS filter on (con-gen.c:337)
 	uint32_t cap;            // t_dst_cache_size (> 0)
-	uint32_t ntiles;         // ceil(n / 4096)
+	uint32_t ntiles;         // ceil(n / (256 * iters))
+	uint32_t iters;          // per-wave iterations of 64 tuples per tile (dst_iters)
 	uint64_t pass_lo, pass_hi; // bit h set: (h % t_rss_queue_num) == t_rss_queue_id, h in 0..127
 	const uint32_t *tab;     // 12 x 256 byte tables of the key
 	void *out;               // cgck_dst_entry_t[cap]
@@ -76,6 +77,7 @@ struct DstParams {
 
 hipError_t launch_toeplitz(const RssParams &p, int num_cus, hipStream_t st);
 hipError_t launch_dst_cache(const DstParams &p, int num_cus, hipStream_t st);
+uint32_t dst_iters(uint32_t n, uint32_t cap, bool filter, uint64_t pass_lo, uint64_t pass_hi, int num_cus);
 
 hipError_t launch_cksum(const KParams &p, uint32_t len_hint, int num_cus, int kernel, hipStream_t st);
 hipError_t launch_synth_fill(uint8_t *base, uint64_t nbytes, uint64_t seed, int num_cus, hipStream_t st);

@@ -17,6 +17,8 @@
 // nothing (it enumerates its tuples) and is bound by VALU/LDS issue.
 #include "cgck_device.h"
 
+#include <stdlib.h>
+
 namespace cgck {
 
 #define RLX_AGENT __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT
@@ -69,10 +71,105 @@ __global__ __launch_bounds__(256) void toeplitz_kernel(RssParams p)
 	}
 }
 
-hipError_t launch_toeplitz(const RssParams &p, int num_cus, hipStream_t st)
+// Dense 12-byte records (the rss_hash4 tuple array), 16-byte aligned: each
+// lane takes 4 consecutive records = 48 bytes = 3 uint4 loads, and writes
+// its 4 results as one uint4 (16 B per lane, coalesced).  Two groups per
+// lane are loaded before either is hashed, so 6 loads are in flight.
+// Byte tables: 12 ds_read_b32 per tuple, but 32 lanes of random bytes land
+// on the 32 banks with ~3.5-way conflicts (MI355X_MICROARCH.md § LDS).
+// Nibble tables (NIB): 24 lookups into 16-entry rows, which map onto 16
+// distinct banks, so every access pattern is conflict-free (identical
+// addresses broadcast).  NT[2i][v] = T[i][v << 4] (high nibble of byte i),
+// NT[2i+1][v] = T[i][v].
+template <bool NIB>
+__device__ __forceinline__ uint32_t hash12(const uint32_t *T, uint32_t w0, uint32_t w1, uint32_t w2)
 {
-	if (p.n == 0)
+	uint32_t h = 0;
+	const uint32_t w[3] = {w0, w1, w2};
+#pragma unroll
+	for (int c = 0; c < 3; c++)
+#pragma unroll
+		for (int j = 0; j < 4; j++) {
+			if (NIB) {
+				h ^= T[(2 * (4 * c + j) + 0) * 16 + ((w[c] >> (8 * j + 4)) & 15u)];
+				h ^= T[(2 * (4 * c + j) + 1) * 16 + ((w[c] >> (8 * j)) & 15u)];
+			} else {
+				h ^= T[(4 * c + j) * 256 + ((w[c] >> (8 * j)) & 255u)];
+			}
+		}
+	return h;
+}
+
+template <bool NIB>
+__device__ __forceinline__ u32x4_t hash4x12(const uint32_t *T, const u32x4_t &a, const u32x4_t &b,
+					    const u32x4_t &c, uint32_t mask)
+{
+	u32x4_t o;
+	o.x = hash12<NIB>(T, a.x, a.y, a.z) & mask;
+	o.y = hash12<NIB>(T, a.w, b.x, b.y) & mask;
+	o.z = hash12<NIB>(T, b.z, b.w, c.x) & mask;
+	o.w = hash12<NIB>(T, c.y, c.z, c.w) & mask;
+	return o;
+}
+
+template <bool NIB>
+__global__ __launch_bounds__(256) void toeplitz12x4_kernel(RssParams p, uint64_t ng)
+{
+	extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+	const uint32_t CGCK_GLOBAL *gt = (const uint32_t CGCK_GLOBAL *)p.tab;
+	if (NIB) {
+		for (uint32_t i = threadIdx.x; i < 24 * 16; i += 256) {
+			const uint32_t r = i >> 4, v = i & 15;
+			smem[i] = gt[(r >> 1) * 256 + ((r & 1) ? v : v << 4)];
+		}
+	} else {
+		for (uint32_t i = threadIdx.x; i < 12 * 256; i += 256)
+			smem[i] = gt[i];
+	}
+	__syncthreads();
+	const u32x4_t CGCK_GLOBAL *src = (const u32x4_t CGCK_GLOBAL *)p.data;
+	u32x4_t CGCK_GLOBAL *out = (u32x4_t CGCK_GLOBAL *)p.out;
+	const uint64_t step = (uint64_t)gridDim.x * 256;
+	uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+	for (; g + step < ng; g += 2 * step) {
+		const uint64_t g2 = g + step;
+		const u32x4_t a0 = src[3 * g], b0 = src[3 * g + 1], c0 = src[3 * g + 2];
+		const u32x4_t a1 = src[3 * g2], b1 = src[3 * g2 + 1], c1 = src[3 * g2 + 2];
+		out[g] = hash4x12<NIB>(smem, a0, b0, c0, p.mask);
+		out[g2] = hash4x12<NIB>(smem, a1, b1, c1, p.mask);
+	}
+	if (g < ng) {
+		const u32x4_t a = src[3 * g], b = src[3 * g + 1], c = src[3 * g + 2];
+		out[g] = hash4x12<NIB>(smem, a, b, c, p.mask);
+	}
+}
+
+hipError_t launch_toeplitz(const RssParams &p0, int num_cus, hipStream_t st)
+{
+	if (p0.n == 0)
 		return hipSuccess;
+	RssParams p = p0;
+	if (p.cnt == 12 && p.stride == 12 && ((uintptr_t)p.data & 15) == 0 && ((uintptr_t)p.out & 15) == 0 &&
+	    p.n >= 4) {
+		const uint64_t ng = p.n / 4;
+		const uint64_t want = (ng + 255) / 256, cap = (uint64_t)num_cus * 8;
+		// Byte tables by default: measured 0.225 vs 0.233 ms for nibble tables
+		// on 64M tuples (the kernel is bound by the mixed read/write stream,
+		// not by LDS conflicts).  CGCK_RSS_NIB=1 selects the nibble tables.
+		const char *ab = getenv("CGCK_RSS_NIB");
+		if (ab && *ab == '1')
+			hipLaunchKernelGGL(toeplitz12x4_kernel<true>, dim3((unsigned)(want < cap ? want : cap)),
+					   dim3(256), 24 * 16 * 4, st, p, ng);
+		else
+			hipLaunchKernelGGL(toeplitz12x4_kernel<false>, dim3((unsigned)(want < cap ? want : cap)),
+					   dim3(256), 12 * 256 * 4, st, p, ng);
+		hipError_t e = hipGetLastError();
+		if (e != hipSuccess || ng * 4 == p.n)
+			return e;
+		p.data += ng * 48;
+		p.out += ng * 4;
+		p.n -= ng * 4;
+	}
 	const uint64_t want = (p.n + 255) / 256;
 	const uint64_t cap = (uint64_t)num_cus * 8;
 	const dim3 g((unsigned)(want < cap ? want : cap)), b(256);
@@ -112,53 +209,78 @@ hipError_t launch_toeplitz(const RssParams &p, int num_cus, hipStream_t st)
 // and reports a timeout.  Once a tile's prefix reaches `cap` no new tickets
 // are drawn.
 
-constexpr int kDstWaves = 4, kDstIters = 16;
-constexpr uint32_t kNEph = 65535 - 5000 + 1; // NEPHEMERAL (subr.h:62-64)
-constexpr uint32_t kEphMin = 5000;           // EPHEMERAL_MIN
+constexpr int kDstWaves = 4, kDstIters = 512; // iterations per wave per tile: p.iters <= kDstIters
+constexpr uint32_t kNEph = 65535 - 5000 + 1;             // NEPHEMERAL (subr.h:62-64)
+constexpr uint32_t kEphMin = 5000;                        // EPHEMERAL_MIN
 constexpr uint64_t kStAgg = 1ull << 62, kStIncl = 2ull << 62;
 constexpr uint32_t kSpinLimit = 1u << 22;
+constexpr int kLookWin = 4; // predecessor words per lane per look-back round trip (256 per wave)
 
+// LDS carve-up (dynamic, 16-byte aligned; Guideline 17): [tables 12 KiB when
+// filtering] [survivor bits: waves x iters/32 x 64 u32] [S: 16 u32].
+constexpr uint32_t kDstMaskBytes = kDstWaves * (kDstIters / 32) * 64 * 4;
+
+// Per-lane tuple cursor: offsets into the faddr, lport and laddr ranges,
+// and the hash share of the laddr bytes and fport (recomputed only when
+// laddr changes, once per 60536 x nf tuples).  The faddr and lport shares
+// are looked up per tuple, unconditionally, so the loop has no divergent
+// branch on the common path.
 struct Cursor {
-	uint32_t fa, lp, la; // offsets into the faddr, lport and laddr ranges
+	uint32_t fa, lp, la;
+	uint32_t hl;
 };
 
-__device__ __forceinline__ void cursor_at(Cursor &c, uint32_t idx, const DstParams &p)
+__device__ __forceinline__ uint32_t hash_fa(const uint32_t *T, uint32_t fa)
+{
+	return T[0 * 256 + (fa >> 24)] ^ T[1 * 256 + ((fa >> 16) & 255u)] ^ T[2 * 256 + ((fa >> 8) & 255u)] ^
+	       T[3 * 256 + (fa & 255u)];
+}
+
+__device__ __forceinline__ uint32_t hash_la(const uint32_t *T, uint32_t la)
+{
+	return T[4 * 256 + (la >> 24)] ^ T[5 * 256 + ((la >> 16) & 255u)] ^ T[6 * 256 + ((la >> 8) & 255u)] ^
+	       T[7 * 256 + (la & 255u)];
+}
+
+// lport = htons(port): data bytes 10, 11 = port >> 8, port & 255.
+__device__ __forceinline__ uint32_t hash_lp(const uint32_t *T, uint32_t lp)
+{
+	return T[10 * 256 + (lp >> 8)] ^ T[11 * 256 + (lp & 255u)];
+}
+
+template <bool FILTER>
+__device__ __forceinline__ void cursor_at(Cursor &c, uint32_t idx, const DstParams &p, const uint32_t *T)
 {
 	const uint32_t q = idx / p.nf;
 	c.fa = idx - q * p.nf;
 	c.lp = q % kNEph;
 	c.la = q / kNEph;
+	if (FILTER)
+		c.hl = hash_la(T, p.laddr_min + c.la) ^ p.hconst;
 }
 
 // idx += 64: at most one carry per digit (64 % nf < nf; 64 / nf + 1 < kNEph).
-__device__ __forceinline__ void cursor_step64(Cursor &c, const DstParams &p)
+template <bool FILTER>
+__device__ __forceinline__ void cursor_step64(Cursor &c, const DstParams &p, const uint32_t *T)
 {
 	c.fa += p.r64;
-	uint32_t dq = p.q64;
-	if (c.fa >= p.nf) {
-		c.fa -= p.nf;
-		dq++;
-	}
-	c.lp += dq;
+	const bool cf = c.fa >= p.nf;
+	c.fa -= cf ? p.nf : 0u;
+	c.lp += p.q64 + (cf ? 1u : 0u);
 	if (c.lp >= kNEph) {
 		c.lp -= kNEph;
 		c.la++;
+		if (FILTER)
+			c.hl = hash_la(T, p.laddr_min + c.la) ^ p.hconst;
 	}
 }
 
-// rss_hash4 data bytes (subr.c:513-521): faddr, laddr (network order =
-// host-order value MSB first), fport as stored, lport = htons(port).  The
-// fport bytes are constant per launch and folded into p.hconst.
-__device__ __forceinline__ uint32_t tuple_hash(const uint32_t *T, uint32_t fa, uint32_t la, uint32_t lp,
-					       uint32_t hconst)
+// Does the tuple under the cursor pass the RSS filter (con-gen.c:337-342)?
+__device__ __forceinline__ bool rss_pass(const Cursor &c, const DstParams &p, const uint32_t *T)
 {
-	uint32_t h = hconst;
-	h ^= T[0 * 256 + (fa >> 24)] ^ T[1 * 256 + ((fa >> 16) & 255u)];
-	h ^= T[2 * 256 + ((fa >> 8) & 255u)] ^ T[3 * 256 + (fa & 255u)];
-	h ^= T[4 * 256 + (la >> 24)] ^ T[5 * 256 + ((la >> 16) & 255u)];
-	h ^= T[6 * 256 + ((la >> 8) & 255u)] ^ T[7 * 256 + (la & 255u)];
-	h ^= T[10 * 256 + (lp >> 8)] ^ T[11 * 256 + (lp & 255u)];
-	return h;
+	const uint32_t h = (hash_fa(T, p.faddr_min + c.fa) ^ hash_lp(T, kEphMin + c.lp) ^ c.hl) & 0x7Fu;
+	const uint32_t w = h < 64 ? (uint32_t)(p.pass_lo >> (h & 32)) : (uint32_t)(p.pass_hi >> (h & 32));
+	return (w >> (h & 31)) & 1u;
 }
 
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v)
@@ -174,8 +296,10 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t m)
 	return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-// Exclusive prefix of tile t: sum of the published counts of tiles < t,
-// walking back from t-1 until an inclusive word.  Wave-uniform result.
+// Exclusive prefix of tile t: the sum of the published counts of the tiles
+// before it, walking back from t-1 until an inclusive word.  Each round
+// trip reads 64 x kLookWin words (lane l, slot k: tile t-1-l-64k), so the
+// walk crosses the tiles in flight in a few round trips.  Wave-uniform.
 __device__ uint32_t dst_lookback(const DstParams &p, uint32_t t, int lane)
 {
 	uint64_t CGCK_GLOBAL *st = (uint64_t CGCK_GLOBAL *)p.status;
@@ -183,13 +307,33 @@ __device__ uint32_t dst_lookback(const DstParams &p, uint32_t t, int lane)
 	int64_t j = (int64_t)t - 1;
 	uint32_t spins = 0;
 	for (;;) {
-		const int64_t idx = j - lane;
-		const uint64_t s = idx >= 0 ? __hip_atomic_load(st + idx, RLX_AGENT) : kStIncl;
-		const uint64_t incl = __ballot((s >> 62) == 2);
-		const uint64_t inval = __ballot((s >> 62) == 0);
-		const int stop = incl ? __builtin_ctzll(incl) : 64;
-		const uint64_t need = stop >= 63 ? ~0ull : ((2ull << stop) - 1);
-		if (inval & need) {
+		uint64_t s[kLookWin];
+#pragma unroll
+		for (int k = 0; k < kLookWin; k++) {
+			const int64_t idx = j - lane - 64 * k;
+			s[k] = idx >= 0 ? __hip_atomic_load(st + idx, RLX_AGENT) : kStIncl;
+		}
+		// nearest inclusive word: slot k, lane ctz
+		int stop_k = kLookWin, stop_l = 63;
+		bool missing = false;
+#pragma unroll
+		for (int k = 0; k < kLookWin; k++) {
+			if (stop_k < kLookWin)
+				break;
+			const uint64_t incl = __ballot((s[k] >> 62) == 2);
+			const uint64_t inval = __ballot((s[k] >> 62) == 0);
+			const int l = incl ? __builtin_ctzll(incl) : 63;
+			const uint64_t need = l >= 63 ? ~0ull : ((2ull << l) - 1);
+			if (inval & need) {
+				missing = true;
+				break;
+			}
+			if (incl) {
+				stop_k = k;
+				stop_l = l;
+			}
+		}
+		if (missing) {
 			if (++spins > kSpinLimit) {
 				if (lane == 0)
 					__hip_atomic_store((uint32_t CGCK_GLOBAL *)p.ctl + 2, 1u, RLX_AGENT);
@@ -198,10 +342,15 @@ __device__ uint32_t dst_lookback(const DstParams &p, uint32_t t, int lane)
 			__builtin_amdgcn_s_sleep(1);
 			continue;
 		}
-		excl += wave_sum(lane <= stop ? (uint32_t)s : 0u);
-		if (stop < 64)
+		uint32_t v = 0;
+#pragma unroll
+		for (int k = 0; k < kLookWin; k++)
+			if (k < stop_k || (k == stop_k && lane <= stop_l))
+				v += (uint32_t)s[k];
+		excl += wave_sum(v);
+		if (stop_k < kLookWin)
 			return excl;
-		j -= 64;
+		j -= 64 * kLookWin;
 	}
 }
 
@@ -209,13 +358,15 @@ template <bool FILTER>
 __global__ __launch_bounds__(256) void dst_cache_kernel(DstParams p)
 {
 	extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-	uint32_t *T = smem;                            // 12 x 256 tables (FILTER)
-	uint32_t *S = smem + (FILTER ? 12 * 256 : 0);  // [0] tile, [1..4] wave counts, [5] tile prefix
+	uint32_t *T = smem;                                                    // 12 x 256 (FILTER)
+	uint32_t *B = smem + (FILTER ? 12 * 256 : 0);                          // [wave][iters/32][lane] bits
+	uint32_t *S = B + kDstWaves * (kDstIters / 32) * 64;                   // [0] tile, [1..4] counts, [5] prefix
 	uint32_t CGCK_GLOBAL *ctl = (uint32_t CGCK_GLOBAL *)p.ctl;
 	uint64_t CGCK_GLOBAL *status = (uint64_t CGCK_GLOBAL *)p.status;
 	u32x4_t CGCK_GLOBAL *out = (u32x4_t CGCK_GLOBAL *)p.out;
 	const int lane = threadIdx.x & 63;
 	const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+	uint32_t *Bw = B + wave * (kDstIters / 32) * 64;
 	if (FILTER) {
 		const uint32_t CGCK_GLOBAL *gt = (const uint32_t CGCK_GLOBAL *)p.tab;
 		for (uint32_t i = threadIdx.x; i < 12 * 256; i += 256)
@@ -232,25 +383,30 @@ __global__ __launch_bounds__(256) void dst_cache_kernel(DstParams p)
 		const uint32_t t = __builtin_amdgcn_readfirstlane(S[0]);
 		if (t >= p.ntiles)
 			break;
-		const uint64_t base = (uint64_t)t * (kDstWaves * kDstIters * 64) + (uint64_t)wave * (kDstIters * 64);
+		const uint64_t base = (uint64_t)t * (kDstWaves * 64 * p.iters) + (uint64_t)wave * (64 * p.iters);
+		const uint32_t start = (uint32_t)(base + lane < p.n ? base + lane : 0);
 
-		// Pass 1: which tuples survive (one ballot per 64).
+		// Pass 1: which tuples survive.  Lane bit u of word B[j0/32] = tuple
+		// j*64 + lane of this wave; one LDS word per lane per 32 iterations.
 		Cursor c;
-		cursor_at(c, (uint32_t)(base + lane < p.n ? base + lane : 0), p);
-		uint64_t m[kDstIters];
+		cursor_at<FILTER>(c, start, p, T);
 		uint32_t cnt = 0;
-#pragma unroll
-		for (int j = 0; j < kDstIters; j++) {
-			bool ok = base + (uint64_t)(j * 64 + lane) < p.n;
-			if (FILTER && ok) {
-				const uint32_t h = tuple_hash(T, p.faddr_min + c.fa, p.laddr_min + c.la, kEphMin + c.lp,
-							      p.hconst) & 0x7Fu;
-				ok = ((h < 64 ? p.pass_lo >> h : p.pass_hi >> (h - 64)) & 1u) != 0;
+		// tuples of this wave still below n, from this lane's first one
+		const uint64_t left = base < p.n ? p.n - base : 0;
+		const uint32_t rem = left > 0xffffffffu ? 0xffffffffu : (uint32_t)left;
+		for (uint32_t j0 = 0; j0 < p.iters; j0 += 32) { // iters is a multiple of 32
+			uint32_t bits = 0;
+#pragma unroll 8
+			for (uint32_t u = 0; u < 32; u++) {
+				const bool in = (j0 + u) * 64 + lane < rem;
+				const bool ok = FILTER ? in & rss_pass(c, p, T) : in;
+				bits |= (ok ? 1u : 0u) << u;
+				cursor_step64<FILTER>(c, p, T);
 			}
-			m[j] = __ballot(ok);
-			cnt += __builtin_popcountll(m[j]);
-			cursor_step64(c, p);
+			Bw[(j0 / 32) * 64 + lane] = bits;
+			cnt += __builtin_popcount(bits);
 		}
+		cnt = wave_sum(cnt);
 		if (lane == 0)
 			S[1 + wave] = cnt;
 		__syncthreads();
@@ -285,39 +441,77 @@ __global__ __launch_bounds__(256) void dst_cache_kernel(DstParams p)
 		const uint32_t E = __builtin_amdgcn_readfirstlane(S[5]);
 
 		// Pass 2: write this tile's survivors at E + their rank, below cap.
-		if (E < p.cap) {
-			cursor_at(c, (uint32_t)(base + lane < p.n ? base + lane : 0), p);
+		if (E < p.cap && cnt) {
+			cursor_at<false>(c, start, p, T);
 			uint32_t pos = E + wexcl;
-#pragma unroll
-			for (int j = 0; j < kDstIters; j++) {
-				const uint32_t at = pos + lanes_below(m[j]);
-				if (((m[j] >> lane) & 1u) && at < p.cap) {
-					const uint32_t fa = p.faddr_min + c.fa, la = p.laddr_min + c.la;
-					const uint32_t lpb = __builtin_bswap16((uint16_t)(kEphMin + c.lp));
-					const uint32_t fab = __builtin_bswap32(fa);
-					// SO_HASH(faddr, lport, fport), subr.h:179-180
-					const uint32_t soh = fab ^ (fab >> 16) ^ __builtin_bswap16((uint16_t)(lpb ^ p.fport_be));
-					const u32x4_t e = {__builtin_bswap32(la), fab, lpb | (p.fport_be << 16), soh};
-					out[at] = e;
+			for (uint32_t j0 = 0; j0 < p.iters && pos < p.cap; j0 += 32) {
+				const uint32_t bits = Bw[(j0 / 32) * 64 + lane];
+				for (uint32_t u = 0; u < 32; u++) {
+					const bool ok = (bits >> u) & 1u;
+					const uint64_t m = __ballot(ok);
+					const uint32_t at = pos + lanes_below(m);
+					if (ok && at < p.cap) {
+						const uint32_t fa = p.faddr_min + c.fa, la = p.laddr_min + c.la;
+						const uint32_t lpb = __builtin_bswap16((uint16_t)(kEphMin + c.lp));
+						const uint32_t fab = __builtin_bswap32(fa);
+						// SO_HASH(faddr, lport, fport), subr.h:179-180
+						const uint32_t soh = fab ^ (fab >> 16) ^ __builtin_bswap16((uint16_t)(lpb ^ p.fport_be));
+						const u32x4_t e = {__builtin_bswap32(la), fab, lpb | (p.fport_be << 16), soh};
+						out[at] = e;
+					}
+					pos += __builtin_popcountll(m);
+					cursor_step64<false>(c, p, T);
 				}
-				pos += __builtin_popcountll(m[j]);
-				cursor_step64(c, p);
 			}
 		}
-		__syncthreads(); // S is rewritten by the next tile
+		__syncthreads(); // S and M are rewritten by the next tile
 	}
 }
 
+// Expected tuples scanned before `cap` survivors exist: cap / (fraction of
+// the 128 hash values that pass), or all of them.
+static uint64_t dst_expected(uint32_t n, uint32_t cap, bool filter, uint64_t pass_lo, uint64_t pass_hi)
+{
+	const uint64_t pass = filter ? __builtin_popcountll(pass_lo) + __builtin_popcountll(pass_hi) : 128;
+	const uint64_t want = pass ? (uint64_t)cap * 128 / pass + cap / 4 : n;
+	return want < n ? want : n;
+}
+
+// Tile = 256 x iters tuples: 64 iterations per wave for long enumerations
+// (the look-back is amortised over 16384 tuples), fewer for short ones so
+// that they still spread over the chip (the reference's default, one laddr
+// and one faddr, is 60536 tuples).
+uint32_t dst_iters(uint32_t n, uint32_t cap, bool filter, uint64_t pass_lo, uint64_t pass_hi, int num_cus)
+{
+	const uint64_t work = dst_expected(n, cap, filter, pass_lo, pass_hi);
+	const uint64_t per = work / ((uint64_t)num_cus * 256);
+	if (const char *e = getenv("CGCK_DST_ITERS")) // A/B sweeps (tools/rss_bench.py)
+		return (uint32_t)atoi(e);
+	uint32_t it = 32;
+	while (it < (uint32_t)kDstIters && it < per)
+		it *= 2;
+	return it;
+}
+
+// Grid: enough workgroups for the expected work (a workgroup in flight
+// finishes the tile it drew), at most 4 per CU.
 hipError_t launch_dst_cache(const DstParams &p, int num_cus, hipStream_t st)
 {
 	if (p.ntiles == 0)
 		return hipSuccess;
-	const uint32_t cap = (uint32_t)num_cus * 8;
-	const dim3 g(p.ntiles < cap ? p.ntiles : cap), b(256);
+	const uint64_t tile = (uint64_t)kDstWaves * 64 * p.iters;
+	uint64_t g = (dst_expected(p.n, p.cap, p.filter, p.pass_lo, p.pass_hi) + 2 * tile - 1) / tile;
+	uint64_t gmax = (uint64_t)num_cus * 4;
+	if (const char *e = getenv("CGCK_DST_WGS")) // A/B sweeps: workgroups per CU
+		gmax = (uint64_t)num_cus * atoi(e);
+	g = g < 8 ? 8 : g;
+	g = g > gmax ? gmax : g;
+	g = g > p.ntiles ? p.ntiles : g;
+	const size_t lds = (p.filter ? 12 * 256 * 4 : 0) + kDstMaskBytes + 64;
 	if (p.filter)
-		hipLaunchKernelGGL(dst_cache_kernel<true>, g, b, (12 * 256 + 16) * 4, st, p);
+		hipLaunchKernelGGL(dst_cache_kernel<true>, dim3((unsigned)g), dim3(256), lds, st, p);
 	else
-		hipLaunchKernelGGL(dst_cache_kernel<false>, g, b, 16 * 4, st, p);
+		hipLaunchKernelGGL(dst_cache_kernel<false>, dim3((unsigned)g), dim3(256), lds, st, p);
 	return hipGetLastError();
 }
 
