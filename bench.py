@@ -45,7 +45,8 @@ def parse():
     ap.add_argument("--no-extra", action="store_true", help="skip the 64 B / IMIX lines")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--only", choices=["1500", "64", "imix"], default=None,
+    ap.add_argument("--no-rss", action="store_true", help="skip the Toeplitz RSS lines")
+    ap.add_argument("--only", choices=["1500", "64", "imix", "rss"], default=None,
                     help="time one workload only (profiling runs)")
     return ap.parse_args()
 
@@ -140,6 +141,88 @@ def bench_imix(torch, dist, eng, cgck, n, plan, steps, warmup):
     return wall, ev_ms, nbytes
 
 
+RSS_KEY = bytes.fromhex("6d5a56da255b0ec24167253d43a38fb0d0ca2bcbae7b30b477cb2da38030f20c6a42b73bbeac01fa")
+RSS_TUPLES = 64 << 20      # batched-hash tuples per GPU (805 MB: well past the 256 MB MALL)
+RSS_DST = (4, 256, 8)      # dst-cache enumeration: laddrs x faddrs x 60536 ports, queues
+
+
+def bench_rss(torch, dist, eng, cgck, plan, steps, warmup):
+    """SURVEY §8(f) rank 4.  (a) cgck_toeplitz over RSS_TUPLES dense 12-byte
+    tuples in HBM (rss_hash4 layout, mask 0x7F): 16 algorithmic bytes per
+    tuple.  (b) cgck_dst_cache over a full enumeration (no early cap):
+    rank r builds the cache of RSS queue r % queues, as con-gen's thread r
+    does (con-gen.c:337-342)."""
+    import numpy as np
+    n = RSS_TUPLES
+    d = cgck.DeviceBuffer(n * 12 + 64)
+    o = cgck.DeviceBuffer(4 * n)
+    eng.synth_strided(d.ptr, (n * 12) // 1500, 1500, 1500, plan["seed"])
+    eng.sync()
+    wall_h, ev_h = timed(torch, dist, eng, cgck,
+                         lambda: eng.toeplitz(d.ptr, n, 12, 12, RSS_KEY, o.ptr, mask=0x7F),
+                         steps, warmup)
+    # parity spot check of this run: first 4096 tuples vs the oracle
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    host = np.zeros(4096 * 12, np.uint8)
+    got = np.zeros(4096, np.uint32)
+    d.download(host, stream=eng.stream)
+    o.download(got, stream=eng.stream)
+    eng.sync()
+    exp = oracle.port().toeplitz_batch(host, 4096, 12, 12, np.frombuffer(RSS_KEY, np.uint8), mask=0x7F)
+    bad_h = int(np.count_nonzero(got != exp))
+    d.free()
+    o.free()
+
+    nl, nf, qn = RSS_DST
+    qi = plan["first"] // plan["n"] % qn
+    key = np.frombuffer(RSS_KEY, np.uint8)
+    prm = cgck.Engine.dst_params((0x0A000001, 0x0A000000 + nl), (0x0A010000, 0x0A010000 + nf - 1),
+                                 0x5000, qn, qi, key)
+    tuples = nl * nf * 60536
+    out = cgck.DeviceBuffer(16 * tuples // qn * 2)
+    cnt = cgck.DeviceBuffer(4)
+    cap = tuples // qn * 2
+    wall_d, ev_d = timed(torch, dist, eng, cgck, lambda: eng.dst_cache(prm, out.ptr, cap, cnt.ptr),
+                         steps, warmup)
+    c = np.zeros(1, np.uint32)
+    cnt.download(c, stream=eng.stream)
+    eng.sync()
+    out.free()
+    cnt.free()
+    return {"hash": (wall_h, ev_h, n, bad_h), "dst": (wall_d, ev_d, tuples, int(c[0]))}
+
+
+def cpu_rss(seconds):
+    """The reference loop (con-gen.c:291-360, restated in oracle/rss_oracle.c)
+    calling the REFERENCE's own rss_hash4 (oracle/_ref/libref_rss.so) when
+    built, on one pinned core: 1 laddr x 16 faddrs x 60536 ports, 8 queues."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    P = oracle.port()
+    R = oracle.reference_rss()
+    fn = R.fn_rss_hash4() if R else None
+    key = np.frombuffer(RSS_KEY, np.uint8)
+    cpus = sorted(os.sched_getaffinity(0))
+    old = set(cpus)
+    tuples, reps, t = 16 * 60536, 0, 0.0
+    try:
+        os.sched_setaffinity(0, {cpus[len(cpus) // 2]})
+        while t < seconds:
+            t0 = time.perf_counter()
+            P.dst_cache(0x0A000001, 0x0A000001, 0x0A010000, 0x0A01000F, 0x5000, 8, 3, key,
+                        1 << 30, hash_fn=fn)
+            t += time.perf_counter() - t0
+            reps += 1
+    finally:
+        os.sched_setaffinity(0, old)
+    return {"value": tuples * reps / t / 1e9, "unit": "Gtuple/s", "cores": 1,
+            "kind": "reference" if R else "port",
+            "sample": f"dst-cache loop over 1 laddr x 16 faddrs x 60536 ports (968576 tuples), "
+                      f"8 queues, {reps} passes, {t:.1f} s on 1 pinned core"}
+
+
 def cpu_baseline(seconds):
     """The reference's checksum loop on this box's host cores (rank 0, N = 1):
     in_cksum(ip, 20) + udp_cksum(ip, 1480) per 1500 B packet, dense stride,
@@ -222,9 +305,14 @@ def main():
         wall, ev_ms, nbytes = bench_imix(torch, dist, eng, cgck, n, plan, args.steps, args.warmup)
         res["imix"] = (wall, ev_ms, nbytes)
 
-    cpu = None
+    if not args.no_rss and args.only in (None, "rss"):
+        res["rss"] = bench_rss(torch, dist, eng, cgck, plan, args.steps, args.warmup)
+
+    cpu = cpu_r = None
     if dist.rank == 0 and dist.world == 1 and not args.no_cpu:
         cpu = cpu_baseline(args.cpu_seconds)
+        if "rss" in res:
+            cpu_r = cpu_rss(min(3.0, args.cpu_seconds))
     dist.barrier()
 
     if dist.rank == 0:
@@ -269,10 +357,29 @@ def main():
             wall, ev_ms, nbytes = res["imix"]
             extra["imix"] = line(0, wall, ev_ms, nbytes + 16 * n)
             extra["imix"]["gb_s"] = nbytes * W * K / wall / 1e9
+        if "rss" in res:
+            wall_h, ev_h, nt, bad_h = res["rss"]["hash"]
+            wall_d, ev_d, td, written = res["rss"]["dst"]
+            ach = nt * 16 / (ev_h * 1e-3)
+            extra["rss_hash"] = {
+                "workload": f"{nt} dense 12-byte tuples per GPU, rss_hash4 (Toeplitz, 40-byte key, "
+                            "mask 0x7F) each", "kernel": "toeplitz12x4_kernel<false>",
+                "gtuple_s": nt * W * K / wall_h / 1e9, "ms_per_step": wall_h / K * 1e3,
+                "kernel_ms": ev_h, "achieved_gbs": ach / 1e9, "hbm_frac": ach / HBM_PEAK,
+                "algorithmic_bytes_per_launch": nt * 16,
+                "parity": {"checked": 4096, "mismatches": bad_h}}
+            extra["dst_cache"] = {
+                "workload": f"thread_init_dst_cache enumeration of {td} tuples per GPU "
+                            f"({RSS_DST[0]} laddrs x {RSS_DST[1]} faddrs x 60536 ports), "
+                            f"{RSS_DST[2]} RSS queues, no early cap", "kernel": "dst_cache_kernel<true>",
+                "gtuple_s": td * W * K / wall_d / 1e9, "ms_per_step": wall_d / K * 1e3,
+                "kernel_ms": ev_d, "entries_written": written}
+            if cpu_r:
+                extra["dst_cache"]["cpu_baseline"] = cpu_r
         if extra:
             out["extra"] = extra
-        if "value" not in out:   # --only 64 / imix profiling runs
-            k = "64B" if "64B" in extra else "imix"
+        if "value" not in out:   # --only 64 / imix / rss profiling runs
+            k = "64B" if "64B" in extra else "imix" if "imix" in extra else "rss_hash"
             out["value"] = extra[k]["gpkt_s"]
             out["config"] = {"workload": k}
         if cpu:
