@@ -8,6 +8,7 @@ hipError_t launch_lpp(const KParams &p, int num_cus, bool nt, int shape, hipStre
 hipError_t launch_slot(const KParams &p, int num_cus, bool nt, hipStream_t st);
 hipError_t launch_lppp(const KParams &p, int num_cus, bool nt, hipStream_t st);
 hipError_t launch_slot2(const KParams &p, int num_cus, bool nt, hipStream_t st);
+hipError_t launch_lpa(const KParams &p, int num_cus, bool nt, hipStream_t st);
 
 // `kernel` = variant | flags (include/cgck.h is agnostic of this; $CGCK_KERNEL
 // overrides it for A/B runs):
@@ -15,7 +16,9 @@ hipError_t launch_slot2(const KParams &p, int num_cus, bool nt, hipStream_t st);
 //     packet, 3 lane per 128-byte slot, 4 software-pipelined lane per packet,
 //     5..8 lane per packet shapes 1..3, 0 (6 clamped, 6 predicated,
 //     4 predicated, 4 clamped chunks up front), 9 lane per 128-byte slot
-//     pipelined two deep (the default for mid-size packets);
+//     pipelined two deep (the default for mid-size packets), 10 lane per
+//     packet for aligned fixed-length strided 20..64-byte packets, A/B
+//     pipelined (the default there);
 //   kNT (bit 4) nontemporal loads, kContig (bit 5) contiguous block ranges,
 //   kExplicit (bit 6) take bits 4-5 as given instead of the measured defaults.
 // len_hint = the batch's packet length (strided) or typical length (descriptors).
@@ -26,10 +29,15 @@ hipError_t launch_cksum(const KParams &p0, uint32_t len_hint, int num_cus, int k
 	KParams p = p0;
 	const bool lane_ok = !(p.flags & kFlagNoLenCheck);
 	int variant = kernel & 15;
+	// aligned fixed-length strided batch of 20..64-byte packets (the 64 B config)
+	const bool lpa_ok = lane_ok && !p.desc && p.ip_len >= 20 && p.ip_len <= 64 &&
+			    ((reinterpret_cast<uintptr_t>(p.base) | p.stride | p.l3_off) & 15) == 0;
 	if (variant == 0)
-		variant = !lane_ok ? 1 : len_hint >= kGroupFromLen ? 1 : len_hint <= kLppUpToLen ? 2 : 9;
+		variant = !lane_ok ? 1 : lpa_ok ? 10 : len_hint >= kGroupFromLen ? 1 : len_hint <= kLppUpToLen ? 2 : 9;
 	if (variant >= 2 && !lane_ok)
 		variant = 1;
+	if (variant == 10 && !lpa_ok)
+		variant = 2;
 	bool nt, contig;
 	if (kernel & kExplicit) {
 		nt = kernel & kNT;
@@ -59,6 +67,8 @@ hipError_t launch_cksum(const KParams &p0, uint32_t len_hint, int num_cus, int k
 		return launch_lppp(p, num_cus, nt, st);
 	case 9:
 		return launch_slot2(p, num_cus, nt, st);
+	case 10:
+		return launch_lpa(p, num_cus, nt, st);
 	default:
 		return launch_group(p, len_hint, num_cus, nt, st);
 	}
