@@ -40,6 +40,7 @@ def main():
         os.environ["CGCK_KERNEL"] = v
         engines[v] = cgck.Engine(0)
     os.environ.pop("CGCK_KERNEL", None)
+    e_probe = cgck.Engine(0)   # default family: probe variant 0 (plain streaming read)
     e0 = next(iter(engines.values()))
     work = {}
     for w in args.workloads.split(","):
@@ -79,11 +80,12 @@ def main():
             for v, (e, fl, o) in cells.items():
                 if (w, v) not in res:
                     continue
-                fn(e, fl, o)  # warm
-                e.record(a)
+                ee = e_probe if w == "probe" else e
+                fn(ee, fl, o)  # warm
+                ee.record(a)
                 for _ in range(args.launches):
-                    fn(e, fl, o)
-                e.record(b)
+                    fn(ee, fl, o)
+                ee.record(b)
                 ms = cgck.Engine.elapsed_ms(a, b) / args.launches
                 if r > 0:
                     res[(w, v)].append(algo / (ms * 1e-3))
