@@ -265,14 +265,14 @@ def cpu_baseline(seconds):
     }
 
 
-def load_traffic():
-    """Per-launch HBM bytes of the dominant kernel from the committed PMC
+def load_traffic(key="1500"):
+    """Per-launch HBM bytes of a workload's kernel from the committed PMC
     summary (profiles/pmc_latest.json, written by tools/pmc_traffic.py from
     separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench)."""
     p = os.path.join(ROOT, "profiles", "pmc_latest.json")
     try:
         with open(p) as f:
-            return json.load(f).get("bytes_per_launch_1500")
+            return json.load(f).get(f"bytes_per_launch_{key}")
     except (OSError, ValueError):
         return None
 
@@ -345,7 +345,7 @@ def main():
                 "roofline": {"bound": "hbm", "achieved": L["achieved_gbs"], "peak": HBM_PEAK / 1e9,
                              "unit": "GB/s", "frac": L["hbm_frac"],
                              "traffic": traffic,
-                             "kernel": "cksum_kernel<16,6,1,false>",
+                             "kernel": "cksum_kernel<16, 6, 1, false, true>",
                              "algorithmic_bytes_per_launch": algo,
                              "kernel_ms_hip_events": ev_ms},
                 "parity": res.get("parity_1500"),
@@ -353,10 +353,12 @@ def main():
         extra = {}
         if "64" in res:
             extra["64B"] = line(64, *res["64"])
+            extra["64B"].update({"kernel": "lpa_kernel<false>", "traffic": load_traffic("64")})
         if "imix" in res:
             wall, ev_ms, nbytes = res["imix"]
             extra["imix"] = line(0, wall, ev_ms, nbytes + 16 * n)
             extra["imix"]["gb_s"] = nbytes * W * K / wall / 1e9
+            extra["imix"].update({"kernel": "slot2_kernel<true, false>", "traffic": load_traffic("imix")})
         if "rss" in res:
             wall_h, ev_h, nt, bad_h = res["rss"]["hash"]
             wall_d, ev_d, td, written = res["rss"]["dst"]
@@ -366,7 +368,7 @@ def main():
                             "mask 0x7F) each", "kernel": "toeplitz12x4_kernel<false>",
                 "gtuple_s": nt * W * K / wall_h / 1e9, "ms_per_step": wall_h / K * 1e3,
                 "kernel_ms": ev_h, "achieved_gbs": ach / 1e9, "hbm_frac": ach / HBM_PEAK,
-                "algorithmic_bytes_per_launch": nt * 16,
+                "algorithmic_bytes_per_launch": nt * 16, "traffic": load_traffic("rss_hash"),
                 "parity": {"checked": 4096, "mismatches": bad_h}}
             extra["dst_cache"] = {
                 "workload": f"thread_init_dst_cache enumeration of {td} tuples per GPU "

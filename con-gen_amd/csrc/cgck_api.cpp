@@ -66,7 +66,7 @@ struct cgck_ctx {
 	size_t d_bytes_cap;
 	uint8_t *d_aux; // descriptors | out | verdict
 	size_t d_aux_cap;
-	void *d_zero; // 64 zero bytes (KParams.zero)
+	void *d_zero; // kZeroBytes zero bytes (KParams.zero)
 	// Toeplitz byte tables of the last key used (cgck_rss.hip)
 	uint32_t *d_rss_tab;
 	size_t d_rss_tab_cap;
@@ -146,14 +146,15 @@ extern "C" int cgck_ctx_create(int device, cgck_ctx_t **out)
 	c->desc_len_hint = 1500;
 	if (const char *kf = getenv("CGCK_KERNEL"))
 		c->family = !strcmp(kf, "group") ? 1 : !strcmp(kf, "lpp") ? 2 : !strcmp(kf, "slot") ? 3
-			  : !strcmp(kf, "slot2") ? 9 : !strcmp(kf, "lpa") ? 10
+			  : !strcmp(kf, "slot2") ? 9 : !strcmp(kf, "lpa") ? 10 : !strcmp(kf, "str") ? 11
 			  : !strncmp(kf, "lpp", 3) ? atoi(kf + 3) : atoi(kf);
 	hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
 	if (e != hipSuccess) {
 		free(c);
 		return set_err(-EIO, "hipStreamCreate: %s", hipGetErrorString(e));
 	}
-	if ((e = hipMalloc(&c->d_zero, 64)) != hipSuccess || (e = hipMemset(c->d_zero, 0, 64)) != hipSuccess) {
+	if ((e = hipMalloc(&c->d_zero, kZeroBytes)) != hipSuccess ||
+	    (e = hipMemset(c->d_zero, 0, kZeroBytes)) != hipSuccess) {
 		(void)hipStreamDestroy(c->stream);
 		free(c);
 		return set_err(-EIO, "zero chunk: %s", hipGetErrorString(e));

@@ -242,4 +242,38 @@ __device__ __forceinline__ uint32_t ocsub(uint32_t x, uint32_t y)
 	return fold16(x + (0xffffu - y));
 }
 
+// --------------------------------------------------------------------------
+// Lane-group partial sums (cgck_group.hip, cgck_stream.hip)
+// --------------------------------------------------------------------------
+
+// Per-packet, per-lane partial state.
+struct Part {
+	uint32_t tot, ip, ps, fld; // fld = stored ip field | stored l4 field << 16 (abs frame)
+};
+
+// Accumulate one loaded chunk (k = chunk index inside the packet).
+template <bool HDR>
+__device__ __forceinline__ void eat(Part &pt, uint4 w, int k, int q, int len, int hl, int fo,
+				    uint32_t flags)
+{
+	const int co = k * 16;
+	if (HDR && co < q + 80) {
+		// Header zone: stored fields, optional zeroing, header sums.
+		if (flags & (CGCK_VERIFY | CGCK_ZERO_FIELDS)) {
+			uint32_t f = msum(w, co, q + 10, q + 12, 0);
+			uint32_t g = fo >= 0 ? msum(w, co, q + hl + fo, q + hl + fo + 2, 0) : 0u;
+			pt.fld += f | (g << 16);
+			zero_bytes(w, co, q + 10, q + 12);
+			if (fo >= 0)
+				zero_bytes(w, co, q + hl + fo, q + hl + fo + 2);
+		}
+		pt.ip = msum(w, co, q, q + hl, pt.ip);
+		pt.ps = msum(w, co, q + 12, q + 20, pt.ps);
+	}
+	if (co >= q && co + 16 <= q + len)
+		pt.tot = sum4(w, pt.tot);
+	else
+		pt.tot = msum(w, co, q, q + len, pt.tot);
+}
+
 } // namespace cgck

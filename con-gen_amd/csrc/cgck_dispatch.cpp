@@ -9,6 +9,8 @@ hipError_t launch_slot(const KParams &p, int num_cus, bool nt, hipStream_t st);
 hipError_t launch_lppp(const KParams &p, int num_cus, bool nt, hipStream_t st);
 hipError_t launch_slot2(const KParams &p, int num_cus, bool nt, hipStream_t st);
 hipError_t launch_lpa(const KParams &p, int num_cus, bool nt, hipStream_t st);
+hipError_t launch_stream(const KParams &p, int num_cus, hipStream_t st);
+bool stream_ok(const KParams &p);
 
 // `kernel` = variant | flags (include/cgck.h is agnostic of this; $CGCK_KERNEL
 // overrides it for A/B runs):
@@ -18,7 +20,9 @@ hipError_t launch_lpa(const KParams &p, int num_cus, bool nt, hipStream_t st);
 //     4 predicated, 4 clamped chunks up front), 9 lane per 128-byte slot
 //     pipelined two deep (the default for mid-size packets), 10 lane per
 //     packet for aligned fixed-length strided 20..64-byte packets, A/B
-//     pipelined (the default there);
+//     pipelined (the default there), 11 the lane-group kernel fed by
+//     LDS-DMA (strided 20..1520-byte packets, no in-place writes; the
+//     default for the 1500 B config);
 //   kNT (bit 4) nontemporal loads, kContig (bit 5) contiguous block ranges,
 //   kExplicit (bit 6) take bits 4-5 as given instead of the measured defaults.
 // len_hint = the batch's packet length (strided) or typical length (descriptors).
@@ -32,12 +36,17 @@ hipError_t launch_cksum(const KParams &p0, uint32_t len_hint, int num_cus, int k
 	// aligned fixed-length strided batch of 20..64-byte packets (the 64 B config)
 	const bool lpa_ok = lane_ok && !p.desc && p.ip_len >= 20 && p.ip_len <= 64 &&
 			    ((reinterpret_cast<uintptr_t>(p.base) | p.stride | p.l3_off) & 15) == 0;
-	if (variant == 0)
+	if (variant == 0) {
 		variant = !lane_ok ? 1 : lpa_ok ? 10 : len_hint >= kGroupFromLen ? 1 : len_hint <= kLppUpToLen ? 2 : 9;
+		if (variant == 1 && len_hint >= kGroupFromLen && kDefaultStream && stream_ok(p))
+			variant = 11;
+	}
 	if (variant >= 2 && !lane_ok)
 		variant = 1;
 	if (variant == 10 && !lpa_ok)
 		variant = 2;
+	if (variant == 11 && !stream_ok(p))
+		variant = 1;
 	bool nt, contig;
 	if (kernel & kExplicit) {
 		nt = kernel & kNT;
@@ -69,6 +78,8 @@ hipError_t launch_cksum(const KParams &p0, uint32_t len_hint, int num_cus, int k
 		return launch_slot2(p, num_cus, nt, st);
 	case 10:
 		return launch_lpa(p, num_cus, nt, st);
+	case 11:
+		return launch_stream(p, num_cus, st);
 	default:
 		return launch_group(p, len_hint, num_cus, nt, st);
 	}

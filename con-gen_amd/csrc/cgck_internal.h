@@ -14,6 +14,10 @@ constexpr uint32_t kFlagNoLenCheck = 1u << 15;
 
 constexpr uint32_t kImixCycleBytes = 4252; // 7*64 + 4*576 + 1500
 
+// Zeroed device bytes per context: 64 lines of 64 B, so dummy loads can be
+// spread over L2 channels instead of all hitting one line.
+constexpr uint32_t kZeroBytes = 64 * 64;
+
 struct KParams {
 	const uint8_t *base;
 	const cgck_desc_t *desc; // nullptr: strided batch
@@ -26,7 +30,7 @@ struct KParams {
 	uint8_t *verdict;
 	uint32_t *bad;
 	uint32_t contig; // set by the launcher: contiguous block ranges
-	const void *zero; // 64 zero bytes of device memory (safe target for clamped loads)
+	const void *zero; // kZeroBytes zero bytes of device memory (safe target for clamped loads)
 };
 
 // Kernel selection flags (see cgck_dispatch.cpp) and the measured defaults
@@ -40,6 +44,10 @@ constexpr uint32_t kLppUpToLen = 128;    // lane-per-packet up to here, lane-per
 constexpr int kDefaultLppShape = 2;       // see launch_lpp (6 chunks up front, predicated: best on 64 B)
 constexpr bool kDefaultGroupNT = true, kDefaultGroupContig = true;
 constexpr bool kDefaultLaneNT = false, kDefaultLaneContig = false;
+// The LDS-DMA stream kernel (cgck_stream.hip) for dense 1500 B batches: off
+// by default — measured 76.9 % vs 77.9 % of HBM peak for the register-load
+// group kernel on the same box (tools/str_sweep.sh).  CGCK_KERNEL=str.
+constexpr bool kDefaultStream = false;
 
 // Toeplitz RSS hash (cgck_rss.hip; subr.c:482-530).  `tab` = cnt x 256 u32
 // byte tables derived from the key on the host (rss_tables in cgck_api.cpp).

@@ -508,11 +508,14 @@ struct Quad {
 };
 
 template <bool NT>
-__device__ __forceinline__ void lpa_load(const KParams &p, uint64_t it, int nch, Quad &q)
+__device__ __forceinline__ void lpa_load(const KParams &p, uint64_t it, bool live, int nch, Quad &q)
 {
 	uint64_t k = it * 256 + threadIdx.x;
 	k = k < p.n ? k : p.n - 1;
-	const uint4 *c0 = reinterpret_cast<const uint4 *>(p.base + k * p.stride + p.l3_off);
+	// past the block's last group: a zero line of the context, one of 64 by
+	// block, instead of re-reading packet bytes that have left the L2
+	const uint4 *c0 = live ? reinterpret_cast<const uint4 *>(p.base + k * p.stride + p.l3_off)
+			       : reinterpret_cast<const uint4 *>((const uint8_t *)p.zero + (blockIdx.x & 63) * 64);
 #pragma unroll
 	for (int i = 0; i < 4; ++i)
 		q.c[i] = ld<NT>(c0 + (i < nch ? i : nch - 1));
@@ -593,18 +596,18 @@ __global__ __launch_bounds__(256) void lpa_kernel(KParams p)
 	uint64_t it = blockIdx.x;
 	if (it >= NI)
 		return;
-	// loads are never skipped: past the end they re-read the last group
-	// (clamped, L2-hot), so the loop has no load under a branch
+	// loads are never skipped (past the end they read a zero line), so the
+	// loop has no load under a branch
 	Quad A, B;
-	lpa_load<NT>(p, it, nch, A);
+	lpa_load<NT>(p, it, true, nch, A);
 	for (;;) {
 		const bool hasB = it + S < NI;
-		lpa_load<NT>(p, hasB ? it + S : it, nch, B);
+		lpa_load<NT>(p, it + S, hasB, nch, B);
 		lpa_reduce<NT>(p, it, len, nch, A);
 		if (!hasB)
 			break;
 		const bool hasA = it + 2 * S < NI;
-		lpa_load<NT>(p, hasA ? it + 2 * S : it + S, nch, A);
+		lpa_load<NT>(p, it + 2 * S, hasA, nch, A);
 		lpa_reduce<NT>(p, it + S, len, nch, B);
 		if (!hasA)
 			break;

@@ -352,6 +352,67 @@ __global__ __launch_bounds__(256) void probe_wave4_kernel(const uint4 *src, uint
 	}
 }
 
+// LDS-DMA streaming probe (MI355X_MICROARCH.md 'ldsdma-fill': 6.4 TB/s
+// default policy, 6.5-6.8 nt chip-wide).  One wave per workgroup streams
+// its contiguous range through a ring of D 4 KiB slots: 4
+// global_load_lds_dwordx4 per slot (1 KiB each, lane l -> bytes 16l), a
+// counted vmcnt + s_barrier before the slot is read back with ds_read_b128
+// (the RAW rule for LDS-DMA data), and a sum so the data is used.
+template <bool NT>
+__device__ __forceinline__ void glds16(const void *gsrc, uint32_t lds_dst)
+{
+	uint32_t keep;
+	if (NT)
+		asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\t"
+			     "s_mov_b32 m0, %0"
+			     : "=&s"(keep)
+			     : "v"(gsrc), "s"(lds_dst)
+			     : "memory");
+	else
+		asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
+			     "s_mov_b32 m0, %0"
+			     : "=&s"(keep)
+			     : "v"(gsrc), "s"(lds_dst)
+			     : "memory");
+}
+
+template <int D, bool NT>
+__global__ __launch_bounds__(64) void probe_glds_kernel(const uint4 *src, uint64_t n16, uint32_t *sink)
+{
+	extern __shared__ __attribute__((aligned(16))) uint4 ring[]; // D x 256 uint4
+	const int lane = threadIdx.x;
+	const uint64_t nst = n16 / 256; // 4 KiB steps
+	const uint64_t per = (nst + gridDim.x - 1) / gridDim.x;
+	const uint64_t s0 = (uint64_t)blockIdx.x * per, s1 = s0 + per < nst ? s0 + per : nst;
+	if (s0 >= s1)
+		return;
+	const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)ring);
+	auto issue = [&](uint64_t st, uint32_t slot) {
+		const uint4 *g = src + st * 256 + lane;
+#pragma unroll
+		for (int j = 0; j < 4; ++j)
+			glds16<NT>(g + 64 * j, lds0 + slot * 4096 + 1024 * j);
+	};
+#pragma unroll
+	for (int d = 0; d < D - 1; ++d)
+		issue(s0 + d < s1 ? s0 + d : s1 - 1, d);
+	uint32_t acc = 0;
+	for (uint64_t s = s0; s < s1; ++s) {
+		const uint32_t slot = (uint32_t)((s - s0) % D);
+		// the slot refilled here was read in the previous step (lgkmcnt(0) below)
+		issue(s + D - 1 < s1 ? s + D - 1 : s1 - 1, (uint32_t)((s - s0 + D - 1) % D));
+		asm volatile("s_waitcnt vmcnt(%0)" ::"i"((D - 1) * 4) : "memory");
+		__builtin_amdgcn_s_barrier();
+#pragma unroll
+		for (int j = 0; j < 4; ++j)
+			acc = sum4(ring[slot * 256 + 64 * j + lane], acc);
+		asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+	}
+	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+	if (acc == 0x12345678u)
+		sink[0] = acc;
+}
+
 hipError_t launch_probe_read(const void *src, uint64_t bytes, uint32_t *sink, int num_cus, int variant,
 			     hipStream_t st)
 {
@@ -378,6 +439,12 @@ hipError_t launch_probe_read(const void *src, uint64_t bytes, uint32_t *sink, in
 	case 32: hipLaunchKernelGGL((probe_wave4_kernel<1>), g, b, 0, st, sp, n16, sink); return hipGetLastError();
 	case 33: hipLaunchKernelGGL((probe_wave4_kernel<2>), g, b, 0, st, sp, n16, sink); return hipGetLastError();
 	case 34: hipLaunchKernelGGL((probe_wave4_kernel<3>), g, b, 0, st, sp, n16, sink); return hipGetLastError();
+	case 40: hipLaunchKernelGGL((probe_glds_kernel<4, false>), dim3(num_cus * 8), dim3(64), 4 * 4096, st, sp, n16, sink); return hipGetLastError();
+	case 41: hipLaunchKernelGGL((probe_glds_kernel<4, true>), dim3(num_cus * 8), dim3(64), 4 * 4096, st, sp, n16, sink); return hipGetLastError();
+	case 42: hipLaunchKernelGGL((probe_glds_kernel<8, false>), dim3(num_cus * 4), dim3(64), 8 * 4096, st, sp, n16, sink); return hipGetLastError();
+	case 43: hipLaunchKernelGGL((probe_glds_kernel<8, true>), dim3(num_cus * 4), dim3(64), 8 * 4096, st, sp, n16, sink); return hipGetLastError();
+	case 44: hipLaunchKernelGGL((probe_glds_kernel<4, true>), dim3(num_cus * 4), dim3(64), 4 * 4096, st, sp, n16, sink); return hipGetLastError();
+	case 45: hipLaunchKernelGGL((probe_glds_kernel<8, true>), dim3(num_cus * 8), dim3(64), 8 * 4096, st, sp, n16, sink); return hipGetLastError();
 	default: break;
 	}
 	const uint4 *s = reinterpret_cast<const uint4 *>(src);

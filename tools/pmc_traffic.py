@@ -14,13 +14,17 @@ import sys
 
 KERNELS = {
     "1500": "cksum_kernel<16, 6, 1, false, true>",
-    "64": "lpp_kernel<false, false, 6, false>",
-    "imix": "slot2_kernel<true, false, 2, 1>",
+    "64": "lpa_kernel<false>",
+    "imix": "slot2_kernel<true, false>",
+    "rss_hash": "toeplitz12x4_kernel<false>",
+    "dst_cache": "dst_cache_kernel<true>",
 }
 # bench.py's batches: 16M packets; reads + 12 B descriptor (IMIX) + 4 B output
 N = 16 << 20
 IMIX_BYTES = 5944726220   # cgck_imix_bytes(16M)
-ALGO = {"1500": N * 1504, "64": N * 68, "imix": IMIX_BYTES + 16 * N}
+ALGO = {"1500": N * 1504, "64": N * 68, "imix": IMIX_BYTES + 16 * N,
+        "rss_hash": (64 << 20) * 16,            # bench.py RSS_TUPLES x (12 B read + 4 B written)
+        "dst_cache": (4 * 256 * 60536 // 8) * 16}  # entries written (no input read); ~1/8 survive
 
 
 def per_kernel(path, counter):
