@@ -193,6 +193,140 @@ __global__ __launch_bounds__(64) void stream_kernel(KParams p)
 	}
 }
 
+// ---------------------------------------------------------------------------
+// Loader/consumer form: one wave per workgroup only moves bytes, three waves
+// only compute (MI355X_MICROARCH.md 'ldsdma-fill': a dedicated LDS-DMA
+// loader wave per CU streams at 6.4-6.8 TB/s beside its consumers).
+// A phase is 3 steps (12 packets); the ring holds kLcPh phases (3 slots
+// each).  Per phase: the loader waits (counted vmcnt) for phase ph, all four
+// waves pass barrier ph, the loader refills the slots of phase ph-1 (which
+// the consumers finished, lgkmcnt(0), before that barrier) with phase
+// ph+kLcPh-1, and consumer c reduces step 3ph+c.  Consumers store their
+// outputs directly: their stores count only in their own vmcnt.
+// ---------------------------------------------------------------------------
+
+template <int kLcPh>
+__device__ __forceinline__ void lc_issue_phase(const KParams &p, uint64_t r0, uint64_t r1, uint64_t ph,
+					       uint64_t last_chunk, const uint8_t *zero, uint32_t lds0)
+{
+	const uint32_t grp = (uint32_t)(ph % kLcPh) * 3;
+#pragma unroll
+	for (int c = 0; c < 3; ++c) {
+		const uint64_t first = r0 + 4 * (3 * ph + c);
+		str_issue(p, first, first < r1, last_chunk, zero, lds0 + (grp + c) * kStrSlot);
+	}
+}
+
+__device__ __forceinline__ void str_consume(const KParams &p, const uint8_t *sl, uint64_t first, uint64_t r1,
+					    uint64_t base)
+{
+	const int lane = threadIdx.x & 63, g = lane >> 4, gl = lane & 15;
+	const uint32_t flags = p.flags;
+	const bool raw = flags & CGCK_RAW;
+	const int len = (int)p.ip_len;
+	const uint64_t a_reg = (base + first * p.stride) & ~(uint64_t)15;
+	const uint64_t pk = first + g;
+	const int o = (int)(base + pk * p.stride - a_reg);
+	const int q = o & 15, c0 = o >> 4;
+	const int nch = (q + len + 15) >> 4;
+	uint4 w[kStrS];
+#pragma unroll
+	for (int s = 0; s < kStrS; ++s) {
+		const int c = c0 + 16 * s + gl;
+		w[s] = *reinterpret_cast<const uint4 *>(sl + 16 * (c < kStrS * 64 ? c : kStrS * 64 - 1));
+	}
+	const uint32_t *hw = reinterpret_cast<const uint32_t *>(sl + o);
+	const uint32_t h0 = hw[0], h1 = hw[1], h2 = hw[2], h3 = hw[3], h4 = hw[4];
+	uint32_t body = 0;
+#pragma unroll
+	for (int s = 0; s < kStrS; ++s)
+		body = 16 * s + gl < nch ? sum4(w[s], body) : body;
+	uint32_t corr = 0;
+	if (gl == 0 && q != 0)
+		corr = msum(w[0], 0, 0, q, 0);
+	const int e = q + len - 16 * (nch - 1);
+#pragma unroll
+	for (int s = 0; s < kStrS; ++s)
+		if (16 * s + gl == nch - 1 && e != 16)
+			corr = fold16(corr) + fold16(msum(w[s], 0, e, 16, 0));
+	uint32_t tot = fold16(body) + (0xffffu - fold16(corr));
+	tot = fold16(gsum<16>(tot));
+	if (gl != 0 || pk >= r1)
+		return;
+	const uint32_t hd = h0 & 15;
+	const int hl = (int)hd * 4;
+	const uint32_t proto = (h2 >> 8) & 0xffu;
+	uint32_t lo = 0, hi = 0, verdict = 0;
+	if (raw) {
+		lo = finish(tot);
+	} else if (len < hl) {
+		verdict = CGCK_BAD_LEN;
+	} else {
+		uint32_t ip = hsum(h4, hsum(h3, hsum(h2, hsum(h1, hsum(h0, 0)))));
+		if (hd != 5) {
+			ip = 0;
+			for (uint32_t i = 0; i < hd; ++i)
+				ip = hsum(hw[i], ip);
+		}
+		const uint32_t IPs = fold16(ip);
+		if (flags & CGCK_IP)
+			lo = finish(IPs);
+		if (flags & CGCK_L4) {
+			uint32_t L = ocsub(tot, IPs);
+			if (!(flags & CGCK_L4_NOPSEUDO))
+				L = fold16(L + fold16(hsum(h4, hsum(h3, 0))) + (proto << 8) +
+					   bswap16((uint32_t)(len - hl) & 0xffffu));
+			hi = finish(L);
+		}
+	}
+	if (p.out)
+		gbl(p.out)[pk] = lo | (hi << 16);
+	if (p.verdict)
+		gbl(p.verdict)[pk] = (uint8_t)verdict;
+}
+
+template <int kLcPh> // phases in the ring (3 slots of 6 KiB each)
+__global__ __launch_bounds__(256) void stream_lc_kernel(KParams p)
+{
+	extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+	const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+	const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)smem);
+	const uint8_t *zero = (const uint8_t *)p.zero + (blockIdx.x & 63) * 64;
+	const uint64_t base = reinterpret_cast<uint64_t>(p.base) + p.l3_off;
+	const uint64_t last_chunk = (base + (p.n - 1) * p.stride + p.ip_len - 1) & ~(uint64_t)15;
+	// contiguous packet range of this workgroup, a multiple of 12 packets
+	const uint64_t nb = gridDim.x;
+	const uint64_t per = (((p.n + nb - 1) / nb) + 11) / 12 * 12;
+	const uint64_t r0 = (uint64_t)blockIdx.x * per;
+	const uint64_t r1 = r0 + per < p.n ? r0 + per : p.n;
+	if (r0 >= r1)
+		return; // uniform across the workgroup
+	const uint64_t nph = (r1 - r0 + 11) / 12;
+
+	if (wave == 0) {
+#pragma unroll
+		for (int d = 0; d < kLcPh - 1; ++d)
+			lc_issue_phase<kLcPh>(p, r0, r1, d, last_chunk, zero, lds0);
+		for (uint64_t ph = 0; ph < nph; ++ph) {
+			// phase ph landed: phases ph+1 .. ph+kLcPh-2 may stay in flight
+			asm volatile("s_waitcnt vmcnt(%0)" ::"i"((kLcPh - 2) * 3 * kStrS) : "memory");
+			__builtin_amdgcn_s_barrier();
+			lc_issue_phase<kLcPh>(p, r0, r1, ph + kLcPh - 1, last_chunk, zero, lds0);
+		}
+		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+	} else {
+		const int c = wave - 1;
+		for (uint64_t ph = 0; ph < nph; ++ph) {
+			__builtin_amdgcn_s_barrier();
+			const uint64_t first = r0 + 4 * (3 * ph + c);
+			if (first < r1)
+				str_consume(p, smem + ((uint32_t)(ph % kLcPh) * 3 + c) * kStrSlot, first, r1, base);
+			// this phase's slots are refilled after the next barrier
+			asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+		}
+	}
+}
+
 bool stream_ok(const KParams &p)
 {
 	const uint32_t fl = p.flags;
@@ -207,6 +341,24 @@ hipError_t launch_stream(const KParams &p, int num_cus, hipStream_t st)
 		const char *e = getenv("CGCK_STR_WPC");
 		return e && atoi(e) > 0 ? atoi(e) : 8;
 	}();
+	static const bool lc = [] { // $CGCK_STR_LC=1: the loader/consumer form
+		const char *e = getenv("CGCK_STR_LC");
+		return e && *e == '1';
+	}();
+	if (lc) {
+		static const int ph = [] { // $CGCK_STR_LCPH: ring phases 3 or 4 (vmcnt counts <= 63)
+			const char *e = getenv("CGCK_STR_LCPH");
+			return e && atoi(e) == 3 ? 3 : 4;
+		}();
+		const uint64_t want = (p.n + 12 * 16 - 1) / (12 * 16); // >= 16 phases per workgroup
+		const uint64_t cap = (uint64_t)num_cus * 2; // 54 / 72 KiB rings: 2 per CU
+		const dim3 g((unsigned)(want < cap ? (want ? want : 1) : cap));
+		if (ph == 3)
+			hipLaunchKernelGGL(stream_lc_kernel<3>, g, dim3(256), 3 * 3 * kStrSlot, st, p);
+		else
+			hipLaunchKernelGGL(stream_lc_kernel<4>, g, dim3(256), 4 * 3 * kStrSlot, st, p);
+		return hipGetLastError();
+	}
 	static const int ring = [] { // $CGCK_STR_RING: ring slots (A/B runs)
 		const char *e = getenv("CGCK_STR_RING");
 		return e && atoi(e) >= 2 && atoi(e) <= 4 ? atoi(e) : 3;
