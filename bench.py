@@ -240,8 +240,7 @@ def cpu_baseline(seconds):
         m = min(4096, n - k)
         blk = P.stream_bytes(k * 1500, m * 1500, SEED)
         buf[k * 1500:(k + m) * 1500] = blk
-    for k in range(n):
-        P.stamp_header(buf, k * 1500, 1500)
+    P.stamp_strided(buf, n, 1500, 1500)
     cpus = sorted(os.sched_getaffinity(0))
     old = set(cpus)
     try:
@@ -263,6 +262,35 @@ def cpu_baseline(seconds):
         "gbps": rate * 1500 / 1e9,
         "all_cores": {"value": rate_all / 1e9, "cores": allc, "gbps": rate_all * 1500 / 1e9},
     }
+
+
+def cpu_baseline_64(seconds):
+    """BASELINE configs[0]: 1M x 64 B IPv4+TCP packets through the reference's
+    checksum loop (in_cksum(ip, 20) + udp_cksum(ip, 44) each) on one pinned
+    host core, same synthetic bytes as the device batch."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    P = oracle.port()
+    R = oracle.reference()
+    fin, fudp = (R or P).fn_pointers()
+    n = 1 << 20
+    buf = P.stream_bytes(0, n * 64, SEED)
+    P.stamp_strided(buf, n, 64, 64)
+    cpus = sorted(os.sched_getaffinity(0))
+    old = set(cpus)
+    try:
+        os.sched_setaffinity(0, {cpus[len(cpus) // 2]})
+        sec, _ = P.cpu_bench(fin, fudp, buf, n, 64, 64, threads=1, reps=1)
+        reps = max(1, int(seconds / max(sec, 1e-3)))
+        sec, _ = P.cpu_bench(fin, fudp, buf, n, 64, 64, threads=1, reps=reps)
+    finally:
+        os.sched_setaffinity(0, old)
+    rate = n * reps / sec
+    return {"value": rate / 1e9, "unit": "Gpkt/s", "cores": 1, "kind": "reference" if R else "port",
+            "sample": f"BASELINE configs[0]: {n} x 64 B packets (64 MB), in_cksum(ip,20)+udp_cksum(ip,44) "
+                      f"each, {reps} passes, {sec:.1f} s on 1 pinned core",
+            "gbps": rate * 64 / 1e9}
 
 
 def load_traffic(key="1500"):
@@ -308,9 +336,11 @@ def main():
     if not args.no_rss and args.only in (None, "rss"):
         res["rss"] = bench_rss(torch, dist, eng, cgck, plan, args.steps, args.warmup)
 
-    cpu = cpu_r = None
+    cpu = cpu_r = cpu_64 = None
     if dist.rank == 0 and dist.world == 1 and not args.no_cpu:
         cpu = cpu_baseline(args.cpu_seconds)
+        if "64" in res:
+            cpu_64 = cpu_baseline_64(min(3.0, args.cpu_seconds))
         if "rss" in res:
             cpu_r = cpu_rss(min(3.0, args.cpu_seconds))
     dist.barrier()
@@ -354,6 +384,8 @@ def main():
         if "64" in res:
             extra["64B"] = line(64, *res["64"])
             extra["64B"].update({"kernel": "lpa_kernel<false>", "traffic": load_traffic("64")})
+            if cpu_64:
+                extra["64B"]["cpu_baseline"] = cpu_64
         if "imix" in res:
             wall, ev_ms, nbytes = res["imix"]
             extra["imix"] = line(0, wall, ev_ms, nbytes + 16 * n)

@@ -206,6 +206,52 @@ def test_fuzz_strided_vs_oracle(engine, port, stride, l3, ln, flags):
     assert np.array_equal(got, ref)
 
 
+# Every kernel family forced through $CGCK_KERNEL (read at context creation),
+# on the strided shapes each one accepts; a family falls back to the group
+# kernel where its preconditions fail, so every cell is a valid comparison.
+FAMILIES = ["group", "lpp", "lpa", "slot2", "str"]
+FAMILY_SHAPES = [  # (stride, l3_off, ip_len, packets)
+    (64, 0, 64, 3000), (64, 0, 48, 333), (32, 0, 20, 333), (128, 16, 64, 333), (72, 2, 60, 333),
+    (256, 0, 255, 333), (1500, 0, 1500, 3000), (1504, 4, 1500, 333), (1520, 0, 1517, 333),
+    (1500, 0, 1000, 333), (1500, 14, 1486, 333),
+]
+
+
+@pytest.fixture(scope="module")
+def family_engines():
+    import os
+    engines = {}
+    for f in FAMILIES:
+        os.environ["CGCK_KERNEL"] = f
+        try:
+            engines[f] = cgck.Engine(0)
+        finally:
+            os.environ.pop("CGCK_KERNEL", None)
+    yield engines
+    for e in engines.values():
+        e.close()
+
+
+@pytest.mark.parametrize("family", FAMILIES)
+@pytest.mark.parametrize("stride,l3,ln,n", FAMILY_SHAPES)
+@pytest.mark.parametrize("flags", [cgck.GEN_BOTH, cgck.RAW, cgck.IP, cgck.L4 | cgck.L4_NOPSEUDO,
+                                   cgck.VERIFY_TOY])
+def test_family_strided_vs_oracle(family_engines, port, family, stride, l3, ln, n, flags):
+    rng = np.random.default_rng(stride * 13 + ln + n)
+    buf = rng.integers(0, 256, n * stride + l3 + ln + 64, dtype=np.uint8)
+    for k in range(n):
+        o = k * stride + l3
+        buf[o] = 0x45 if k % 7 else (0x40 | int(rng.integers(5, 16)))
+        buf[o + 9] = (6, 17, 1, 6, 99, 6, 6)[k % 7]
+    ref = buf.copy()
+    exp, ever = port.batch_strided(ref, n, stride, l3, ln, flags)
+    got = buf.copy()
+    out, ver = family_engines[family].run_host_strided(got, n, stride, l3, ln, flags)
+    bad = np.nonzero((out != exp) | (ver != ever))[0]
+    assert len(bad) == 0, f"{family}: {len(bad)} mismatches, first {bad[:5]}"
+    assert np.array_equal(got, ref)
+
+
 def test_edges(engine, port):
     # empty batch
     engine.strided(0, 0, 64, 0, 64, cgck.GEN_BOTH)
