@@ -48,6 +48,9 @@ constexpr bool kDefaultLaneNT = false, kDefaultLaneContig = false;
 // by default — measured 76.9 % vs 77.9 % of HBM peak for the register-load
 // group kernel on the same box (tools/str_sweep.sh).  CGCK_KERNEL=str.
 constexpr bool kDefaultStream = false;
+// Batched Toeplitz hash over dense 12-byte tuples: 0 two-group loop, 2 A/B
+// pipelined (cgck_rss.hip).
+constexpr int kDefaultRssVariant = 2;
 
 // Toeplitz RSS hash (cgck_rss.hip; subr.c:482-530).  `tab` = cnt x 256 u32
 // byte tables derived from the key on the host (rss_tables in cgck_api.cpp).

@@ -144,6 +144,64 @@ __global__ __launch_bounds__(256) void toeplitz12x4_kernel(RssParams p, uint64_t
 	}
 }
 
+// Software-pipelined form (the lpa lesson, cgck_lane.hip): per lane two
+// 48-byte groups in flight in explicit A/B registers, loads unconditional
+// (index clamped to the last group), so each group's output store trails the
+// next group's loads and no wait includes a store acknowledgement; the store
+// is inline asm so the compiler does not hold later registers behind it.
+__device__ __forceinline__ void t12_load(const u32x4_t CGCK_GLOBAL *src, uint64_t g, uint64_t ng, u32x4_t (&r)[3])
+{
+	const uint64_t gg = g < ng ? g : ng - 1;
+	r[0] = src[3 * gg];
+	r[1] = src[3 * gg + 1];
+	r[2] = src[3 * gg + 2];
+}
+
+__device__ __forceinline__ void t12_store(uint32_t *out, uint64_t g, const u32x4_t &v)
+{
+	u32x4_t *o = reinterpret_cast<u32x4_t *>(out) + g;
+	asm volatile("global_store_dwordx4 %0, %1, off" ::"v"(o), "v"(v) : "memory");
+}
+
+__global__ __launch_bounds__(256) void toeplitz12x4_ab_kernel(RssParams p, uint64_t ng)
+{
+	extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+	const uint32_t CGCK_GLOBAL *gt = (const uint32_t CGCK_GLOBAL *)p.tab;
+	for (uint32_t i = threadIdx.x; i < 12 * 256; i += 256)
+		smem[i] = gt[i];
+	__syncthreads();
+	const u32x4_t CGCK_GLOBAL *src = (const u32x4_t CGCK_GLOBAL *)p.data;
+	const uint64_t NI = (ng + 255) / 256, S = gridDim.x;
+	uint64_t it = blockIdx.x;
+	if (it >= NI)
+		return;
+	u32x4_t A[3], B[3];
+	t12_load(src, it * 256 + threadIdx.x, ng, A);
+	for (;;) {
+		const bool hasB = it + S < NI;
+		t12_load(src, (hasB ? it + S : it) * 256 + threadIdx.x, ng, B);
+		{
+			const uint64_t g = it * 256 + threadIdx.x;
+			const u32x4_t h = hash4x12<false>(smem, A[0], A[1], A[2], p.mask);
+			if (g < ng)
+				t12_store(p.out, g, h);
+		}
+		if (!hasB)
+			break;
+		const bool hasA = it + 2 * S < NI;
+		t12_load(src, (hasA ? it + 2 * S : it + S) * 256 + threadIdx.x, ng, A);
+		{
+			const uint64_t g = (it + S) * 256 + threadIdx.x;
+			const u32x4_t h = hash4x12<false>(smem, B[0], B[1], B[2], p.mask);
+			if (g < ng)
+				t12_store(p.out, g, h);
+		}
+		if (!hasA)
+			break;
+		it += 2 * S;
+	}
+}
+
 hipError_t launch_toeplitz(const RssParams &p0, int num_cus, hipStream_t st)
 {
 	if (p0.n == 0)
@@ -152,16 +210,28 @@ hipError_t launch_toeplitz(const RssParams &p0, int num_cus, hipStream_t st)
 	if (p.cnt == 12 && p.stride == 12 && ((uintptr_t)p.data & 15) == 0 && ((uintptr_t)p.out & 15) == 0 &&
 	    p.n >= 4) {
 		const uint64_t ng = p.n / 4;
-		const uint64_t want = (ng + 255) / 256, cap = (uint64_t)num_cus * 8;
-		// Byte tables by default: measured 0.225 vs 0.233 ms for nibble tables
-		// on 64M tuples (the kernel is bound by the mixed read/write stream,
-		// not by LDS conflicts).  CGCK_RSS_NIB=1 selects the nibble tables.
-		const char *ab = getenv("CGCK_RSS_NIB");
-		if (ab && *ab == '1')
-			hipLaunchKernelGGL(toeplitz12x4_kernel<true>, dim3((unsigned)(want < cap ? want : cap)),
+		const uint64_t want = (ng + 255) / 256;
+		// Byte tables: measured 0.225 vs 0.233 ms for nibble tables on 64M
+		// tuples (the kernel is bound by the mixed read/write stream, not by
+		// LDS conflicts).
+		static const int var = [] { // $CGCK_RSS_VAR: 0 two-group loop, 1 nibble tables, 2 A/B pipelined
+			const char *e = getenv("CGCK_RSS_VAR");
+			return e ? atoi(e) : kDefaultRssVariant;
+		}();
+		// 2 blocks per CU: 65.4 % of HBM peak vs 62.5 % at 8 (tools/rss_sweep.sh)
+		static const int bpc = [] {
+			const char *e = getenv("CGCK_RSS_BPC");
+			return e && atoi(e) > 0 ? atoi(e) : 2;
+		}();
+		const uint64_t capb = (uint64_t)num_cus * bpc;
+		if (var == 2)
+			hipLaunchKernelGGL(toeplitz12x4_ab_kernel, dim3((unsigned)(want < capb ? want : capb)), dim3(256),
+					   12 * 256 * 4, st, p, ng);
+		else if (var == 1)
+			hipLaunchKernelGGL(toeplitz12x4_kernel<true>, dim3((unsigned)(want < capb ? want : capb)),
 					   dim3(256), 24 * 16 * 4, st, p, ng);
 		else
-			hipLaunchKernelGGL(toeplitz12x4_kernel<false>, dim3((unsigned)(want < cap ? want : cap)),
+			hipLaunchKernelGGL(toeplitz12x4_kernel<false>, dim3((unsigned)(want < capb ? want : capb)),
 					   dim3(256), 12 * 256 * 4, st, p, ng);
 		hipError_t e = hipGetLastError();
 		if (e != hipSuccess || ng * 4 == p.n)

@@ -443,3 +443,38 @@ def test_full_size_imix(engine, port):
     engine.sync()
     bad, chk = port.check_synth_imix(n, SEED, cgck.GEN_BOTH, o, 64)
     assert bad == 0 and chk == n // 64
+
+
+# ---------------------------------------------------------------------------
+# Shared-nothing worker threads (con-gen.c:1092-1100): every thread calls the
+# drop-in symbols on its own context at the same time; results stay exact.
+# ---------------------------------------------------------------------------
+
+def test_dropin_concurrent_threads(engine, golden_basic):
+    import threading
+    g = golden_basic["len_off_grid"]
+    buf = hexa(g["buf_hex"])
+    frames = golden_basic["udp_frames"][:32]
+    errors = []
+
+    def worker(tid):
+        try:
+            for rep in range(3):
+                off = (tid + rep) % 16
+                got = [cgck.in_cksum(buf, off, n) for n in g["lens"][::7]]
+                if got != g["in_cksum"][off][::7]:
+                    errors.append(f"thread {tid}: in_cksum at offset {off}")
+                for f in frames:
+                    fr = hexa(f["frame_hex"])
+                    if cgck.udp_cksum(fr, 14, f["l4len"]) != f["udp_cksum"]:
+                        errors.append(f"thread {tid}: udp_cksum")
+                        break
+        finally:
+            cgck.thread_release()
+
+    ts = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=120)
+    assert not errors, errors[:5]

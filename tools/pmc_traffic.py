@@ -16,7 +16,7 @@ KERNELS = {
     "1500": "cksum_kernel<16, 6, 1, false, true>",
     "64": "lpa_kernel<false>",
     "imix": "slot2_kernel<true, false>",
-    "rss_hash": "toeplitz12x4_kernel<false>",
+    "rss_hash": "toeplitz12x4_ab_kernel",
     "dst_cache": "dst_cache_kernel<true>",
 }
 # bench.py's batches: 16M packets; reads + 12 B descriptor (IMIX) + 4 B output

@@ -1,8 +1,9 @@
-# A/B timing of the Toeplitz RSS kernels (tools/rss_bench.py) under the
-# CGCK_RSS_NIB / CGCK_DST_ITERS / CGCK_DST_WGS knobs.  GPU box only.
+# A/B timing of the batched Toeplitz hash (tools/rss_bench.py) under the
+# CGCK_RSS_VAR / CGCK_RSS_BPC knobs (CGCK_DST_ITERS / CGCK_DST_WGS for the
+# dst-cache build).  GPU box only; each cell its own process.
 cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out; : > gpurun_out/rsweep.log
-for v in 0 1; do
-  echo "nib=$v" >> gpurun_out/rsweep.log
-  CGCK_RSS_NIB=$v timeout -k 10 60 python tools/rss_bench.py --reps 20 2>/dev/null | grep '"hash"' >> gpurun_out/rsweep.log || exit 1
+for cell in ${CELLS:-0:8 2:8 2:4 2:16 1:8 0:8 2:8}; do
+  echo "var:bpc=$cell" >> gpurun_out/rsweep.log
+  CGCK_RSS_VAR=${cell%%:*} CGCK_RSS_BPC=${cell##*:} timeout -k 10 60 python tools/rss_bench.py --reps 20 2>/dev/null | grep '"hash"' >> gpurun_out/rsweep.log || exit 1
 done
 echo done
