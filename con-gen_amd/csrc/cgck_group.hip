@@ -11,6 +11,8 @@
 // htons(l4len) read as a little-endian word (struct pseudo, subr.c:119-125).
 #include "cgck_device.h"
 
+#include <stdlib.h>
+
 namespace cgck {
 
 // Part and eat(): cgck_device.h (shared with the LDS-DMA stream kernel).
@@ -181,7 +183,13 @@ static hipError_t launch_t(const KParams &p, int max_blocks, bool nt, hipStream_
 
 hipError_t launch_group(const KParams &p, uint32_t max_len, int num_cus, bool nt, hipStream_t st)
 {
-	const int max_blocks = num_cus * 16;
+	// 48 blocks per CU: 80.4 % vs 78.5-78.9 % at 24 and 78.2 % at 16 on one box
+	// (tools/bpc_sweep.sh): shorter contiguous block ranges
+	static const int bpc = [] { // $CGCK_GRP_BPC: blocks per CU (A/B runs)
+		const char *e = getenv("CGCK_GRP_BPC");
+		return e && atoi(e) > 0 ? atoi(e) : 48;
+	}();
+	const int max_blocks = num_cus * bpc;
 	const bool d = p.desc != nullptr;
 	if (max_len <= 80) // <= 6 chunks at any alignment: two steps of 4 lanes
 		return d ? launch_t<4, 2, 4, true>(p, max_blocks, nt, st)

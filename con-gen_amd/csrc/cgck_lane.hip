@@ -617,9 +617,11 @@ __global__ __launch_bounds__(256) void lpa_kernel(KParams p)
 
 hipError_t launch_lpa(const KParams &p, int num_cus, bool nt, hipStream_t st)
 {
+	// 3 blocks per CU: 66.6 % of HBM peak vs 64.3 % at 4 and 63.0 % at 8 on one
+	// box (tools/bpc_sweep.sh); fewer waves, each with two groups in flight
 	static const int bpc = [] {
 		const char *e = getenv("CGCK_LPA_BPC");
-		return e && atoi(e) > 0 ? atoi(e) : 8;
+		return e && atoi(e) > 0 ? atoi(e) : 3;
 	}();
 	uint64_t want = (p.n + 255) / 256, mb = (uint64_t)num_cus * bpc;
 	const dim3 g((unsigned)(want < mb ? want : mb));
