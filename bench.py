@@ -383,7 +383,7 @@ def main():
         extra = {}
         if "64" in res:
             extra["64B"] = line(64, *res["64"])
-            extra["64B"].update({"kernel": "lpa_kernel<false>", "traffic": load_traffic("64")})
+            extra["64B"].update({"kernel": "lpa_kernel<false, 4>", "traffic": load_traffic("64")})
             if cpu_64:
                 extra["64B"]["cpu_baseline"] = cpu_64
         if "imix" in res:

@@ -508,9 +508,8 @@ struct Quad {
 };
 
 template <bool NT>
-__device__ __forceinline__ void lpa_load(const KParams &p, uint64_t it, bool live, int nch, Quad &q)
+__device__ __forceinline__ void lpa_load(const KParams &p, uint64_t k, bool live, int nch, Quad &q)
 {
-	uint64_t k = it * 256 + threadIdx.x;
 	k = k < p.n ? k : p.n - 1;
 	// past the block's last group: a zero line of the context, one of 64 by
 	// block, instead of re-reading packet bytes that have left the L2
@@ -521,10 +520,12 @@ __device__ __forceinline__ void lpa_load(const KParams &p, uint64_t it, bool liv
 		q.c[i] = ld<NT>(c0 + (i < nch ? i : nch - 1));
 }
 
+// Reduce packet k's quad and store its u32 output.  (A staged form — four
+// results per lane leaving as one 16-byte store after an LDS transpose —
+// measured 66.7 % vs 69.5 % of HBM peak on one box.)
 template <bool NT>
-__device__ __forceinline__ void lpa_reduce(const KParams &p, uint64_t it, int len, int nch, const Quad &q)
+__device__ __forceinline__ void lpa_reduce(const KParams &p, uint64_t k, int len, int nch, const Quad &q)
 {
-	const uint64_t k = it * 256 + threadIdx.x;
 	const bool ok = k < p.n;
 	// Fast path (wave-uniform): ip_cksum + tcp_cksum only, whole chunks, and
 	// every packet of the wave with ip_hl = 5 — the 64 B config.  IP header =
@@ -588,7 +589,7 @@ __device__ __forceinline__ void lpa_reduce(const KParams &p, uint64_t it, int le
 	}
 }
 
-template <bool NT>
+template <bool NT, int DEPTH>
 __global__ __launch_bounds__(256) void lpa_kernel(KParams p)
 {
 	const int len = (int)p.ip_len, nch = (len + 15) >> 4;
@@ -596,39 +597,59 @@ __global__ __launch_bounds__(256) void lpa_kernel(KParams p)
 	uint64_t it = blockIdx.x;
 	if (it >= NI)
 		return;
-	// loads are never skipped (past the end they read a zero line), so the
-	// loop has no load under a branch
-	Quad A, B;
-	lpa_load<NT>(p, it, true, nch, A);
+	// DEPTH packet groups per lane in a register ring: the load of group
+	// d + DEPTH - 1 is issued before group d is reduced.  Loads are never
+	// skipped (past the end they read a zero line), so the loop has no load
+	// under a branch and every wait is a counted vmcnt.
+	Quad Q[DEPTH];
+#pragma unroll
+	for (int d = 0; d < DEPTH - 1; ++d)
+		lpa_load<NT>(p, (it + d * S) * 256 + threadIdx.x, it + d * S < NI, nch, Q[d]);
 	for (;;) {
-		const bool hasB = it + S < NI;
-		lpa_load<NT>(p, it + S, hasB, nch, B);
-		lpa_reduce<NT>(p, it, len, nch, A);
-		if (!hasB)
-			break;
-		const bool hasA = it + 2 * S < NI;
-		lpa_load<NT>(p, it + 2 * S, hasA, nch, A);
-		lpa_reduce<NT>(p, it + S, len, nch, B);
-		if (!hasA)
-			break;
-		it += 2 * S;
+#pragma unroll
+		for (int d = 0; d < DEPTH; ++d) {
+			const uint64_t ahead = it + (uint64_t)(d + DEPTH - 1) * S;
+			lpa_load<NT>(p, ahead * 256 + threadIdx.x, ahead < NI, nch, Q[(d + DEPTH - 1) % DEPTH]);
+			lpa_reduce<NT>(p, (it + d * S) * 256 + threadIdx.x, len, nch, Q[d]);
+			if (it + (uint64_t)(d + 1) * S >= NI)
+				return;
+		}
+		it += (uint64_t)DEPTH * S;
 	}
 }
 
 hipError_t launch_lpa(const KParams &p, int num_cus, bool nt, hipStream_t st)
 {
-	// 3 blocks per CU: 66.6 % of HBM peak vs 64.3 % at 4 and 63.0 % at 8 on one
-	// box (tools/bpc_sweep.sh); fewer waves, each with two groups in flight
-	static const int bpc = [] {
+	// One block per CU (one wave per SIMD) with four packet groups per lane in
+	// flight: 68.8-69.1 % of HBM peak vs 66.2-66.4 % for two groups at 3 blocks
+	// per CU and 67.9-68.7 % for three groups (tools/lpa_depth.sh, one box).
+	// The per-packet reduce is short, so fewer waves with deeper register
+	// rings keep more bytes in flight per instruction issued.
+	static const int bpc = [] { // $CGCK_LPA_BPC: blocks per CU (A/B runs)
 		const char *e = getenv("CGCK_LPA_BPC");
-		return e && atoi(e) > 0 ? atoi(e) : 3;
+		return e && atoi(e) > 0 ? atoi(e) : 1;
+	}();
+	static const int depth = [] { // $CGCK_LPA_DEPTH: packet groups per lane in flight, 2..4
+		const char *e = getenv("CGCK_LPA_DEPTH");
+		const int d = e ? atoi(e) : 0;
+		return d >= 2 && d <= 4 ? d : 4;
 	}();
 	uint64_t want = (p.n + 255) / 256, mb = (uint64_t)num_cus * bpc;
 	const dim3 g((unsigned)(want < mb ? want : mb));
-	if (nt)
-		hipLaunchKernelGGL((lpa_kernel<true>), g, dim3(256), 0, st, p);
+#define CGCK_LPA(D)                                                                            \
+	do {                                                                                   \
+		if (nt)                                                                        \
+			hipLaunchKernelGGL((lpa_kernel<true, D>), g, dim3(256), 0, st, p);      \
+		else                                                                           \
+			hipLaunchKernelGGL((lpa_kernel<false, D>), g, dim3(256), 0, st, p);     \
+	} while (0)
+	if (depth == 4)
+		CGCK_LPA(4);
+	else if (depth == 3)
+		CGCK_LPA(3);
 	else
-		hipLaunchKernelGGL((lpa_kernel<false>), g, dim3(256), 0, st, p);
+		CGCK_LPA(2);
+#undef CGCK_LPA
 	return hipGetLastError();
 }
 
