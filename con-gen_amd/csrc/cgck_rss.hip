@@ -144,8 +144,8 @@ __global__ __launch_bounds__(256) void toeplitz12x4_kernel(RssParams p, uint64_t
 	}
 }
 
-// Software-pipelined form (the lpa lesson, cgck_lane.hip): per lane two
-// 48-byte groups in flight in explicit A/B registers, loads unconditional
+// Software-pipelined form (the lpa lesson, cgck_lane.hip): per lane DEPTH
+// 48-byte groups in flight in a register ring, loads unconditional
 // (index clamped to the last group), so each group's output store trails the
 // next group's loads and no wait includes a store acknowledgement; the store
 // is inline asm so the compiler does not hold later registers behind it.
@@ -163,6 +163,7 @@ __device__ __forceinline__ void t12_store(uint32_t *out, uint64_t g, const u32x4
 	asm volatile("global_store_dwordx4 %0, %1, off" ::"v"(o), "v"(v) : "memory");
 }
 
+template <int DEPTH>
 __global__ __launch_bounds__(256) void toeplitz12x4_ab_kernel(RssParams p, uint64_t ng)
 {
 	extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
@@ -175,30 +176,26 @@ __global__ __launch_bounds__(256) void toeplitz12x4_ab_kernel(RssParams p, uint6
 	uint64_t it = blockIdx.x;
 	if (it >= NI)
 		return;
-	u32x4_t A[3], B[3];
-	t12_load(src, it * 256 + threadIdx.x, ng, A);
+	// DEPTH groups per lane in a register ring: group d + DEPTH - 1 is loaded
+	// before group d is hashed (past the end the index clamps to this block's
+	// last group, so no load sits under a branch)
+	auto gof = [&](uint64_t i) { return (i < NI ? i : it) * 256 + threadIdx.x; };
+	u32x4_t R[DEPTH][3];
+#pragma unroll
+	for (int d = 0; d < DEPTH - 1; ++d)
+		t12_load(src, gof(it + d * S), ng, R[d]);
 	for (;;) {
-		const bool hasB = it + S < NI;
-		t12_load(src, (hasB ? it + S : it) * 256 + threadIdx.x, ng, B);
-		{
-			const uint64_t g = it * 256 + threadIdx.x;
-			const u32x4_t h = hash4x12<false>(smem, A[0], A[1], A[2], p.mask);
+#pragma unroll
+		for (int d = 0; d < DEPTH; ++d) {
+			t12_load(src, gof(it + (uint64_t)(d + DEPTH - 1) * S), ng, R[(d + DEPTH - 1) % DEPTH]);
+			const uint64_t g = (it + d * S) * 256 + threadIdx.x;
+			const u32x4_t h = hash4x12<false>(smem, R[d][0], R[d][1], R[d][2], p.mask);
 			if (g < ng)
 				t12_store(p.out, g, h);
+			if (it + (uint64_t)(d + 1) * S >= NI)
+				return;
 		}
-		if (!hasB)
-			break;
-		const bool hasA = it + 2 * S < NI;
-		t12_load(src, (hasA ? it + 2 * S : it + S) * 256 + threadIdx.x, ng, A);
-		{
-			const uint64_t g = (it + S) * 256 + threadIdx.x;
-			const u32x4_t h = hash4x12<false>(smem, B[0], B[1], B[2], p.mask);
-			if (g < ng)
-				t12_store(p.out, g, h);
-		}
-		if (!hasA)
-			break;
-		it += 2 * S;
+		it += (uint64_t)DEPTH * S;
 	}
 }
 
@@ -223,10 +220,21 @@ hipError_t launch_toeplitz(const RssParams &p0, int num_cus, hipStream_t st)
 			const char *e = getenv("CGCK_RSS_BPC");
 			return e && atoi(e) > 0 ? atoi(e) : 2;
 		}();
+		// ring depth 3: 62.3-65.9 % vs 60.1-63.5 % for 2 and 63.5 % for 4 at 2
+		// blocks per CU (tools/rss_sweep.sh, two boxes; profiles/r01/sweep_rss_depth.log)
+		static const int depth = [] { // $CGCK_RSS_DEPTH: groups per lane in flight, 2..4
+			const char *e = getenv("CGCK_RSS_DEPTH");
+			const int d = e ? atoi(e) : 0;
+			return d >= 2 && d <= 4 ? d : 3;
+		}();
 		const uint64_t capb = (uint64_t)num_cus * bpc;
-		if (var == 2)
-			hipLaunchKernelGGL(toeplitz12x4_ab_kernel, dim3((unsigned)(want < capb ? want : capb)), dim3(256),
-					   12 * 256 * 4, st, p, ng);
+		const dim3 gb((unsigned)(want < capb ? want : capb));
+		if (var == 2 && depth == 4)
+			hipLaunchKernelGGL(toeplitz12x4_ab_kernel<4>, gb, dim3(256), 12 * 256 * 4, st, p, ng);
+		else if (var == 2 && depth == 3)
+			hipLaunchKernelGGL(toeplitz12x4_ab_kernel<3>, gb, dim3(256), 12 * 256 * 4, st, p, ng);
+		else if (var == 2)
+			hipLaunchKernelGGL(toeplitz12x4_ab_kernel<2>, gb, dim3(256), 12 * 256 * 4, st, p, ng);
 		else if (var == 1)
 			hipLaunchKernelGGL(toeplitz12x4_kernel<true>, dim3((unsigned)(want < capb ? want : capb)),
 					   dim3(256), 24 * 16 * 4, st, p, ng);
