@@ -210,8 +210,8 @@ def test_fuzz_strided_vs_oracle(engine, port, stride, l3, ln, flags):
 # on the strided shapes each one accepts; a family falls back to the group
 # kernel where its preconditions fail, so every cell is a valid comparison.
 FAMILIES = ["group", "lpp", "lpa", "slot2", "str"]
-FAMILY_SHAPES = [  # (stride, l3_off, ip_len, packets)
-    (64, 0, 64, 3000), (64, 0, 48, 333), (32, 0, 20, 333), (128, 16, 64, 333), (72, 2, 60, 333),
+FAMILY_SHAPES = [  # (stride, l3_off, ip_len, packets); odd counts: every ip_hl = 5
+    (64, 0, 64, 3000), (64, 0, 64, 4097), (64, 16, 64, 999), (64, 0, 48, 333), (32, 0, 20, 333), (128, 16, 64, 333), (72, 2, 60, 333),
     (256, 0, 255, 333), (1500, 0, 1500, 3000), (1504, 4, 1500, 333), (1520, 0, 1517, 333),
     (1500, 0, 1000, 333), (1500, 14, 1486, 333),
 ]
@@ -241,7 +241,7 @@ def test_family_strided_vs_oracle(family_engines, port, family, stride, l3, ln, 
     buf = rng.integers(0, 256, n * stride + l3 + ln + 64, dtype=np.uint8)
     for k in range(n):
         o = k * stride + l3
-        buf[o] = 0x45 if k % 7 else (0x40 | int(rng.integers(5, 16)))
+        buf[o] = 0x45 if (k % 7 or n % 2) else (0x40 | int(rng.integers(5, 16)))
         buf[o + 9] = (6, 17, 1, 6, 99, 6, 6)[k % 7]
     ref = buf.copy()
     exp, ever = port.batch_strided(ref, n, stride, l3, ln, flags)
