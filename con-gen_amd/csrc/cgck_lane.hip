@@ -520,9 +520,12 @@ __device__ __forceinline__ void lpa_load(const KParams &p, uint64_t k, bool live
 		q.c[i] = ld<NT>(c0 + (i < nch ? i : nch - 1));
 }
 
-// Reduce packet k's quad and store its u32 output.  (A staged form — four
-// results per lane leaving as one 16-byte store after an LDS transpose —
-// measured 66.7 % vs 69.5 % of HBM peak on one box.)
+// Reduce packet k's quad and store its u32 output.  The store carries the
+// nontemporal policy: +3 points of HBM peak in the slower of the two states a
+// process lands in, +1.5 in the faster (tools/ab_lib.sh; the same policy on
+// the group, slot and hash kernels' stores lost up to 13 points).  (A staged
+// form — four results per lane leaving as one 16-byte store after an LDS
+// transpose — measured 66.7 % vs 69.5 % of HBM peak on one box.)
 template <bool NT>
 __device__ __forceinline__ void lpa_reduce(const KParams &p, uint64_t k, int len, int nch, const Quad &q)
 {
@@ -546,7 +549,7 @@ __device__ __forceinline__ void lpa_reduce(const KParams &p, uint64_t k, int len
 			const uint32_t out = finish(IPs) | (finish(L) << 16);
 			if (p.out) {
 				uint32_t *o = p.out + k;
-				asm volatile("global_store_dword %0, %1, off" ::"v"(o), "v"(out) : "memory");
+				asm volatile("global_store_dword %0, %1, off nt" ::"v"(o), "v"(out) : "memory");
 			}
 			if (p.verdict)
 				gbl(p.verdict)[k] = 0;
@@ -582,7 +585,7 @@ __device__ __forceinline__ void lpa_reduce(const KParams &p, uint64_t k, int len
 			// store.  Every vmcnt the compiler computes stays conservative: the
 			// hidden store only makes in-order waits include it.
 			uint32_t *o = p.out + k;
-			asm volatile("global_store_dword %0, %1, off" ::"v"(o), "v"(r.out) : "memory");
+			asm volatile("global_store_dword %0, %1, off nt" ::"v"(o), "v"(r.out) : "memory");
 		}
 		if (p.verdict)
 			gbl(p.verdict)[k] = (uint8_t)r.verdict;
