@@ -81,9 +81,14 @@ _u32 = ctypes.c_uint32
 def load(path=None):
     """Load libcgck.so (once).  Raises if it is missing: there is no fallback."""
     global _lib
-    if _lib is not None:
-        return _lib
-    path = path or LIB_PATH
+    if _lib is None:
+        _lib = bind(path or LIB_PATH)
+    return _lib
+
+
+def bind(path):
+    """A ctypes binding of one libcgck.so build (tools/ab_inproc.py loads two
+    builds into one process this way; everything else goes through load())."""
     if not os.path.exists(path):
         raise CgckError(f"libcgck.so not built at {path} (run make -C con-gen_amd)")
     L = ctypes.CDLL(path)
@@ -128,7 +133,6 @@ def load(path=None):
     L.cgck_dst_cache.argtypes = [_vp, ctypes.POINTER(DstParams), _vp, _u32, _vp, _vp]
     L.cgck_dst_cache_host.argtypes = [_vp, ctypes.POINTER(DstParams), _vp, _u32,
                                       ctypes.POINTER(_u32)]
-    _lib = L
     return L
 
 
