@@ -12,9 +12,12 @@ reported under "extra".
     python bench.py --gpus N --steps K --warmup W
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
-Rank 0 prints one JSON line.  The CPU baseline (rank 0, N = 1 only) times the
-reference's own subr.c checksum unit (oracle/_ref, when built) or the oracle
-restatement on a bounded sample of the same workload.
+Rank 0 prints one JSON line.  The cpu_baseline leg (rank 0) is the only part
+that touches oracle/: as the checker (parity of this run's first outputs,
+checker_leg) and, at N = 1, as the CPU baseline timing the reference's own
+subr.c checksum unit (oracle/_ref, when built) or the oracle restatement on a
+bounded sample of the same workload.  Host-resident burst rates of SURVEY
+§8(f) ranks 1-2 (tools/txburst, N = 1) are reported under extra.burst.
 """
 import argparse
 import json
@@ -46,6 +49,7 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-rss", action="store_true", help="skip the Toeplitz RSS lines")
+    ap.add_argument("--no-burst", action="store_true", help="skip the host-resident burst lines")
     ap.add_argument("--only", choices=["1500", "64", "imix", "rss"], default=None,
                     help="time one workload only (profiling runs)")
     return ap.parse_args()
@@ -161,16 +165,12 @@ def bench_rss(torch, dist, eng, cgck, plan, steps, warmup):
     wall_h, ev_h = timed(torch, dist, eng, cgck,
                          lambda: eng.toeplitz(d.ptr, n, 12, 12, RSS_KEY, o.ptr, mask=0x7F),
                          steps, warmup)
-    # parity spot check of this run: first 4096 tuples vs the oracle
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle
+    # this run's first 4096 tuples and results, for the parity check of the checker leg
     host = np.zeros(4096 * 12, np.uint8)
     got = np.zeros(4096, np.uint32)
     d.download(host, stream=eng.stream)
     o.download(got, stream=eng.stream)
     eng.sync()
-    exp = oracle.port().toeplitz_batch(host, 4096, 12, 12, np.frombuffer(RSS_KEY, np.uint8), mask=0x7F)
-    bad_h = int(np.count_nonzero(got != exp))
     d.free()
     o.free()
 
@@ -190,7 +190,74 @@ def bench_rss(torch, dist, eng, cgck, plan, steps, warmup):
     eng.sync()
     out.free()
     cnt.free()
-    return {"hash": (wall_h, ev_h, n, bad_h), "dst": (wall_d, ev_d, tuples, int(c[0]))}
+    return {"hash": (wall_h, ev_h, n), "hash_sample": (host, got), "dst": (wall_d, ev_d, tuples, int(c[0]))}
+
+
+BURSTS = (32, 256, 2048)   # receive / transmit burst sizes (netmap-like 2048 B slots)
+
+
+def bench_burst():
+    """SURVEY §8(f) ranks 1 and 2 at the transport's burst granularity, through
+    the C-ABI from C (tools/txburst.c): a BSD-verify cgck_desc_host per RX
+    burst, and the deferred TX window (per packet udp_cksum + in_cksum queued,
+    one cgck_tx_flush).  Host-resident, so PCIe/latency bound: never `value`."""
+    import subprocess
+    exe = os.path.join(ROOT, "tools", "txburst")
+    if not os.path.exists(exe):
+        return None
+    r = subprocess.run([exe, "0.3"], capture_output=True, text=True, timeout=180)
+    if r.returncode != 0:
+        return {"error": r.stderr.strip()[-300:]}
+    return [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+
+
+def checker_leg(res, plan, cgck):
+    """Parity of this run's outputs against the oracle (rank 0; the oracle is
+    only the checker here): the first 65536 1500 B packets (every 16th) and
+    the first 4096 hashed tuples."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    P = oracle.port()
+    if "out_1500" in res:
+        o = res["out_1500"]
+        bad, chk = P.check_synth_strided(len(o), 1500, 1500, plan["seed"], cgck.GEN_BOTH, o, 16)
+        res["parity_1500"] = {"checked": chk, "mismatches": bad}
+    if "rss" in res:
+        host, got = res["rss"]["hash_sample"]
+        exp = P.toeplitz_batch(host, 4096, 12, 12, np.frombuffer(RSS_KEY, np.uint8), mask=0x7F)
+        res["parity_rss"] = {"checked": 4096, "mismatches": int(np.count_nonzero(got != exp))}
+
+
+def cpu_burst():
+    """The reference's per-packet pair (in_cksum(ip, 20) + udp_cksum(ip, len - 20),
+    the recompute that both verify and fill perform) over one burst of the same
+    ring layout, on one pinned core: microseconds per burst."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    P = oracle.port()
+    R = oracle.reference()
+    fin, fudp = (R or P).fn_pointers()
+    cpus = sorted(os.sched_getaffinity(0))
+    old = set(cpus)
+    rows = []
+    try:
+        os.sched_setaffinity(0, {cpus[len(cpus) // 2]})
+        for ln in (1500, 64):
+            ring = P.stream_bytes(0, max(BURSTS) * 2048, SEED)
+            P.stamp_strided(ring[14:], max(BURSTS) - 1, 2048, ln)
+            for b in BURSTS:
+                m = min(b, max(BURSTS) - 1)
+                reps = max(1, int(2e6 // (m * ln)))
+                sec, _ = P.cpu_bench(fin, fudp, ring[14:], m, 2048, ln, threads=1, reps=reps)
+                rows.append({"pkt_len": ln, "burst": b, "us_per_burst": sec / reps * 1e6 * b / m,
+                             "mpkt_s": m * reps / sec / 1e6})
+    finally:
+        os.sched_setaffinity(0, old)
+    return {"unit": "us per burst", "cores": 1, "kind": "reference" if R else "port",
+            "sample": "in_cksum(ip,20)+udp_cksum(ip,len-20) per packet over one burst of 2048 B "
+                      "slots (IPv4 at +14), cache-warm", "rows": rows}
 
 
 def cpu_rss(seconds):
@@ -320,12 +387,7 @@ def main():
     if args.only in (None, "1500"):
         wall, ev_ms, o = bench_strided(torch, dist, eng, cgck, n, 1500, plan, args.steps, args.warmup)
         res["1500"] = (wall, ev_ms)
-        # parity spot check of the timed run's output (first packets vs the referee)
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import oracle
-        bad, chk = oracle.port().check_synth_strided(min(n, 65536), 1500, 1500, plan["seed"],
-                                                     cgck.GEN_BOTH, o, 16)
-        res["parity_1500"] = {"checked": chk, "mismatches": bad}
+        res["out_1500"] = o[:min(n, 65536)].copy()   # checked by the checker leg
     if not args.no_extra and args.only in (None, "64"):
         wall, ev_ms, _ = bench_strided(torch, dist, eng, cgck, n, 64, plan, args.steps, args.warmup)
         res["64"] = (wall, ev_ms)
@@ -336,8 +398,16 @@ def main():
     if not args.no_rss and args.only in (None, "rss"):
         res["rss"] = bench_rss(torch, dist, eng, cgck, plan, args.steps, args.warmup)
 
-    cpu = cpu_r = cpu_64 = None
+    burst = None
+    if dist.rank == 0 and dist.world == 1 and not args.no_burst and args.only is None:
+        burst = bench_burst()
+    if dist.rank == 0:
+        checker_leg(res, plan, cgck)
+
+    cpu = cpu_r = cpu_64 = cpu_b = None
     if dist.rank == 0 and dist.world == 1 and not args.no_cpu:
+        if burst:
+            cpu_b = cpu_burst()
         cpu = cpu_baseline(args.cpu_seconds)
         if "64" in res:
             cpu_64 = cpu_baseline_64(min(3.0, args.cpu_seconds))
@@ -392,7 +462,7 @@ def main():
             extra["imix"]["gb_s"] = nbytes * W * K / wall / 1e9
             extra["imix"].update({"kernel": "slot2_kernel<true, false>", "traffic": load_traffic("imix")})
         if "rss" in res:
-            wall_h, ev_h, nt, bad_h = res["rss"]["hash"]
+            wall_h, ev_h, nt = res["rss"]["hash"]
             wall_d, ev_d, td, written = res["rss"]["dst"]
             ach = nt * 16 / (ev_h * 1e-3)
             extra["rss_hash"] = {
@@ -401,7 +471,7 @@ def main():
                 "gtuple_s": nt * W * K / wall_h / 1e9, "ms_per_step": wall_h / K * 1e3,
                 "kernel_ms": ev_h, "achieved_gbs": ach / 1e9, "hbm_frac": ach / HBM_PEAK,
                 "algorithmic_bytes_per_launch": nt * 16, "traffic": load_traffic("rss_hash"),
-                "parity": {"checked": 4096, "mismatches": bad_h}}
+                "parity": res.get("parity_rss")}
             extra["dst_cache"] = {
                 "workload": f"thread_init_dst_cache enumeration of {td} tuples per GPU "
                             f"({RSS_DST[0]} laddrs x {RSS_DST[1]} faddrs x 60536 ports), "
@@ -410,6 +480,13 @@ def main():
                 "kernel_ms": ev_d, "entries_written": written}
             if cpu_r:
                 extra["dst_cache"]["cpu_baseline"] = cpu_r
+        if burst:
+            extra["burst"] = {"what": "SURVEY §8(f) rank 1 (rx_verify: cgck_desc_host, BSD verify flags, "
+                                      "per RX burst) and rank 2 (tx_fill: cgck_tx_begin, per packet "
+                                      "udp_cksum + in_cksum, cgck_tx_flush) on host-resident 2048 B ring "
+                                      "slots, called from C (tools/txburst.c)", "rows": burst}
+            if cpu_b:
+                extra["burst"]["cpu_baseline"] = cpu_b
         if extra:
             out["extra"] = extra
         if "value" not in out:   # --only 64 / imix / rss profiling runs

@@ -15,6 +15,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <mutex>
+#include <shared_mutex>
 #include <vector>
 
 #include "cgck_internal.h"
@@ -275,8 +277,39 @@ extern "C" int cgck_desc(cgck_ctx_t *c, void *base, const cgck_desc_t *desc, uin
 }
 
 // --------------------------------------------------------------------------
-// Host-resident batch: H2D, kernel, D2H
+// Host-resident batch
 // --------------------------------------------------------------------------
+//
+// Three ways in, by what the caller's memory is:
+//  * registered ring memory (cgck_host_register: the netmap pool, XDP UMEM,
+//    DPDK mempool): the kernel reads the packets over the fabric where they
+//    lie and in-place stores land there — no copy of the packet bytes;
+//  * a small pageable burst (packet bytes <= kStageBytes): the CPU copies
+//    each packet into this context's pinned staging and the kernel reads the
+//    staging — one launch and one synchronisation, the RX-burst latency path
+//    (a DMA from pageable memory costs more than the copy at these sizes);
+//  * a large pageable batch: DMA of [base, base + bytes) into device scratch.
+// Descriptors and per-packet outputs pass through pinned staging in the first
+// two cases.
+
+static constexpr size_t kStageBytes = 512 << 10;
+
+// [p, p + bytes) inside one registered host allocation: its device pointer
+static void *registered_ptr(void *p, size_t bytes)
+{
+	hipPointerAttribute_t a, b;
+	if (hipPointerGetAttributes(&a, p) != hipSuccess || a.type != hipMemoryTypeHost || !a.devicePointer) {
+		(void)hipGetLastError();
+		return nullptr;
+	}
+	void *end = (uint8_t *)p + bytes - 1;
+	if (hipPointerGetAttributes(&b, end) != hipSuccess || b.type != hipMemoryTypeHost ||
+	    (uint8_t *)b.devicePointer - (uint8_t *)a.devicePointer != (ptrdiff_t)(bytes - 1)) {
+		(void)hipGetLastError();
+		return nullptr;
+	}
+	return a.devicePointer;
+}
 
 extern "C" int cgck_desc_host(cgck_ctx_t *c, void *base, size_t bytes, const cgck_desc_t *desc,
 			      uint64_t n, uint32_t flags, uint32_t *out, uint8_t *verdict)
@@ -290,7 +323,53 @@ extern "C" int cgck_desc_host(cgck_ctx_t *c, void *base, size_t bytes, const cgc
 		return 0;
 	if (!base || !desc)
 		return set_err(-EINVAL, "cgck_desc_host: NULL base or descriptors");
+	size_t pkt_bytes = 0;
+	for (uint64_t i = 0; i < n; i++) {
+		const uint64_t end = desc[i].frame_off + desc[i].l3_off + desc[i].ip_len;
+		if (end > bytes || end < desc[i].frame_off)
+			return set_err(-EINVAL, "cgck_desc_host: descriptor %llu reaches past the %zu bytes given",
+				       (unsigned long long)i, bytes);
+		pkt_bytes += ((size_t)desc[i].ip_len + 15) & ~(size_t)15;
+	}
 	HIP_TRY(hipSetDevice(c->device));
+	hipStream_t st = c->stream;
+	void *dev_base = registered_ptr(base, bytes);
+	if (dev_base || pkt_bytes <= kStageBytes) {
+		// pinned staging: [packets (staged case)] | descriptors | out | verdict
+		const size_t sbytes = dev_base ? 0 : pkt_bytes;
+		const size_t d_off = sbytes, o_off = (d_off + 12 * n + 15) & ~(size_t)15, v_off = o_off + 4 * n;
+		if ((rc = grow_host((void **)&c->h_stage, &c->h_stage_cap, v_off + n)))
+			return rc;
+		uint8_t *h = c->h_stage;
+		cgck_desc_t *d = (cgck_desc_t *)(h + d_off);
+		if (dev_base) {
+			memcpy(d, desc, 12 * n);
+		} else {
+			size_t at = 0;
+			for (uint64_t i = 0; i < n; i++) {
+				memcpy(h + at, (const uint8_t *)base + desc[i].frame_off + desc[i].l3_off, desc[i].ip_len);
+				d[i].frame_off = at;
+				d[i].l3_off = 0;
+				d[i].ip_len = desc[i].ip_len;
+				at += ((size_t)desc[i].ip_len + 15) & ~(size_t)15;
+			}
+		}
+		uint32_t *o = (uint32_t *)(h + o_off);
+		uint8_t *v = h + v_off;
+		KParams p = {dev_base ? (const uint8_t *)dev_base : h, d, n, 0, 0, 0, flags, o, v, nullptr, 0, nullptr};
+		if ((rc = run(c, p, c->desc_len_hint, st)))
+			return rc;
+		HIP_TRY(hipStreamSynchronize(st));
+		if (out)
+			memcpy(out, o, 4 * n);
+		if (verdict)
+			memcpy(verdict, v, n);
+		if ((flags & CGCK_STORE) && !dev_base)
+			for (uint64_t i = 0; i < n; i++)
+				memcpy((uint8_t *)base + desc[i].frame_off + desc[i].l3_off, h + d[i].frame_off,
+				       desc[i].ip_len);
+		return 0;
+	}
 	const size_t dbytes = 12 * n, obytes = 4 * n, vbytes = n;
 	if ((rc = grow_dev((void **)&c->d_bytes, &c->d_bytes_cap, bytes)))
 		return rc;
@@ -299,7 +378,6 @@ extern "C" int cgck_desc_host(cgck_ctx_t *c, void *base, size_t bytes, const cgc
 	uint8_t *d_desc = c->d_aux;
 	uint32_t *d_out = (uint32_t *)(c->d_aux + ((dbytes + 15) & ~(size_t)15));
 	uint8_t *d_ver = (uint8_t *)(d_out + n);
-	hipStream_t st = c->stream;
 	HIP_TRY(hipMemcpyAsync(c->d_bytes, base, bytes, hipMemcpyHostToDevice, st));
 	HIP_TRY(hipMemcpyAsync(d_desc, desc, dbytes, hipMemcpyHostToDevice, st));
 	KParams p = {c->d_bytes, (const cgck_desc_t *)d_desc, n, 0, 0, 0, flags, d_out, d_ver, nullptr, 0, nullptr};
@@ -315,14 +393,41 @@ extern "C" int cgck_desc_host(cgck_ctx_t *c, void *base, size_t bytes, const cgc
 	return 0;
 }
 
+// Ranges registered through cgck_host_register, so the deferred TX flush can
+// read queued packets where they lie.  Written only by register/unregister
+// (set-up time); each flush takes the reader side once.
+namespace {
+struct RegRange {
+	uint8_t *lo, *hi;
+	uint8_t *dev; // device pointer of lo
+};
+std::shared_mutex g_reg_mu;
+std::vector<RegRange> g_reg;
+} // namespace
+
 extern "C" int cgck_host_register(void *ptr, size_t bytes)
 {
 	HIP_TRY(hipHostRegister(ptr, bytes, hipHostRegisterDefault));
+	void *dev = nullptr;
+	if (hipHostGetDevicePointer(&dev, ptr, 0) != hipSuccess || !dev) {
+		(void)hipGetLastError();
+		return 0; // registered; the TX flush just keeps staging for it
+	}
+	std::unique_lock<std::shared_mutex> lk(g_reg_mu);
+	g_reg.push_back({(uint8_t *)ptr, (uint8_t *)ptr + bytes, (uint8_t *)dev});
 	return 0;
 }
 
 extern "C" int cgck_host_unregister(void *ptr)
 {
+	{
+		std::unique_lock<std::shared_mutex> lk(g_reg_mu);
+		for (size_t i = 0; i < g_reg.size(); i++)
+			if (g_reg[i].lo == (uint8_t *)ptr) {
+				g_reg.erase(g_reg.begin() + i);
+				break;
+			}
+	}
 	HIP_TRY(hipHostUnregister(ptr));
 	return 0;
 }
@@ -458,10 +563,25 @@ extern "C" int cgck_tx_flush(void)
 		return 0;
 	cgck_ctx *c = tls_ctx();
 	HIP_TRY(hipSetDevice(c->device));
-	// Stage every region 16-byte aligned, descriptors after them.
+	// Packets inside one registered range (the transport's pool, rank 3) are
+	// read where they lie; otherwise every region is staged 16-byte aligned
+	// in pinned memory.  Descriptors and outputs follow.
+	RegRange reg{nullptr, nullptr, nullptr};
+	{
+		std::shared_lock<std::shared_mutex> lk(g_reg_mu);
+		for (const RegRange &r : g_reg)
+			if (q[0].ip >= r.lo && q[0].ip < r.hi) {
+				reg = r;
+				break;
+			}
+	}
+	for (uint64_t i = 0; reg.lo && i < n; i++)
+		if (q[i].ip < reg.lo || q[i].ip + q[i].span > reg.hi)
+			reg.lo = nullptr;
 	size_t bytes = 0;
-	for (const TxEntry &e : q)
-		bytes += (e.span + 15) & ~(size_t)15;
+	if (!reg.lo)
+		for (const TxEntry &e : q)
+			bytes += (e.span + 15) & ~(size_t)15;
 	const size_t desc_off = bytes, out_off = (desc_off + 12 * n + 15) & ~(size_t)15;
 	int rc;
 	if ((rc = grow_host((void **)&c->h_stage, &c->h_stage_cap, out_off + 4 * n)))
@@ -470,17 +590,21 @@ extern "C" int cgck_tx_flush(void)
 	uint32_t *o = (uint32_t *)(c->h_stage + out_off);
 	size_t at = 0;
 	for (uint64_t i = 0; i < n; i++) {
-		memcpy(c->h_stage + at, q[i].ip, q[i].span);
-		d[i].frame_off = at;
+		if (reg.lo) {
+			d[i].frame_off = (uint64_t)(q[i].ip - reg.lo);
+		} else {
+			memcpy(c->h_stage + at, q[i].ip, q[i].span);
+			d[i].frame_off = at;
+			at += (q[i].span + 15) & ~(size_t)15;
+		}
 		d[i].l3_off = 0;
 		d[i].ip_len = (uint16_t)q[i].span;
-		at += (q[i].span + 15) & ~(size_t)15;
 	}
 	// Both kinds in one launch: IP entries ask for the header checksum, L4
 	// entries for the segment checksum; both read their fields as zero, as
 	// the reference's callers have just stored them (ip_output.c:61,
 	// tcp_subr.c:75 / gbtcp/tcp.c:426,436).
-	KParams p = {c->h_stage, d, n, 0, 0, 0, CGCK_IP | CGCK_L4 | CGCK_ZERO_FIELDS, o, nullptr, nullptr, 0, nullptr};
+	KParams p = {reg.lo ? reg.dev : c->h_stage, d, n, 0, 0, 0, CGCK_IP | CGCK_L4 | CGCK_ZERO_FIELDS, o, nullptr, nullptr, 0, nullptr};
 	if ((rc = run(c, p, 1500, c->stream)))
 		return rc;
 	HIP_TRY(hipStreamSynchronize(c->stream));

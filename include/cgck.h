@@ -128,9 +128,13 @@ int cgck_desc(cgck_ctx_t *ctx, void *base, const cgck_desc_t *desc, uint64_t n,
  * handled correctly; the hint only picks the faster kernel. */
 int cgck_set_desc_len_hint(cgck_ctx_t *ctx, uint32_t max_ip_len);
 
-/* Host-resident batch (ring memory): H2D of [base, base+bytes) and of the
- * descriptors through pinned staging, kernel, D2H of out/verdict (and, with
- * CGCK_STORE, the filled bytes back into `base`).  Synchronous. */
+/* Host-resident batch (ring memory), synchronous.  Registered memory
+ * (cgck_host_register) is read where it lies and in-place stores land there;
+ * a small pageable burst (packet bytes <= 512 KiB) is copied packet by packet
+ * into pinned staging that the kernel reads; a larger pageable batch goes by
+ * DMA of [base, base+bytes).  Results come back to out/verdict (and, with
+ * CGCK_STORE, the filled fields into `base`).  -EINVAL when a descriptor
+ * reaches past `bytes`. */
 int cgck_desc_host(cgck_ctx_t *ctx, void *base, size_t bytes,
 		   const cgck_desc_t *desc, uint64_t n, uint32_t flags,
 		   uint32_t *out, uint8_t *verdict);

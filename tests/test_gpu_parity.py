@@ -327,26 +327,61 @@ def test_verify_fixture_verdicts(engine, golden_verify, align):
         assert (v & 1) == 1 - c["toy_ip"] and ((v >> 1) & 1) == 1 - c["toy_l4"], c["kind"]
 
 
-def test_host_resident_batch(engine, port):
-    rng = np.random.default_rng(21)
-    buf, desc = random_batch(rng, 500, 1500)
-    for flags in (cgck.GEN_BOTH, cgck.FILL_BOTH, cgck.VERIFY_BSD):
-        ref = buf.copy()
-        exp, ever = port.batch_desc(ref, desc.view(np.uint8), len(desc), flags)
-        got = buf.copy()
-        out = np.zeros(len(desc), np.uint32)
-        ver = np.zeros(len(desc), np.uint8)
-        engine.desc_host(got, desc, flags, out, ver)
-        assert np.array_equal(out, exp) and np.array_equal(ver, ever) and np.array_equal(got, ref)
+@pytest.mark.parametrize("npk,registered", [(500, False), (3000, False), (500, True), (3000, True)])
+def test_host_resident_batch(engine, port, npk, registered):
+    """cgck_desc_host's three ways in: a small pageable burst (pinned staging,
+    500 packets), a large pageable batch (DMA, 3000 packets > 512 KiB), and
+    ring memory registered with cgck_host_register (read where it lies)."""
+    rng = np.random.default_rng(21 + npk)
+    buf, desc = random_batch(rng, npk, 1500)
+    L = cgck.load()
+    if registered:
+        size = (len(buf) + 4095) // 4096 * 4096
+        raw = np.zeros(size + 4096, np.uint8)
+        off = (-raw.ctypes.data) % 4096
+        ring = raw[off:off + size]
+        assert L.cgck_host_register(ring.ctypes.data, size) == 0
+    try:
+        for flags in (cgck.GEN_BOTH, cgck.FILL_BOTH, cgck.VERIFY_BSD):
+            ref = buf.copy()
+            exp, ever = port.batch_desc(ref, desc.view(np.uint8), len(desc), flags)
+            if registered:
+                ring[:len(buf)] = buf
+                got = ring[:len(buf)]
+            else:
+                got = buf.copy()
+            out = np.zeros(len(desc), np.uint32)
+            ver = np.zeros(len(desc), np.uint8)
+            engine.desc_host(got, desc, flags, out, ver)
+            assert np.array_equal(out, exp) and np.array_equal(ver, ever) and np.array_equal(got, ref)
+    finally:
+        if registered:
+            L.cgck_host_unregister(ring.ctypes.data)
 
 
-def test_deferred_tx_fill(engine, port):
+def test_host_resident_desc_past_buffer(engine):
+    """A descriptor that reaches past the given bytes is refused (-EINVAL),
+    not read."""
+    buf = np.zeros(4096, np.uint8)
+    desc = np.zeros(2, cgck.DESC_DTYPE)
+    desc[0] = (0, 0, 1500)
+    desc[1] = (3000, 14, 1500)
+    with pytest.raises(cgck.CgckError):
+        engine.desc_host(buf, desc, cgck.GEN_BOTH, np.zeros(2, np.uint32), np.zeros(2, np.uint8))
+
+
+@pytest.mark.parametrize("registered", [False, True])
+def test_deferred_tx_fill(engine, port, registered):
     """Deferred TX window: the stack's own call pattern (tcp_output.c:416-418
     then ip_output.c:61-64, each storing the return value) inside
     cgck_tx_begin/flush yields the same bytes as the synchronous reference
-    sequence."""
+    sequence — staged, or read in place from a registered ring."""
     rng = np.random.default_rng(23)
-    ring = np.zeros((256, 2048), np.uint8)   # netmap-like slots, IP at +14
+    raw = np.zeros(256 * 2048 + 4096, np.uint8)
+    off = (-raw.ctypes.data) % 4096
+    ring = raw[off:off + 256 * 2048].reshape(256, 2048)   # netmap-like slots, IP at +14
+    if registered:
+        assert cgck.load().cgck_host_register(ring.ctypes.data, ring.nbytes) == 0
     want = []
     for i in range(256):
         ln = int(rng.integers(40, 523))       # MTU 522 (con-gen.c:741)
@@ -372,7 +407,11 @@ def test_deferred_tx_fill(engine, port):
         row[14 + 10:14 + 12] = 0                                # ip->ip_sum = 0
         v = cgck.ip_cksum(row, 14)                              # ip->ip_sum = ip_cksum(ip)
         row[14 + 10:14 + 12] = np.frombuffer(np.uint16(v).tobytes(), np.uint8)
-    assert cgck.tx_flush() == 2 * len(want)
+    try:
+        assert cgck.tx_flush() == 2 * len(want)
+    finally:
+        if registered:
+            cgck.load().cgck_host_unregister(ring.ctypes.data)
     for i, (ln, ref, fo) in enumerate(want):
         assert np.array_equal(ring[i, 14:14 + ln], ref), i
 

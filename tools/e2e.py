@@ -22,7 +22,6 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "con-gen_amd"))
-sys.path.insert(0, os.path.join(ROOT, "oracle"))
 import cgck  # noqa: E402
 
 L = cgck.load()

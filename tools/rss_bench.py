@@ -8,11 +8,9 @@ import argparse
 import json
 import os
 import sys
-import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "con-gen_amd"))
-sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
 import numpy as np  # noqa: E402
 
@@ -61,25 +59,10 @@ def bench_dst(eng, nl, nf, qn, qi, cap, reps):
             "gtuple_s_scanned": n / ms / 1e6 if cap >= n else None}
 
 
-def cpu_dst(nl, nf, qn, qi, cap):
-    import oracle
-    P = oracle.port()
-    R = oracle.reference_rss()
-    fn = R.fn_rss_hash4() if R else None
-    key = np.frombuffer(KEY, np.uint8)
-    t0 = time.perf_counter()
-    e = P.dst_cache(0x0A000001, 0x0A000000 + nl, 0x0A010000, 0x0A010000 + nf - 1, 0x5000, qn, qi,
-                    key, cap, hash_fn=fn)
-    t = time.perf_counter() - t0
-    return {"kind": "reference" if R else "port", "tuples": nl * nf * 60536, "written": len(e),
-            "s": t, "gtuple_s": nl * nf * 60536 / t / 1e9}
-
-
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=64 << 20)
     ap.add_argument("--reps", type=int, default=20)
-    ap.add_argument("--cpu", action="store_true")
     a = ap.parse_args()
     import torch  # noqa: F401  (shares torch's HIP runtime, as bench.py does)
     eng = cgck.Engine(0)
@@ -87,8 +70,6 @@ def main():
     print(json.dumps({"dst_full": bench_dst(eng, 4, 256, 8, 3, 1 << 31, a.reps)}), flush=True)
     print(json.dumps({"dst_default": bench_dst(eng, 1, 1, 4, 1, 100000, a.reps)}), flush=True)
     print(json.dumps({"dst_100k_of_16": bench_dst(eng, 1, 256, 16, 3, 100000, a.reps)}), flush=True)
-    if a.cpu:
-        print(json.dumps({"cpu_dst": cpu_dst(1, 16, 8, 3, 1 << 31)}), flush=True)
     eng.close()
 
 

@@ -1,0 +1,180 @@
+/*
+ * Burst-level timing of SURVEY §8(f) ranks 1 and 2 through the C-ABI, called
+ * the way con-gen's C code would call it (no Python per packet):
+ *
+ *   rx_verify — one cgck_desc_host() per receive burst over a netmap-like
+ *               ring (2048-byte slots, IPv4 header at +14) with the BSD
+ *               verify semantics (ip_input.c:45-58, tcp_input.c:75-85);
+ *               verdicts and results come back to host memory.  Measured
+ *               on pageable ring memory, then with the ring registered
+ *               (cgck_host_register, rank 3: read where it lies).
+ *   tx_fill   — the deferred TX window: per packet the stack's own calls,
+ *               udp_cksum(ip, len - 20) then in_cksum(ip, 20), queued between
+ *               cgck_tx_begin() and cgck_tx_flush() (glue.c:15-41 batch point),
+ *               the flush writing every field in place.
+ *
+ * Prints one JSON line per (mode, packet length, burst).  Parity of both
+ * paths is covered by tests/test_gpu_parity.py; here each run also checks
+ * that the verify pass flags exactly the packets it corrupted.
+ *
+ *   tools/txburst [seconds per cell, default 0.4]
+ */
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include "cgck.h"
+
+#define SLOT 2048
+#define L3 14
+
+static double now(void)
+{
+	struct timespec ts;
+	clock_gettime(CLOCK_MONOTONIC, &ts);
+	return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+
+static int cmpd(const void *a, const void *b)
+{
+	double x = *(const double *)a, y = *(const double *)b;
+	return x < y ? -1 : x > y;
+}
+
+/* IPv4 + TCP packet of `len` bytes with pseudo-random payload, zero checksum fields */
+static void make_packet(uint8_t *ip, int len, uint64_t *s)
+{
+	for (int i = 0; i < len; i++) {
+		*s ^= *s << 13;
+		*s ^= *s >> 7;
+		*s ^= *s << 17;
+		ip[i] = (uint8_t)*s;
+	}
+	ip[0] = 0x45;
+	ip[1] = 0;
+	ip[2] = (uint8_t)(len >> 8);
+	ip[3] = (uint8_t)len;
+	ip[9] = 6;
+	ip[10] = ip[11] = 0;
+	ip[20 + 16] = ip[20 + 17] = 0;
+}
+
+static double median(double *t, int n)
+{
+	qsort(t, n, sizeof(double), cmpd);
+	return t[n / 2];
+}
+
+int main(int argc, char **argv)
+{
+	const double budget = argc > 1 ? atof(argv[1]) : 0.4;
+	const int bursts[] = {32, 256, 2048};
+	const int lens[] = {1500, 64};
+	const int maxb = 2048, maxit = 100000;
+	uint8_t *ring = aligned_alloc(4096, (size_t)maxb * SLOT);
+	cgck_desc_t *desc = malloc(sizeof(cgck_desc_t) * maxb);
+	uint32_t *out = malloc(4 * maxb);
+	uint8_t *ver = malloc(maxb);
+	double *t = malloc(sizeof(double) * maxit);
+	cgck_ctx_t *ctx;
+	if (!ring || !desc || !out || !ver || !t || cgck_ctx_create(0, &ctx)) {
+		fprintf(stderr, "txburst: setup failed: %s\n", cgck_last_error());
+		return 1;
+	}
+	for (int li = 0; li < 2; li++) {
+		const int len = lens[li];
+		uint64_t s = 0x9E3779B97F4A7C15ull;
+		for (int i = 0; i < maxb; i++) {
+			make_packet(ring + (size_t)i * SLOT + L3, len, &s);
+			desc[i].frame_off = (uint64_t)i * SLOT;
+			desc[i].l3_off = L3;
+			desc[i].ip_len = (uint16_t)len;
+		}
+		/* fill both fields in place (the TX result a receiver would see) */
+		if (cgck_desc_host(ctx, ring, (size_t)maxb * SLOT, desc, maxb,
+				   CGCK_IP | CGCK_L4 | CGCK_ZERO_FIELDS | CGCK_STORE, out, NULL)) {
+			fprintf(stderr, "txburst: fill failed: %s\n", cgck_last_error());
+			return 1;
+		}
+		/* corrupt one payload byte of every 64th packet */
+		for (int i = 0; i < maxb; i += 64)
+			ring[(size_t)i * SLOT + L3 + len - 1] ^= 0x5A;
+		for (int bi = 0; bi < 6; bi++) {
+			/* cells 3..5: the same bursts with the ring registered (rank 3) */
+			const int R = bursts[bi % 3], reg = bi >= 3;
+			const uint32_t vf = CGCK_IP | CGCK_L4 | CGCK_VERIFY | CGCK_V_IP_ZERO_IS_FFFF |
+					    CGCK_V_UDP_ZERO_SKIP;
+			if (bi == 3 && cgck_host_register(ring, (size_t)maxb * SLOT)) {
+				fprintf(stderr, "txburst: register failed: %s\n", cgck_last_error());
+				return 1;
+			}
+			int it = 0, bad_l4 = 0, bad_ip = 0;
+			double t0 = now();
+			for (int w = 0; w < 20; w++)
+				cgck_desc_host(ctx, ring, (size_t)R * SLOT, desc, R, vf, out, ver);
+			while (it < maxit && now() - t0 < budget) {
+				double a = now();
+				if (cgck_desc_host(ctx, ring, (size_t)R * SLOT, desc, R, vf, out, ver)) {
+					fprintf(stderr, "txburst: verify failed: %s\n", cgck_last_error());
+					return 1;
+				}
+				t[it++] = now() - a;
+			}
+			for (int i = 0; i < R; i++) {
+				bad_ip += (ver[i] & CGCK_BAD_IP) != 0;
+				bad_l4 += (ver[i] & CGCK_BAD_L4) != 0;
+			}
+			const double us = median(t, it) * 1e6;
+			printf("{\"mode\": \"%s\", \"pkt_len\": %d, \"burst\": %d, \"iters\": %d, "
+			       "\"us_median\": %.2f, \"mpkt_s\": %.3f, \"bad_ip\": %d, \"bad_l4\": %d, "
+			       "\"bad_l4_expected\": %d}\n",
+			       reg ? "rx_verify_registered" : "rx_verify", len, R, it, us, R / us, bad_ip, bad_l4,
+			       (R + 63) / 64);
+			fflush(stdout);
+		}
+		cgck_host_unregister(ring);
+		for (int bi = 0; bi < 6; bi++) {
+			/* cells 3..5: the ring registered, the flush reads it in place */
+			const int R = bursts[bi % 3], reg = bi >= 3;
+			int it = 0, w = 0;
+			if (bi == 3 && cgck_host_register(ring, (size_t)maxb * SLOT)) {
+				fprintf(stderr, "txburst: register failed: %s\n", cgck_last_error());
+				return 1;
+			}
+			double t0 = now();
+			while (it < maxit && now() - t0 < budget + 0.05) {
+				double a = now();
+				cgck_tx_begin();
+				for (int i = 0; i < R; i++) {
+					uint8_t *ip = ring + (size_t)i * SLOT + L3;
+					uint16_t v;
+					ip[20 + 16] = ip[20 + 17] = 0; /* tcp_template: th_sum = 0 */
+					v = udp_cksum((struct ip *)ip, len - 20); /* th->th_sum = tcp_cksum(...) */
+					memcpy(ip + 20 + 16, &v, 2);
+					ip[10] = ip[11] = 0;           /* ip->ip_sum = 0 */
+					v = in_cksum(ip, 20);          /* ip->ip_sum = ip_cksum(ip) */
+					memcpy(ip + 10, &v, 2);
+				}
+				const int r = cgck_tx_flush();
+				if (r != 2 * R) {
+					fprintf(stderr, "txburst: flush wrote %d of %d: %s\n", r, 2 * R,
+						cgck_last_error());
+					return 1;
+				}
+				if (w++ >= 20)
+					t[it++] = now() - a;
+			}
+			const double us = median(t, it) * 1e6;
+			printf("{\"mode\": \"%s\", \"pkt_len\": %d, \"burst\": %d, \"iters\": %d, "
+			       "\"us_median\": %.2f, \"mpkt_s\": %.3f}\n",
+			       reg ? "tx_fill_registered" : "tx_fill", len, R, it, us, R / us);
+			fflush(stdout);
+		}
+		cgck_host_unregister(ring);
+	}
+	cgck_ctx_destroy(ctx);
+	cgck_thread_release();
+	return 0;
+}
