@@ -290,8 +290,13 @@ __device__ __forceinline__ void finish(const KParams &p, uint64_t k, uint64_t a0
 // than one store per iteration: 58.5% vs 65.5% of HBM peak on 64 B.)
 
 // Lane per slot: a window of kWaveStage consecutive packets of the wave's
-// range [sb, sb + kWaveStage), written by head lanes, flushed by all lanes.
-constexpr int kWaveStage = 256;
+// range [sb, sb + kWaveStage), written by head lanes, flushed by all lanes
+// with nontemporal stores.  2048-packet windows (40 KiB of LDS per block, 4
+// blocks per CU) against 256: +9.8 % on IMIX in the same process, 1024 with
+// nt +4-5 %, nt alone at 256 nothing (tools/ab_inproc.py,
+// profiles/r01/ab_slot_window.log): each flush's stores stall the next loads
+// once (in-order vmcnt), so fewer, longer flushes.
+constexpr int kWaveStage = 2048;
 
 struct WaveStage {
 	uint32_t *so;
@@ -307,7 +312,7 @@ __device__ __forceinline__ void wave_stage_flush(const KParams &p, WaveStage &s,
 	const int c = (int)(e - s.sb);
 	for (int i = l; i < c; i += 64) {
 		if (p.out)
-			gbl(p.out)[s.sb + i] = s.so[i];
+			__builtin_nontemporal_store(s.so[i], gbl(p.out) + s.sb + i);
 		if (p.verdict)
 			gbl(p.verdict)[s.sb + i] = s.sv[i];
 	}
@@ -1174,8 +1179,10 @@ static hipError_t launch_slot2_t(const KParams &p, int max_blocks, bool nt, hipS
 
 hipError_t launch_slot2(const KParams &p, int num_cus, bool nt, hipStream_t st)
 {
-	// 8 blocks per CU requested; 2 waves per SIMD are resident (178 VGPRs).
-	// $CGCK_BPC overrides the blocks per CU for A/B runs.
+	// 8 blocks per CU requested; 41 KiB of LDS per block (the 2048-packet
+	// output windows) keeps 3 resident per CU — 1984-packet windows (4
+	// resident) and 3072 (2) measured the same.  $CGCK_BPC overrides the
+	// blocks per CU for A/B runs.
 	static const int bpc = [] {
 		const char *e = getenv("CGCK_BPC");
 		return e && atoi(e) > 0 ? atoi(e) : 8;
