@@ -1,20 +1,25 @@
 #!/bin/sh
-# Build a variant of libcgck.so for A/B runs: copy the sources to a scratch
-# directory, apply a sed expression to one source file, compile to
-# con-gen_amd/<name>.so (git-ignored).  Host side only.
-#   tools/build_variant.sh NAME FILE 'SED-EXPR'
+# Build a variant of libcgck.so for A/B runs into con-gen_amd/<name>.so
+# (git-ignored).  Host side only.
+#   tools/build_variant.sh NAME FILE 'SED-EXPR'   working tree + one sed edit
+#   tools/build_variant.sh NAME --rev REV         the sources of git revision REV
 set -eu
-NAME=$1; FILE=$2; EXPR=$3
+NAME=$1
 R=$(cd "$(dirname "$0")/.." && pwd)
 T=$(mktemp -d /tmp/cgck_variant.XXXXXX)
 mkdir -p "$T/con-gen_amd"
-cp -r "$R/con-gen_amd/csrc" "$T/con-gen_amd/csrc"
-ln -s "$R/include" "$T/include"   # csrc includes ../../include/cgck.h
-sed -i "$EXPR" "$T/con-gen_amd/csrc/$FILE"
-if cmp -s "$R/con-gen_amd/csrc/$FILE" "$T/con-gen_amd/csrc/$FILE"; then echo "sed changed nothing" >&2; rm -rf "$T"; exit 1; fi
+if [ "$2" = "--rev" ]; then
+	(cd "$R" && git archive "$3" con-gen_amd/csrc include) | tar -x -C "$T"
+else
+	FILE=$2; EXPR=$3
+	cp -r "$R/con-gen_amd/csrc" "$T/con-gen_amd/csrc"
+	ln -s "$R/include" "$T/include"   # csrc includes ../../include/cgck.h
+	sed -i "$EXPR" "$T/con-gen_amd/csrc/$FILE"
+	if cmp -s "$R/con-gen_amd/csrc/$FILE" "$T/con-gen_amd/csrc/$FILE"; then echo "sed changed nothing" >&2; rm -rf "$T"; exit 1; fi
+fi
 cd "$T/con-gen_amd"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -Wall -Werror -mcode-object-version=5 \
-	-I"$R/include" -shared -o "$R/con-gen_amd/$NAME.so" \
+	-I"$T/include" -shared -o "$R/con-gen_amd/$NAME.so" \
 	csrc/cgck_group.hip csrc/cgck_lane.hip csrc/cgck_stream.hip csrc/cgck_synth.hip csrc/cgck_rss.hip \
 	csrc/cgck_dispatch.cpp csrc/cgck_api.cpp
 rm -rf "$T"
