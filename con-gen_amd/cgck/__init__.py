@@ -65,6 +65,7 @@ EXPORTS = (
     "cgck_host_alloc", "cgck_host_free", "cgck_memcpy", "cgck_memset", "cgck_event_create",
     "cgck_event_destroy", "cgck_event_record", "cgck_event_elapsed_ms", "cgck_probe_read",
     "toeplitz_hash", "rss_hash4", "cgck_toeplitz", "cgck_dst_cache", "cgck_dst_cache_host",
+    "cgck_burst_open", "cgck_burst_close",
 )
 
 
@@ -133,6 +134,8 @@ def bind(path):
     L.cgck_dst_cache.argtypes = [_vp, ctypes.POINTER(DstParams), _vp, _u32, _vp, _vp]
     L.cgck_dst_cache_host.argtypes = [_vp, ctypes.POINTER(DstParams), _vp, _u32,
                                       ctypes.POINTER(_u32)]
+    L.cgck_burst_open.argtypes = [_vp, _u32, ctypes.c_size_t, _u32]
+    L.cgck_burst_close.argtypes = [_vp]
     return L
 
 
@@ -195,6 +198,16 @@ def rss_hash4(laddr, faddr, lport, fport, key, key_size=None):
     k = _u8(key)
     return load().rss_hash4(laddr, faddr, lport, fport, k.ctypes.data,
                             len(k) if key_size is None else key_size)
+
+
+def burst_open(max_pkts=4096, max_bytes=4 << 20, idle_ms=0):
+    """cgck_burst_open(NULL, ...): the resident burst server on this thread's
+    drop-in context."""
+    _check(load().cgck_burst_open(None, max_pkts, max_bytes, idle_ms), "cgck_burst_open")
+
+
+def burst_close():
+    _check(load().cgck_burst_close(None), "cgck_burst_close")
 
 
 def tx_begin():
@@ -282,6 +295,13 @@ class Engine:
 
     def sync(self):
         _check(load().cgck_ctx_sync(self.ctx), "cgck_ctx_sync")
+
+    def burst_open(self, max_pkts=4096, max_bytes=4 << 20, idle_ms=0):
+        """cgck_burst_open: keep a burst server resident on this context."""
+        _check(load().cgck_burst_open(self.ctx, max_pkts, max_bytes, idle_ms), "cgck_burst_open")
+
+    def burst_close(self):
+        _check(load().cgck_burst_close(self.ctx), "cgck_burst_close")
 
     def set_desc_len_hint(self, n):
         _check(load().cgck_set_desc_len_hint(self.ctx, n), "cgck_set_desc_len_hint")

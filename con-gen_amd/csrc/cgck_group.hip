@@ -26,7 +26,7 @@ namespace cgck {
 constexpr int kGrpStage = 2048;
 
 template <int G, int S, int U, bool DESC, bool NT>
-__global__ __launch_bounds__(256) void cksum_kernel(KParams p)
+__device__ __forceinline__ void cksum_body(const KParams &p)
 {
 	__shared__ uint32_t so[kGrpStage];
 	constexpr int GPB = 256 / G;        // groups per block
@@ -189,6 +189,82 @@ __global__ __launch_bounds__(256) void cksum_kernel(KParams p)
 	}
 	if (stage && sc.it < sc.end)
 		flush(sc.end * PPB);
+}
+
+template <int G, int S, int U, bool DESC, bool NT>
+__global__ __launch_bounds__(256) void cksum_kernel(KParams p)
+{
+	cksum_body<G, S, U, DESC, NT>(p);
+}
+
+// --------------------------------------------------------------------------
+// Burst server: one resident workgroup that serves small host-resident
+// batches (RX bursts, TX flushes) without a launch or a stream
+// synchronisation per batch.  The host writes a request into a host-coherent
+// mailbox (BurstBox, cgck_internal.h) and bumps seq_req; thread 0 polls it
+// with system-scope acquire loads, the workgroup runs the group kernel's body
+// over the batch (descriptors, packets and outputs in host-coherent staging),
+// and thread 0 publishes seq_done with a system-scope release.  Every poll
+// loop is bounded: the server exits on `stop`, or after idle_ticks of the
+// 100 MHz real-time counter without a request (the host relaunches it on
+// the next request), so no launch outlives its context for long.
+// --------------------------------------------------------------------------
+
+__device__ __forceinline__ uint32_t sys_load(const uint32_t *p)
+{
+	return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const void *zero)
+{
+	__shared__ uint32_t cmd; // 1 run the pending request, 2 exit
+	uint32_t last = 0;       // thread 0: the last request served
+	if (threadIdx.x == 0)
+		last = sys_load(&box->seq_done);
+	for (;;) {
+		if (threadIdx.x == 0) {
+			const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+			const uint64_t idle = box->idle_ticks;
+			uint32_t c = 0;
+			while (c == 0) {
+				const uint32_t r = sys_load(&box->seq_req);
+				if (sys_load(&box->stop))
+					c = 2;
+				else if (r != last)
+					c = 1, last = r;
+				else if (__builtin_amdgcn_s_memrealtime() - t0 > idle)
+					c = 2;
+				else
+					__builtin_amdgcn_s_sleep(4);
+			}
+			cmd = c;
+		}
+		__syncthreads();
+		const uint32_t c = cmd;
+		if (c == 2)
+			break;
+		__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); // the host's request writes, every thread
+		const KParams p = {box->base, box->desc, box->n, 0, 0, 0, box->flags, box->out, box->verdict,
+				   nullptr, 0, zero};
+		// many packets per pass: each pass costs host round trips (descriptor,
+		// then packet bytes), so the shapes carry 256 / 64 packets per pass
+		if (box->max_len <= 80)
+			cksum_body<4, 2, 4, true, false>(p);
+		else
+			cksum_body<16, 6, 4, true, false>(p);
+		__builtin_amdgcn_fence(__ATOMIC_RELEASE, ""); // this thread's outputs, system scope
+		__syncthreads();
+		if (threadIdx.x == 0)
+			__hip_atomic_store(&box->seq_done, last, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+	}
+	if (threadIdx.x == 0)
+		__hip_atomic_store(&box->alive, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+hipError_t launch_burst_server(BurstBox *box, const void *zero, hipStream_t st)
+{
+	hipLaunchKernelGGL(burst_server_kernel, dim3(1), dim3(256), 0, st, box, zero);
+	return hipGetLastError();
 }
 
 template <int G, int S, int U, bool DESC>

@@ -33,6 +33,27 @@ struct KParams {
 	const void *zero; // kZeroBytes zero bytes of device memory (safe target for clamped loads)
 };
 
+// Mailbox of the burst server (cgck_group.hip), in host-coherent pinned
+// memory: the host fills a request and bumps seq_req (release); the server
+// answers with seq_done (release) once the outputs are visible.
+struct BurstBox {
+	uint32_t seq_req;    // host -> device: number of the pending request
+	uint32_t seq_done;   // device -> host: last request served
+	uint32_t stop;       // host -> device: exit now
+	uint32_t alive;      // host sets 1 at launch; the server clears it on exit
+	uint32_t n;          // request: packets
+	uint32_t flags;      // request: CGCK_* flags
+	uint32_t max_len;    // request: longest ip_len (picks the lane shape)
+	uint32_t pad;
+	uint64_t idle_ticks; // 100 MHz ticks without a request before the server exits
+	const uint8_t *base; // request: batch base (device view of the staging)
+	const cgck_desc_t *desc;
+	uint32_t *out;
+	uint8_t *verdict;
+};
+
+hipError_t launch_burst_server(BurstBox *box, const void *zero, hipStream_t st);
+
 // Kernel selection flags (see cgck_dispatch.cpp) and the measured defaults
 // (tools/sweep.py; profiles/r01).  The group kernel streams whole lines per
 // wave-instruction, so nontemporal loads + contiguous block ranges win

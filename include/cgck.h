@@ -159,6 +159,17 @@ int cgck_thread_release(void);
 int cgck_tx_begin(void);
 int cgck_tx_flush(void);
 
+/* Burst server (latency).  Keeps one workgroup
+ * resident on `ctx` (NULL: this thread's drop-in context) that serves small
+ * host-resident batches through a host-coherent mailbox: cgck_desc_host and
+ * the synchronous drop-in calls then skip the kernel launch and the stream
+ * synchronisation whenever a batch fits (at most max_pkts and 64 packets,
+ * max_bytes and 64 KiB of packet bytes).  The server exits after idle_ms without a
+ * request (0: 200 ms) and is relaunched by the next one; close stops it.
+ * cgck_ctx_destroy and cgck_thread_release close it too. */
+int cgck_burst_open(cgck_ctx_t *ctx, uint32_t max_pkts, size_t max_bytes, uint32_t idle_ms);
+int cgck_burst_close(cgck_ctx_t *ctx);
+
 /* Synthetic batches generated on the device.  Byte j of the
  * stream is byte (j & 7) of splitmix64(seed, j >> 3); each packet then gets
  * ver/ihl 0x45, tos 0, total length, ip_p = 6 and zeroed IP/TCP checksum

@@ -359,6 +359,106 @@ def test_host_resident_batch(engine, port, npk, registered):
             L.cgck_host_unregister(ring.ctypes.data)
 
 
+@pytest.mark.parametrize("registered", [False, True])
+def test_burst_server_desc_host(engine, port, registered):
+    """cgck_desc_host through the resident burst server (cgck_burst_open): the
+    same bytes, results and verdicts as the referee, staged or in place; a
+    batch larger than the server's capacity takes the launch path."""
+    L = cgck.load()
+    engine.burst_open(max_pkts=1024, max_bytes=1 << 20)
+    try:
+        for npk in (1, 37, 700, 1500):          # 1500 packets: over max_pkts, launch path
+            rng = np.random.default_rng(31 + npk)
+            buf, desc = random_batch(rng, npk, 1500)
+            if registered:
+                size = (len(buf) + 4095) // 4096 * 4096
+                raw = np.zeros(size + 4096, np.uint8)
+                off = (-raw.ctypes.data) % 4096
+                ring = raw[off:off + size]
+                assert L.cgck_host_register(ring.ctypes.data, size) == 0
+            try:
+                for flags in (cgck.GEN_BOTH, cgck.FILL_BOTH, cgck.VERIFY_BSD, cgck.VERIFY_TOY):
+                    ref = buf.copy()
+                    exp, ever = port.batch_desc(ref, desc.view(np.uint8), len(desc), flags)
+                    if registered:
+                        ring[:len(buf)] = buf
+                        got = ring[:len(buf)]
+                    else:
+                        got = buf.copy()
+                    out = np.zeros(len(desc), np.uint32)
+                    ver = np.zeros(len(desc), np.uint8)
+                    engine.desc_host(got, desc, flags, out, ver)
+                    assert np.array_equal(out, exp) and np.array_equal(ver, ever), (npk, flags)
+                    assert np.array_equal(got, ref), (npk, flags)
+            finally:
+                if registered:
+                    L.cgck_host_unregister(ring.ctypes.data)
+    finally:
+        engine.burst_close()
+
+
+def test_burst_server_idle_relaunch(engine, port):
+    """The server exits after idle_ms without a request and the next request
+    relaunches it; close is idempotent."""
+    import time
+    engine.burst_open(max_pkts=256, max_bytes=1 << 20, idle_ms=20)
+    try:
+        for rep in range(3):
+            rng = np.random.default_rng(41 + rep)
+            buf, desc = random_batch(rng, 64, 1500)
+            exp, ever = port.batch_desc(buf.copy(), desc.view(np.uint8), len(desc), cgck.VERIFY_BSD)
+            out, ver = np.zeros(len(desc), np.uint32), np.zeros(len(desc), np.uint8)
+            engine.desc_host(buf.copy(), desc, cgck.VERIFY_BSD, out, ver)
+            assert np.array_equal(out, exp) and np.array_equal(ver, ever), rep
+            time.sleep(0.1)                      # > idle_ms: the server has exited
+    finally:
+        engine.burst_close()
+    engine.burst_close()
+
+
+def test_burst_server_dropin_and_tx(port):
+    """The drop-in symbols and the deferred TX window on this thread's context
+    with its burst server open (cgck_burst_open(NULL, ...))."""
+    cgck.burst_open(max_pkts=512, max_bytes=1 << 20)
+    try:
+        rng = np.random.default_rng(5)
+        for n in (0, 1, 19, 20, 21, 64, 1479, 1480, 1500):
+            for off in (0, 1, 7):
+                buf = rng.integers(0, 256, off + n + 64, dtype=np.uint8)
+                assert cgck.in_cksum(buf, off, n) == port.in_cksum(buf, off, n), (n, off)
+        for ln in (20, 40, 64, 576, 1500):
+            pkt = rng.integers(0, 256, ln + 16, dtype=np.uint8)
+            pkt[0] = 0x45
+            pkt[9] = 6
+            assert cgck.udp_cksum(pkt, 0, ln - 20) == port.udp_cksum(pkt, 0, ln - 20), ln
+        ring = np.zeros((64, 2048), np.uint8)
+        want = []
+        for i in range(64):
+            ln = int(rng.integers(40, 1501))
+            pkt = rng.integers(0, 256, ln, dtype=np.uint8)
+            pkt[0] = 0x45
+            pkt[9] = 6
+            pkt[36:38] = 0
+            pkt[10:12] = 0
+            ring[i, 14:14 + ln] = pkt
+            ref = pkt.copy()
+            ref[36:38] = np.frombuffer(np.uint16(port.udp_cksum(ref, 0, ln - 20)).tobytes(), np.uint8)
+            ref[10:12] = np.frombuffer(np.uint16(port.in_cksum(ref, 0, 20)).tobytes(), np.uint8)
+            want.append((ln, ref))
+        cgck.tx_begin()
+        for i, (ln, ref) in enumerate(want):
+            row = ring[i]
+            v = cgck.udp_cksum(row, 14, ln - 20)
+            row[14 + 36:14 + 38] = np.frombuffer(np.uint16(v).tobytes(), np.uint8)
+            v = cgck.ip_cksum(row, 14)
+            row[14 + 10:14 + 12] = np.frombuffer(np.uint16(v).tobytes(), np.uint8)
+        assert cgck.tx_flush() == 2 * len(want)
+        for i, (ln, ref) in enumerate(want):
+            assert np.array_equal(ring[i, 14:14 + ln], ref), i
+    finally:
+        cgck.burst_close()
+
+
 def test_host_resident_desc_past_buffer(engine):
     """A descriptor that reaches past the given bytes is refused (-EINVAL),
     not read."""

@@ -5,14 +5,17 @@
  *   rx_verify — one cgck_desc_host() per receive burst over a netmap-like
  *               ring (2048-byte slots, IPv4 header at +14) with the BSD
  *               verify semantics (ip_input.c:45-58, tcp_input.c:75-85);
- *               verdicts and results come back to host memory.  Measured
- *               on pageable ring memory, then with the ring registered
- *               (cgck_host_register, rank 3: read where it lies).
+ *               verdicts and results come back to host memory.
  *   tx_fill   — the deferred TX window: per packet the stack's own calls,
  *               udp_cksum(ip, len - 20) then in_cksum(ip, 20), queued between
  *               cgck_tx_begin() and cgck_tx_flush() (glue.c:15-41 batch point),
  *               the flush writing every field in place.
  *
+ * RX is measured four ways: the launch path on pageable ring memory, the
+ * ring registered (cgck_host_register: read where it lies), the resident
+ * burst server (cgck_burst_open: no launch or stream sync per call), and
+ * both; TX the first two; plus one synchronous drop-in in_cksum without and
+ * with the server.
  * Prints one JSON line per (mode, packet length, burst).  Parity of both
  * paths is covered by tests/test_gpu_parity.py; here each run also checks
  * that the verify pass flags exactly the packets it corrupted.
@@ -101,78 +104,110 @@ int main(int argc, char **argv)
 		/* corrupt one payload byte of every 64th packet */
 		for (int i = 0; i < maxb; i += 64)
 			ring[(size_t)i * SLOT + L3 + len - 1] ^= 0x5A;
-		for (int bi = 0; bi < 6; bi++) {
-			/* cells 3..5: the same bursts with the ring registered (rank 3) */
-			const int R = bursts[bi % 3], reg = bi >= 3;
-			const uint32_t vf = CGCK_IP | CGCK_L4 | CGCK_VERIFY | CGCK_V_IP_ZERO_IS_FFFF |
-					    CGCK_V_UDP_ZERO_SKIP;
-			if (bi == 3 && cgck_host_register(ring, (size_t)maxb * SLOT)) {
+		/* passes: 0 launch path, 1 registered ring, 2 burst server, 3 server + registered */
+		for (int pass = 0; pass < 4; pass++) {
+			const int reg = pass & 1, srv = pass >= 2;
+			static const char *rx_name[4] = {"rx_verify", "rx_verify_registered", "rx_verify_server",
+							 "rx_verify_registered_server"};
+			static const char *tx_name[2] = {"tx_fill", "tx_fill_registered"};
+			if (pass == 1 || pass == 2) /* the previous pass's TX cells refilled the fields: toggle the corruption back */
+				for (int i = 0; i < maxb; i += 64)
+					ring[(size_t)i * SLOT + L3 + len - 1] ^= 0x5A;
+			if (reg && cgck_host_register(ring, (size_t)maxb * SLOT)) {
 				fprintf(stderr, "txburst: register failed: %s\n", cgck_last_error());
 				return 1;
 			}
-			int it = 0, bad_l4 = 0, bad_ip = 0;
+			if (srv && (cgck_burst_open(ctx, maxb, (size_t)maxb * 1536, 0) ||
+				    cgck_burst_open(NULL, maxb, (size_t)maxb * 1536, 0))) {
+				fprintf(stderr, "txburst: burst_open failed: %s\n", cgck_last_error());
+				return 1;
+			}
+			for (int bi = 0; bi < 3; bi++) {
+				const int R = bursts[bi];
+				const uint32_t vf = CGCK_IP | CGCK_L4 | CGCK_VERIFY | CGCK_V_IP_ZERO_IS_FFFF |
+						    CGCK_V_UDP_ZERO_SKIP;
+				int it = 0, bad_l4 = 0, bad_ip = 0;
+				double t0 = now();
+				for (int w = 0; w < 20; w++)
+					cgck_desc_host(ctx, ring, (size_t)R * SLOT, desc, R, vf, out, ver);
+				while (it < maxit && now() - t0 < budget) {
+					double a = now();
+					if (cgck_desc_host(ctx, ring, (size_t)R * SLOT, desc, R, vf, out, ver)) {
+						fprintf(stderr, "txburst: verify failed: %s\n", cgck_last_error());
+						return 1;
+					}
+					t[it++] = now() - a;
+				}
+				for (int i = 0; i < R; i++) {
+					bad_ip += (ver[i] & CGCK_BAD_IP) != 0;
+					bad_l4 += (ver[i] & CGCK_BAD_L4) != 0;
+				}
+				const double us = median(t, it) * 1e6;
+				printf("{\"mode\": \"%s\", \"pkt_len\": %d, \"burst\": %d, \"iters\": %d, "
+				       "\"us_median\": %.2f, \"mpkt_s\": %.3f, \"bad_ip\": %d, \"bad_l4\": %d, "
+				       "\"bad_l4_expected\": %d}\n",
+				       rx_name[pass], len, R, it, us, R / us, bad_ip, bad_l4, (R + 63) / 64);
+				fflush(stdout);
+			}
+			for (int bi = 0; bi < 3 && !srv; bi++) { /* TX flushes do not use the server */
+				const int R = bursts[bi];
+				int it = 0, w = 0;
+				double t0 = now();
+				while (it < maxit && now() - t0 < budget + 0.05) {
+					double a = now();
+					cgck_tx_begin();
+					for (int i = 0; i < R; i++) {
+						uint8_t *ip = ring + (size_t)i * SLOT + L3;
+						uint16_t v;
+						ip[20 + 16] = ip[20 + 17] = 0; /* tcp_template: th_sum = 0 */
+						v = udp_cksum((struct ip *)ip, len - 20); /* th->th_sum = tcp_cksum(...) */
+						memcpy(ip + 20 + 16, &v, 2);
+						ip[10] = ip[11] = 0;           /* ip->ip_sum = 0 */
+						v = in_cksum(ip, 20);          /* ip->ip_sum = ip_cksum(ip) */
+						memcpy(ip + 10, &v, 2);
+					}
+					const int r = cgck_tx_flush();
+					if (r != 2 * R) {
+						fprintf(stderr, "txburst: flush wrote %d of %d: %s\n", r, 2 * R,
+							cgck_last_error());
+						return 1;
+					}
+					if (w++ >= 20)
+						t[it++] = now() - a;
+				}
+				const double us = median(t, it) * 1e6;
+				printf("{\"mode\": \"%s\", \"pkt_len\": %d, \"burst\": %d, \"iters\": %d, "
+				       "\"us_median\": %.2f, \"mpkt_s\": %.3f}\n",
+				       tx_name[reg], len, R, it, us, R / us);
+				fflush(stdout);
+			}
+			if (srv) {
+				cgck_burst_close(ctx);
+				cgck_burst_close(NULL);
+			}
+			if (reg)
+				cgck_host_unregister(ring);
+		}
+		/* drop-in latency: one synchronous in_cksum(ip, 20), launch path vs server */
+		for (int srv = 0; srv < 2; srv++) {
+			int it = 0;
+			if (srv && cgck_burst_open(NULL, 64, 1 << 16, 0)) {
+				fprintf(stderr, "txburst: burst_open failed: %s\n", cgck_last_error());
+				return 1;
+			}
 			double t0 = now();
-			for (int w = 0; w < 20; w++)
-				cgck_desc_host(ctx, ring, (size_t)R * SLOT, desc, R, vf, out, ver);
 			while (it < maxit && now() - t0 < budget) {
 				double a = now();
-				if (cgck_desc_host(ctx, ring, (size_t)R * SLOT, desc, R, vf, out, ver)) {
-					fprintf(stderr, "txburst: verify failed: %s\n", cgck_last_error());
-					return 1;
-				}
+				volatile uint16_t v = in_cksum(ring + L3, 20);
+				(void)v;
 				t[it++] = now() - a;
 			}
-			for (int i = 0; i < R; i++) {
-				bad_ip += (ver[i] & CGCK_BAD_IP) != 0;
-				bad_l4 += (ver[i] & CGCK_BAD_L4) != 0;
-			}
-			const double us = median(t, it) * 1e6;
-			printf("{\"mode\": \"%s\", \"pkt_len\": %d, \"burst\": %d, \"iters\": %d, "
-			       "\"us_median\": %.2f, \"mpkt_s\": %.3f, \"bad_ip\": %d, \"bad_l4\": %d, "
-			       "\"bad_l4_expected\": %d}\n",
-			       reg ? "rx_verify_registered" : "rx_verify", len, R, it, us, R / us, bad_ip, bad_l4,
-			       (R + 63) / 64);
+			printf("{\"mode\": \"%s\", \"pkt_len\": 20, \"burst\": 1, \"iters\": %d, "
+			       "\"us_median\": %.2f}\n", srv ? "in_cksum_server" : "in_cksum", it, median(t, it) * 1e6);
 			fflush(stdout);
+			if (srv)
+				cgck_burst_close(NULL);
 		}
-		cgck_host_unregister(ring);
-		for (int bi = 0; bi < 6; bi++) {
-			/* cells 3..5: the ring registered, the flush reads it in place */
-			const int R = bursts[bi % 3], reg = bi >= 3;
-			int it = 0, w = 0;
-			if (bi == 3 && cgck_host_register(ring, (size_t)maxb * SLOT)) {
-				fprintf(stderr, "txburst: register failed: %s\n", cgck_last_error());
-				return 1;
-			}
-			double t0 = now();
-			while (it < maxit && now() - t0 < budget + 0.05) {
-				double a = now();
-				cgck_tx_begin();
-				for (int i = 0; i < R; i++) {
-					uint8_t *ip = ring + (size_t)i * SLOT + L3;
-					uint16_t v;
-					ip[20 + 16] = ip[20 + 17] = 0; /* tcp_template: th_sum = 0 */
-					v = udp_cksum((struct ip *)ip, len - 20); /* th->th_sum = tcp_cksum(...) */
-					memcpy(ip + 20 + 16, &v, 2);
-					ip[10] = ip[11] = 0;           /* ip->ip_sum = 0 */
-					v = in_cksum(ip, 20);          /* ip->ip_sum = ip_cksum(ip) */
-					memcpy(ip + 10, &v, 2);
-				}
-				const int r = cgck_tx_flush();
-				if (r != 2 * R) {
-					fprintf(stderr, "txburst: flush wrote %d of %d: %s\n", r, 2 * R,
-						cgck_last_error());
-					return 1;
-				}
-				if (w++ >= 20)
-					t[it++] = now() - a;
-			}
-			const double us = median(t, it) * 1e6;
-			printf("{\"mode\": \"%s\", \"pkt_len\": %d, \"burst\": %d, \"iters\": %d, "
-			       "\"us_median\": %.2f, \"mpkt_s\": %.3f}\n",
-			       reg ? "tx_fill_registered" : "tx_fill", len, R, it, us, R / us);
-			fflush(stdout);
-		}
-		cgck_host_unregister(ring);
 	}
 	cgck_ctx_destroy(ctx);
 	cgck_thread_release();
