@@ -589,7 +589,10 @@ def test_full_size_imix(engine, port):
 # drop-in symbols on its own context at the same time; results stay exact.
 # ---------------------------------------------------------------------------
 
-def test_dropin_concurrent_threads(engine, golden_basic):
+@pytest.mark.parametrize("server", [False, True])
+def test_dropin_concurrent_threads(engine, golden_basic, server):
+    """Eight threads on their own drop-in contexts; with `server`, each keeps
+    its own resident burst server (eight polling workgroups at once)."""
     import threading
     g = golden_basic["len_off_grid"]
     buf = hexa(g["buf_hex"])
@@ -598,6 +601,8 @@ def test_dropin_concurrent_threads(engine, golden_basic):
 
     def worker(tid):
         try:
+            if server:
+                cgck.burst_open(max_pkts=64, max_bytes=1 << 16)
             for rep in range(3):
                 off = (tid + rep) % 16
                 got = [cgck.in_cksum(buf, off, n) for n in g["lens"][::7]]
