@@ -55,3 +55,12 @@ def test_single_rank_is_noop():
     assert d.world == 1 and d.max(3.0) == 3.0
     d.barrier()
     d.close()
+
+
+def test_cpu_burst_leg_runs():
+    """bench.py's CPU burst baseline (oracle as the timed reference loop, one
+    pinned core) produces a row per packet length and burst size."""
+    r = bench.cpu_burst()
+    assert r["cores"] == 1 and r["kind"] in ("reference", "port")
+    assert {(x["pkt_len"], x["burst"]) for x in r["rows"]} == {(ln, b) for ln in (1500, 64) for b in bench.BURSTS}
+    assert all(x["us_per_burst"] > 0 for x in r["rows"])
