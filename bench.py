@@ -376,10 +376,14 @@ def main():
     args = parse()
     import torch   # first: the process then shares torch's HIP runtime
     dist = Dist()
-    torch.cuda.set_device(dist.local)
+    # one rank per GPU; ranks past the visible devices share them, which only
+    # happens when N>1 is rehearsed on a one-GPU box
+    ndev = torch.cuda.device_count()
+    dev = dist.local % ndev if ndev else dist.local
+    torch.cuda.set_device(dev)
     import cgck
     import numpy as np
-    eng = cgck.Engine(dist.local)
+    eng = cgck.Engine(dev)
     plan = shard_plan(dist.rank, dist.world, args.packets)
     n = plan["n"]
     res = {}
