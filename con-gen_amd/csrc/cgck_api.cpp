@@ -1135,6 +1135,32 @@ extern "C" int cgck_dev_alloc(size_t bytes, void **ptr)
 	*ptr = nullptr;
 	if (cgck_device_count() <= 0)
 		return set_err(-ENODEV, "cgck: no HIP device visible");
+	// Plain hipMalloc.  Physically contiguous allocations
+	// (hipDeviceMallocContiguous) were measured as a cure for the 64 B
+	// fast/slow state: every contiguous 1 GiB input of a
+	// probe read fast, but whole bench runs moved by -1.1..+2.7 points from
+	// box to box (profiles/r01/alloc_ab.log), so they stay an A/B option:
+	// $CGCK_DEV_ALLOC_FLAGS sets hipExtMallocWithFlags flags for requests up to
+	// $CGCK_DEV_ALLOC_CONTIG_MAX bytes (default 8 GiB).
+	static const unsigned cflags = [] {
+		const char *e = getenv("CGCK_DEV_ALLOC_FLAGS");
+		return e ? (unsigned)strtoul(e, nullptr, 0) : 0u;
+	}();
+	static const size_t cmax = [] {
+		const char *e = getenv("CGCK_DEV_ALLOC_CONTIG_MAX");
+		return e ? (size_t)strtoull(e, nullptr, 0) : (size_t)8 << 30;
+	}();
+	const unsigned aflags = bytes <= cmax ? cflags : 0u;
+	if (aflags) {
+		const hipError_t e = hipExtMallocWithFlags(ptr, bytes ? bytes : 1, aflags);
+		if (e == hipSuccess)
+			return 0;
+		(void)hipGetLastError();
+		if (getenv("CGCK_ALLOC_VERBOSE"))
+			fprintf(stderr, "cgck_dev_alloc: flags %#x for %zu bytes failed (%s), plain hipMalloc\n",
+				aflags, bytes, hipGetErrorString(e));
+	}
+	*ptr = nullptr;
 	HIP_TRY(hipMalloc(ptr, bytes ? bytes : 1));
 	return 0;
 }
