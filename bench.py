@@ -471,7 +471,7 @@ def main():
             ach = nt * 16 / (ev_h * 1e-3)
             extra["rss_hash"] = {
                 "workload": f"{nt} dense 12-byte tuples per GPU, rss_hash4 (Toeplitz, 40-byte key, "
-                            "mask 0x7F) each", "kernel": "toeplitz12x4_ab_kernel<3>",
+                            "mask 0x7F) each", "kernel": "toeplitz12x4_ab_kernel<12>",
                 "gtuple_s": nt * W * K / wall_h / 1e9, "ms_per_step": wall_h / K * 1e3,
                 "kernel_ms": ev_h, "achieved_gbs": ach / 1e9, "hbm_frac": ach / HBM_PEAK,
                 "algorithmic_bytes_per_launch": nt * 16, "traffic": load_traffic("rss_hash"),

@@ -217,21 +217,38 @@ hipError_t launch_toeplitz(const RssParams &p0, int num_cus, hipStream_t st)
 			const char *e = getenv("CGCK_RSS_VAR");
 			return e ? atoi(e) : kDefaultRssVariant;
 		}();
-		// 2 blocks per CU: 65.4 % of HBM peak vs 62.5 % at 8 (tools/rss_sweep.sh)
+		// 1 block per CU with a deep register ring (below); at the earlier
+		// depth 3, 2 blocks per CU read 65.4 % of HBM peak vs 62.5 % at 8
+		// (tools/rss_sweep.sh)
 		static const int bpc = [] {
 			const char *e = getenv("CGCK_RSS_BPC");
-			return e && atoi(e) > 0 ? atoi(e) : 2;
+			return e && atoi(e) > 0 ? atoi(e) : 1;
 		}();
-		// ring depth 3: 62.3-65.9 % vs 60.1-63.5 % for 2 and 63.5 % for 4 at 2
-		// blocks per CU (tools/rss_sweep.sh, two boxes; profiles/r01/sweep_rss_depth.log)
-		static const int depth = [] { // $CGCK_RSS_DEPTH: groups per lane in flight, 2..4
+		// ring depth 12 at 1 block per CU (181 VGPRs, no spills), in-process
+		// A/B chain (tools/ab_inproc.py, profiles/r01/ab_rss_depth_chain.log):
+		// depth 3 at 2 blocks/CU -> depth 4 at 1 block +1.7 %, 5 +3.1 %, 6 +4.6 %
+		// over 4; 8 +1.2 %, 10 +3.6 % over 6; 12 +2.9 %, 16 -1.7 % over 10
+		// (76.7 % of peak); 2 blocks/CU at depth 6 -8 %
+		static const int depth = [] { // $CGCK_RSS_DEPTH: groups per lane in flight, 2..6, 8, 10, 12, 16
 			const char *e = getenv("CGCK_RSS_DEPTH");
 			const int d = e ? atoi(e) : 0;
-			return d >= 2 && d <= 4 ? d : 3;
+			return (d >= 2 && d <= 6) || d == 8 || d == 10 || d == 12 || d == 16 ? d : 12;
 		}();
 		const uint64_t capb = (uint64_t)num_cus * bpc;
 		const dim3 gb((unsigned)(want < capb ? want : capb));
-		if (var == 2 && depth == 4)
+		if (var == 2 && depth == 16)
+			hipLaunchKernelGGL(toeplitz12x4_ab_kernel<16>, gb, dim3(256), 12 * 256 * 4, st, p, ng);
+		else if (var == 2 && depth == 12)
+			hipLaunchKernelGGL(toeplitz12x4_ab_kernel<12>, gb, dim3(256), 12 * 256 * 4, st, p, ng);
+		else if (var == 2 && depth == 10)
+			hipLaunchKernelGGL(toeplitz12x4_ab_kernel<10>, gb, dim3(256), 12 * 256 * 4, st, p, ng);
+		else if (var == 2 && depth == 8)
+			hipLaunchKernelGGL(toeplitz12x4_ab_kernel<8>, gb, dim3(256), 12 * 256 * 4, st, p, ng);
+		else if (var == 2 && depth == 6)
+			hipLaunchKernelGGL(toeplitz12x4_ab_kernel<6>, gb, dim3(256), 12 * 256 * 4, st, p, ng);
+		else if (var == 2 && depth == 5)
+			hipLaunchKernelGGL(toeplitz12x4_ab_kernel<5>, gb, dim3(256), 12 * 256 * 4, st, p, ng);
+		else if (var == 2 && depth == 4)
 			hipLaunchKernelGGL(toeplitz12x4_ab_kernel<4>, gb, dim3(256), 12 * 256 * 4, st, p, ng);
 		else if (var == 2 && depth == 3)
 			hipLaunchKernelGGL(toeplitz12x4_ab_kernel<3>, gb, dim3(256), 12 * 256 * 4, st, p, ng);
