@@ -65,8 +65,12 @@ EXPORTS = (
     "cgck_host_alloc", "cgck_host_free", "cgck_memcpy", "cgck_memset", "cgck_event_create",
     "cgck_event_destroy", "cgck_event_record", "cgck_event_elapsed_ms", "cgck_probe_read",
     "toeplitz_hash", "rss_hash4", "cgck_toeplitz", "cgck_dst_cache", "cgck_dst_cache_host",
-    "cgck_burst_open", "cgck_burst_close",
+    "cgck_burst_open", "cgck_burst_close", "cgck_thread_ctx", "cgck_set_error_handler",
+    "cgck_rx_begin", "cgck_rx_end", "cgck_window_stats", "cgck_ctx_last_kernel",
 )
+
+# cgck_error_fn: void (*)(const char *what, const char *msg, void *arg)
+ERROR_FN = ctypes.CFUNCTYPE(None, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_void_p)
 
 
 class CgckError(RuntimeError):
@@ -136,6 +140,13 @@ def bind(path):
                                       ctypes.POINTER(_u32)]
     L.cgck_burst_open.argtypes = [_vp, _u32, ctypes.c_size_t, _u32]
     L.cgck_burst_close.argtypes = [_vp]
+    L.cgck_thread_ctx.restype = _vp
+    L.cgck_set_error_handler.restype = None
+    L.cgck_set_error_handler.argtypes = [ERROR_FN, _vp]
+    L.cgck_rx_begin.argtypes = [_vp, ctypes.c_size_t, _vp, _u64]
+    L.cgck_window_stats.argtypes = [ctypes.POINTER(_u64)]
+    L.cgck_ctx_last_kernel.restype = ctypes.c_char_p
+    L.cgck_ctx_last_kernel.argtypes = [_vp]
     return L
 
 
@@ -208,6 +219,46 @@ def burst_open(max_pkts=4096, max_bytes=4 << 20, idle_ms=0):
 
 def burst_close():
     _check(load().cgck_burst_close(None), "cgck_burst_close")
+
+
+def fn_pointers():
+    """(in_cksum, udp_cksum) addresses in libcgck.so, for C harnesses that
+    call the drop-in symbols (oracle.Port.replay_rx, oracle_cpu_bench)."""
+    L = load()
+    return (ctypes.cast(L.in_cksum, ctypes.c_void_p).value,
+            ctypes.cast(L.udp_cksum, ctypes.c_void_p).value)
+
+
+def rx_begin(base, desc):
+    """cgck_rx_begin over a numpy byte array (the ring) and DESC_DTYPE
+    descriptors (ip_len = bytes received after l3_off).  Returns the number
+    of frames precomputed."""
+    assert desc.dtype == DESC_DTYPE
+    return _check(load().cgck_rx_begin(base.ctypes.data, base.nbytes, desc.ctypes.data, len(desc)),
+                  "cgck_rx_begin")
+
+
+def rx_end():
+    """cgck_rx_end: returns how many drop-in calls the window answered."""
+    return _check(load().cgck_rx_end(), "cgck_rx_end")
+
+
+def window_stats():
+    """[rx served, rx synchronous, tx queued, tx synchronous] of this thread."""
+    a = (_u64 * 4)()
+    _check(load().cgck_window_stats(a), "cgck_window_stats")
+    return list(a)
+
+
+_err_cb = None
+
+
+def set_error_handler(fn):
+    """cgck_set_error_handler: fn(what: str, msg: str) (None restores the
+    default).  The drop-ins abort if the handler returns."""
+    global _err_cb
+    _err_cb = None if fn is None else ERROR_FN(lambda w, m, a: fn(w.decode(), m.decode()))
+    load().cgck_set_error_handler(_err_cb if _err_cb is not None else ERROR_FN(), None)
 
 
 def tx_begin():
@@ -292,6 +343,12 @@ class Engine:
     @property
     def stream(self):
         return load().cgck_ctx_stream(self.ctx)
+
+    @property
+    def last_kernel(self):
+        """The kernel the dispatcher launched last on this context (the name
+        rocprofv3 reports)."""
+        return load().cgck_ctx_last_kernel(self.ctx).decode()
 
     def sync(self):
         _check(load().cgck_ctx_sync(self.ctx), "cgck_ctx_sync")

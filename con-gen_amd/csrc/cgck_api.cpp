@@ -1,12 +1,13 @@
 // cgck_api.cpp — host side of libcgck.so: the C-ABI declared in
-// include/cgck.h.  Contexts (stream + staging), the drop-in in_cksum /
-// udp_cksum symbols (subr.h:373-374), device-resident and host-resident
-// batches, the deferred TX fill, synthetic generation and timing.
+// include/cgck.h.  Contexts (stream + staging), device-resident and
+// host-resident batches, registered rings, the burst server, the Toeplitz
+// RSS batch and dst-cache entry points, synthetic generation and timing.
+// The drop-in symbols and the per-thread RX / TX windows are in
+// cgck_dropin.cpp.
 //
-// Every checksum this library returns is computed by the gfx950 kernels in
-// cgck_kernels.hip; there is no host arithmetic path.  Without a usable
-// device every entry point fails with -ENODEV (the drop-in symbols print the
-// reason and abort, since their prototype has no error channel).
+// Every checksum this library returns is computed by the gfx950 kernels
+// (cgck_group.hip, cgck_lane.hip); there is no host arithmetic path.  Without
+// a usable device every entry point fails with -ENODEV.
 #include <hip/hip_runtime.h>
 
 #include <errno.h>
@@ -16,11 +17,12 @@
 #include <string.h>
 #include <time.h>
 
+#include <atomic>
 #include <mutex>
 #include <shared_mutex>
 #include <vector>
 
-#include "cgck_internal.h"
+#include "cgck_host.h"
 
 using namespace cgck;
 
@@ -30,7 +32,7 @@ using namespace cgck;
 
 static thread_local char t_err[256];
 
-static int set_err(int code, const char *fmt, ...)
+int cgck::set_err(int code, const char *fmt, ...)
 {
 	va_list ap;
 	va_start(ap, fmt);
@@ -39,12 +41,7 @@ static int set_err(int code, const char *fmt, ...)
 	return code;
 }
 
-#define HIP_TRY(expr)                                                                     \
-	do {                                                                              \
-		hipError_t e_ = (expr);                                                   \
-		if (e_ != hipSuccess)                                                     \
-			return set_err(-EIO, "%s: %s", #expr, hipGetErrorString(e_));     \
-	} while (0)
+const char *cgck::err_text() { return t_err; }
 
 extern "C" const char *cgck_last_error(void) { return t_err; }
 extern "C" int cgck_abi_version(void) { return CGCK_ABI_VERSION; }
@@ -53,52 +50,13 @@ extern "C" int cgck_abi_version(void) { return CGCK_ABI_VERSION; }
 // Context
 // --------------------------------------------------------------------------
 
-struct cgck_ctx {
-	int device;
-	int num_cus;
-	hipStream_t stream;
-	uint32_t desc_len_hint;
-	int family; // kernel family: 0 auto, 1 group, 2 lane-per-packet ($CGCK_KERNEL)
-	// pinned host staging (drop-in calls, deferred TX)
-	uint8_t *h_stage;
-	size_t h_stage_cap;
-	uint32_t *h_out;
-	size_t h_out_cap;
-	// device scratch (host-resident batches)
-	uint8_t *d_bytes;
-	size_t d_bytes_cap;
-	uint8_t *d_aux; // descriptors | out | verdict
-	size_t d_aux_cap;
-	void *d_zero; // kZeroBytes zero bytes (KParams.zero)
-	// Toeplitz byte tables of the last key used (cgck_rss.hip)
-	uint32_t *d_rss_tab;
-	size_t d_rss_tab_cap;
-	uint32_t *h_rss_tab; // host copy (malloc)
-	size_t h_rss_tab_cap;
-	uint8_t *rss_key; // the key the tables were built from (malloc)
-	int rss_key_len;
-	uint32_t rss_cnt;
-	bool rss_valid;
-	hipStream_t rss_stream; // stream of the last launch that read d_rss_tab
-	// dst-cache scratch: control words + look-back status (zeroed per launch)
-	uint8_t *d_dst;
-	size_t d_dst_cap;
-	// burst server (cgck_burst_open): mailbox and staging, host-coherent pinned
-	BurstBox *bbox;      // nullptr: closed
-	uint8_t *bstage;     // [packets | descriptors | out | verdict]
-	size_t bstage_cap;
-	uint8_t *bstage_dev; // device view of bstage
-	BurstBox *bbox_dev;  // device view of bbox
-	uint32_t bmax;       // packets per request
-	uint32_t bseq;
-	hipStream_t bstream; // the server's own stream (it stays resident)
-};
+static void rss_users_free(cgck_ctx *c);
 
 struct cgck_event {
 	hipEvent_t ev;
 };
 
-static int grow_host(void **p, size_t *cap, size_t need)
+int cgck::grow_host(void **p, size_t *cap, size_t need)
 {
 	if (need <= *cap)
 		return 0;
@@ -112,7 +70,7 @@ static int grow_host(void **p, size_t *cap, size_t need)
 	return 0;
 }
 
-static int grow_dev(void **p, size_t *cap, size_t need)
+int cgck::grow_dev(void **p, size_t *cap, size_t need)
 {
 	if (need <= *cap)
 		return 0;
@@ -155,6 +113,7 @@ extern "C" int cgck_ctx_create(int device, cgck_ctx_t **out)
 		return set_err(-ENOMEM, "cgck_ctx_create: out of memory");
 	c->device = device;
 	c->num_cus = prop.multiProcessorCount;
+	c->last_kernel = "";
 	c->desc_len_hint = 1500;
 	if (const char *kf = getenv("CGCK_KERNEL"))
 		c->family = !strcmp(kf, "group") ? 1 : !strcmp(kf, "lpp") ? 2 : !strcmp(kf, "slot") ? 3
@@ -198,6 +157,7 @@ extern "C" int cgck_ctx_destroy(cgck_ctx_t *c)
 		(void)hipFree(c->d_rss_tab);
 	if (c->d_dst)
 		(void)hipFree(c->d_dst);
+	rss_users_free(c);
 	free(c->h_rss_tab);
 	free(c->rss_key);
 	free(c);
@@ -205,6 +165,8 @@ extern "C" int cgck_ctx_destroy(cgck_ctx_t *c)
 }
 
 extern "C" void *cgck_ctx_stream(cgck_ctx_t *c) { return c ? (void *)c->stream : nullptr; }
+
+extern "C" const char *cgck_ctx_last_kernel(cgck_ctx_t *c) { return c && c->last_kernel ? c->last_kernel : ""; }
 
 extern "C" int cgck_ctx_sync(cgck_ctx_t *c)
 {
@@ -244,14 +206,16 @@ static int check_flags(uint32_t flags)
 	return 0;
 }
 
-static int run(cgck_ctx *c, const KParams &p0, uint32_t max_len, hipStream_t st)
+int cgck::run(cgck_ctx *c, const KParams &p0, uint32_t len_hint, hipStream_t st)
 {
 	HIP_TRY(hipSetDevice(c->device));
 	KParams p = p0;
 	p.zero = c->d_zero;
-	hipError_t e = launch_cksum(p, max_len, c->num_cus, c->family, st);
+	hipError_t e = launch_cksum(p, len_hint, c->num_cus, c->family, st);
 	if (e != hipSuccess)
 		return set_err(-EIO, "cksum launch: %s", hipGetErrorString(e));
+	if (p.n)
+		c->last_kernel = t_kernel;
 	return 0;
 }
 
@@ -419,14 +383,9 @@ static void *registered_ptr(void *p, size_t bytes)
 	return a.devicePointer;
 }
 
-extern "C" int cgck_desc_host(cgck_ctx_t *c, void *base, size_t bytes, const cgck_desc_t *desc,
-			      uint64_t n, uint32_t flags, uint32_t *out, uint8_t *verdict)
+int cgck::desc_host(cgck_ctx *c, void *base, size_t bytes, const cgck_desc_t *desc, uint64_t n, uint32_t flags,
+		    uint32_t *out, uint8_t *verdict)
 {
-	if (!c)
-		return set_err(-EINVAL, "cgck_desc_host: NULL context");
-	int rc = check_flags(flags);
-	if (rc)
-		return rc;
 	if (n == 0)
 		return 0;
 	if (!base || !desc)
@@ -441,9 +400,12 @@ extern "C" int cgck_desc_host(cgck_ctx_t *c, void *base, size_t bytes, const cgc
 				       (unsigned long long)i, bytes);
 		pkt_bytes += ((size_t)desc[i].ip_len + 15) & ~(size_t)15;
 	}
+	// the internal group-only flags pick the group shape from the batch itself
+	const uint32_t hint = (flags & (kFlagL4Auto | kFlagNoLenCheck)) ? max_len : c->desc_len_hint;
 	HIP_TRY(hipSetDevice(c->device));
 	hipStream_t st = c->stream;
 	void *dev_base = registered_ptr(base, bytes);
+	int rc;
 	if (burst_fits(c, n, dev_base ? 0 : pkt_bytes, pkt_bytes)) {
 		// the resident server: same staging layout, no launch, no stream sync
 		const BurstLayout L = burst_layout(dev_base ? 0 : pkt_bytes, n);
@@ -496,7 +458,7 @@ extern "C" int cgck_desc_host(cgck_ctx_t *c, void *base, size_t bytes, const cgc
 		uint32_t *o = (uint32_t *)(h + o_off);
 		uint8_t *v = h + v_off;
 		KParams p = {dev_base ? (const uint8_t *)dev_base : h, d, n, 0, 0, 0, flags, o, v, nullptr, 0, nullptr};
-		if ((rc = run(c, p, c->desc_len_hint, st)))
+		if ((rc = run(c, p, hint, st)))
 			return rc;
 		HIP_TRY(hipStreamSynchronize(st));
 		if (out)
@@ -509,6 +471,7 @@ extern "C" int cgck_desc_host(cgck_ctx_t *c, void *base, size_t bytes, const cgc
 				       desc[i].ip_len);
 		return 0;
 	}
+	// a large pageable batch: DMA of [base, base + bytes) into device scratch
 	const size_t dbytes = 12 * n, obytes = 4 * n, vbytes = n;
 	if ((rc = grow_dev((void **)&c->d_bytes, &c->d_bytes_cap, bytes)))
 		return rc;
@@ -520,29 +483,73 @@ extern "C" int cgck_desc_host(cgck_ctx_t *c, void *base, size_t bytes, const cgc
 	HIP_TRY(hipMemcpyAsync(c->d_bytes, base, bytes, hipMemcpyHostToDevice, st));
 	HIP_TRY(hipMemcpyAsync(d_desc, desc, dbytes, hipMemcpyHostToDevice, st));
 	KParams p = {c->d_bytes, (const cgck_desc_t *)d_desc, n, 0, 0, 0, flags, d_out, d_ver, nullptr, 0, nullptr};
-	if ((rc = run(c, p, c->desc_len_hint, st)))
+	if ((rc = run(c, p, hint, st)))
 		return rc;
 	if (out)
 		HIP_TRY(hipMemcpyAsync(out, d_out, obytes, hipMemcpyDeviceToHost, st));
 	if (verdict)
 		HIP_TRY(hipMemcpyAsync(verdict, d_ver, vbytes, hipMemcpyDeviceToHost, st));
-	if (flags & CGCK_STORE)
-		HIP_TRY(hipMemcpyAsync(base, c->d_bytes, bytes, hipMemcpyDeviceToHost, st));
+	uint8_t *back = nullptr;
+	if (flags & CGCK_STORE) {
+		// Only the packets' own spans go back: every other byte of [base,
+		// base + bytes) may have changed since the H2D snapshot (the NIC or
+		// the caller writing other slots of the ring).
+		if ((rc = grow_host((void **)&c->h_stage, &c->h_stage_cap, bytes)))
+			return rc;
+		back = c->h_stage;
+		HIP_TRY(hipMemcpyAsync(back, c->d_bytes, bytes, hipMemcpyDeviceToHost, st));
+	}
 	HIP_TRY(hipStreamSynchronize(st));
+	if (back)
+		for (uint64_t i = 0; i < n; i++) {
+			const size_t o = desc[i].frame_off + desc[i].l3_off;
+			memcpy((uint8_t *)base + o, back + o, desc[i].ip_len);
+		}
 	return 0;
 }
 
-// Ranges registered through cgck_host_register, so the deferred TX flush can
-// read queued packets where they lie.  Written only by register/unregister
-// (set-up time); each flush takes the reader side once.
+extern "C" int cgck_desc_host(cgck_ctx_t *c, void *base, size_t bytes, const cgck_desc_t *desc,
+			      uint64_t n, uint32_t flags, uint32_t *out, uint8_t *verdict)
+{
+	if (!c)
+		return set_err(-EINVAL, "cgck_desc_host: NULL context");
+	int rc = check_flags(flags);
+	if (rc)
+		return rc;
+	return desc_host(c, base, bytes, desc, n, flags, out, verdict);
+}
+
+// Ranges registered through cgck_host_register, so the deferred TX window
+// can tell ring memory from a caller's stack or heap, and its flush read the
+// queued packets where they lie.  Written only by register/unregister
+// (set-up time); lookups take the reader side.
 namespace {
-struct RegRange {
-	uint8_t *lo, *hi;
-	uint8_t *dev; // device pointer of lo
-};
 std::shared_mutex g_reg_mu;
 std::vector<RegRange> g_reg;
+std::atomic<uint64_t> g_reg_gen{1}; // bumped by every register / unregister
+// per thread: the range of the last hit, valid while the generation holds
+thread_local uint64_t t_reg_gen = 0;
+thread_local RegRange t_reg_last{nullptr, nullptr, nullptr};
 } // namespace
+
+bool cgck::reg_find(const void *p, size_t bytes, RegRange *r)
+{
+	const uint8_t *b = (const uint8_t *)p;
+	if (t_reg_gen == g_reg_gen.load(std::memory_order_acquire) && b >= t_reg_last.lo && b < t_reg_last.hi &&
+	    bytes <= (size_t)(t_reg_last.hi - b)) {
+		*r = t_reg_last; // the TX window's per-call check: no lock on the hot path
+		return true;
+	}
+	std::shared_lock<std::shared_mutex> lk(g_reg_mu);
+	for (const RegRange &x : g_reg)
+		if (b >= x.lo && b < x.hi && bytes <= (size_t)(x.hi - b)) {
+			*r = x;
+			t_reg_last = x;
+			t_reg_gen = g_reg_gen.load(std::memory_order_acquire);
+			return true;
+		}
+	return false;
+}
 
 extern "C" int cgck_host_register(void *ptr, size_t bytes)
 {
@@ -554,6 +561,7 @@ extern "C" int cgck_host_register(void *ptr, size_t bytes)
 	}
 	std::unique_lock<std::shared_mutex> lk(g_reg_mu);
 	g_reg.push_back({(uint8_t *)ptr, (uint8_t *)ptr + bytes, (uint8_t *)dev});
+	g_reg_gen.fetch_add(1, std::memory_order_acq_rel);
 	return 0;
 }
 
@@ -566,55 +574,21 @@ extern "C" int cgck_host_unregister(void *ptr)
 				g_reg.erase(g_reg.begin() + i);
 				break;
 			}
+		g_reg_gen.fetch_add(1, std::memory_order_acq_rel);
 	}
 	HIP_TRY(hipHostUnregister(ptr));
 	return 0;
 }
 
 // --------------------------------------------------------------------------
-// Drop-in symbols (subr.h:373-374) and the deferred TX window
+// One region for the drop-in symbols (cgck_dropin.cpp): staged into pinned
+// memory that the kernel reads over the fabric (or served by the resident
+// burst server when one is open)
 // --------------------------------------------------------------------------
 
-namespace {
-
-struct TxEntry {
-	uint8_t *ip; // IPv4 header in caller (ring) memory
-	uint32_t span; // bytes staged
-	uint16_t hl;
-	int16_t fo; // -1: IP header entry (field ip+10); else L4 field offset after the header
-};
-
-struct ThreadState {
-	cgck_ctx *ctx = nullptr;
-	bool tx_open = false;
-	std::vector<TxEntry> txq;
-};
-
-thread_local ThreadState t_state;
-
-[[noreturn]] void die(const char *what)
+int cgck::one_region(cgck_ctx *c, const void *src, uint32_t span, uint32_t ip_len, uint32_t flags, uint32_t *out)
 {
-	fprintf(stderr, "libcgck: %s: %s\n", what, t_err);
-	abort();
-}
-
-cgck_ctx *tls_ctx()
-{
-	if (!t_state.ctx) {
-		const char *e = getenv("CGCK_DEVICE");
-		int dev = e ? atoi(e) : 0;
-		if (cgck_ctx_create(dev, &t_state.ctx) != 0)
-			die("no gfx950 context for the drop-in checksum");
-	}
-	return t_state.ctx;
-}
-
-// One region through the kernel: stage `span` bytes from `src` into pinned
-// memory (the kernel reads pinned host memory directly over the fabric),
-// launch, wait, return the u32 result.
-uint32_t one_packet(const void *src, uint32_t span, uint32_t ip_len, uint32_t flags)
-{
-	cgck_ctx *c = tls_ctx();
+	int rc;
 	if (ip_len <= 0xffff && burst_fits(c, 1, span, span)) {
 		// the resident server: one descriptor, no launch, no stream sync
 		const BurstLayout L = burst_layout(span, 1);
@@ -624,31 +598,28 @@ uint32_t one_packet(const void *src, uint32_t span, uint32_t ip_len, uint32_t fl
 		d->frame_off = 0;
 		d->l3_off = 0;
 		d->ip_len = (uint16_t)ip_len;
-		if (burst_serve(c, nullptr, 1, flags, ip_len, L) != 0)
-			die("burst server");
-		return *(const uint32_t *)(c->bstage + L.o_off);
+		if ((rc = burst_serve(c, nullptr, 1, flags, ip_len, L)))
+			return rc;
+		*out = *(const uint32_t *)(c->bstage + L.o_off);
+		return 0;
 	}
-	if (grow_host((void **)&c->h_stage, &c->h_stage_cap, span + 16) ||
-	    grow_host((void **)&c->h_out, &c->h_out_cap, 64))
-		die("staging allocation");
+	if ((rc = grow_host((void **)&c->h_stage, &c->h_stage_cap, span + 16)) ||
+	    (rc = grow_host((void **)&c->h_out, &c->h_out_cap, 64)))
+		return rc;
 	if (span)
 		memcpy(c->h_stage, src, span);
 	KParams p = {c->h_stage, nullptr, 1, 0, 0, ip_len, flags, c->h_out, nullptr, nullptr, 0, nullptr};
-	if (run(c, p, ip_len, c->stream) != 0)
-		die("kernel launch");
-	if (hipStreamSynchronize(c->stream) != hipSuccess) {
-		set_err(-EIO, "hipStreamSynchronize failed");
-		die("kernel completion");
-	}
-	return c->h_out[0];
+	if ((rc = run(c, p, ip_len, c->stream)))
+		return rc;
+	HIP_TRY(hipStreamSynchronize(c->stream));
+	*out = c->h_out[0];
+	return 0;
 }
-
-} // namespace
 
 extern "C" int cgck_burst_open(cgck_ctx_t *c, uint32_t max_pkts, size_t max_bytes, uint32_t idle_ms)
 {
-	if (!c)
-		c = tls_ctx();
+	if (!c && !(c = thread_ctx()))
+		return -ENODEV; // thread_ctx set the message
 	if (c->bbox)
 		return set_err(-EBUSY, "cgck_burst_open: already open on this context");
 	if (max_pkts == 0 || max_bytes == 0)
@@ -687,7 +658,7 @@ extern "C" int cgck_burst_open(cgck_ctx_t *c, uint32_t max_pkts, size_t max_byte
 extern "C" int cgck_burst_close(cgck_ctx_t *c)
 {
 	if (!c)
-		c = t_state.ctx; // this thread's drop-in context, if it exists
+		c = thread_ctx_if_any(); // this thread's drop-in context, if it exists
 	if (!c || !c->bbox)
 		return 0;
 	(void)hipSetDevice(c->device);
@@ -705,146 +676,9 @@ extern "C" int cgck_burst_close(cgck_ctx_t *c)
 }
 
 
-extern "C" uint16_t in_cksum(void *data, int len)
-{
-	if (len < 0) {
-		// The reference's cksum_raw never terminates sensibly on a negative
-		// size (subr.c:164 compares it as size_t); refuse loudly instead.
-		set_err(-EINVAL, "in_cksum: negative length %d", len);
-		die("in_cksum");
-	}
-	const uint8_t *b = (const uint8_t *)data;
-	if (t_state.tx_open && len >= 20 && (b[0] >> 4) == 4 && len == (b[0] & 15) * 4) {
-		t_state.txq.push_back({(uint8_t *)data, (uint32_t)len, (uint16_t)len, -1});
-		return 0;
-	}
-	return (uint16_t)one_packet(data, (uint32_t)len, (uint32_t)len, CGCK_RAW);
-}
-
-extern "C" uint16_t udp_cksum(struct ip *ipp, int len)
-{
-	const uint8_t *ip = (const uint8_t *)ipp;
-	if (len < 0) {
-		set_err(-EINVAL, "udp_cksum: negative length %d", len);
-		die("udp_cksum");
-	}
-	const uint32_t hl = (ip[0] & 15) * 4;
-	const uint32_t ip_len = hl + (uint32_t)len;
-	if (t_state.tx_open && hl >= 20 && ip_len <= 0xffff && (ip[9] == 6 || ip[9] == 17)) {
-		const int fo = ip[9] == 6 ? 16 : 6;
-		if ((uint32_t)len >= (uint32_t)fo + 2) {
-			t_state.txq.push_back({(uint8_t *)ip, ip_len, (uint16_t)hl, (int16_t)fo});
-			return 0;
-		}
-	}
-	// The pseudo-header reads ip+9 and ip+12..19 whatever ip_hl says
-	// (subr.c:205-207), so at least 20 bytes are staged.
-	const uint32_t span = ip_len < 20 ? 20 : ip_len;
-	return (uint16_t)(one_packet(ip, span, ip_len, CGCK_L4 | kFlagNoLenCheck) >> 16);
-}
-
-extern "C" int cgck_thread_release(void)
-{
-	t_state.txq.clear();
-	t_state.tx_open = false;
-	if (t_state.ctx) {
-		cgck_ctx_destroy(t_state.ctx);
-		t_state.ctx = nullptr;
-	}
-	return 0;
-}
-
-extern "C" int cgck_tx_begin(void)
-{
-	if (t_state.tx_open)
-		return set_err(-EBUSY, "cgck_tx_begin: window already open on this thread");
-	t_state.tx_open = true;
-	t_state.txq.clear();
-	return 0;
-}
-
-extern "C" int cgck_tx_flush(void)
-{
-	if (!t_state.tx_open)
-		return set_err(-EINVAL, "cgck_tx_flush: no open window on this thread");
-	t_state.tx_open = false;
-	std::vector<TxEntry> q;
-	q.swap(t_state.txq);
-	const uint64_t n = q.size();
-	if (n == 0)
-		return 0;
-	cgck_ctx *c = tls_ctx();
-	HIP_TRY(hipSetDevice(c->device));
-	// Packets inside one registered range (the transport's pool, rank 3) are
-	// read where they lie; otherwise every region is staged 16-byte aligned
-	// in pinned memory.  Descriptors and outputs follow.
-	RegRange reg{nullptr, nullptr, nullptr};
-	{
-		std::shared_lock<std::shared_mutex> lk(g_reg_mu);
-		for (const RegRange &r : g_reg)
-			if (q[0].ip >= r.lo && q[0].ip < r.hi) {
-				reg = r;
-				break;
-			}
-	}
-	for (uint64_t i = 0; reg.lo && i < n; i++)
-		if (q[i].ip < reg.lo || q[i].ip + q[i].span > reg.hi)
-			reg.lo = nullptr;
-	size_t bytes = 0; // staged bytes
-	if (!reg.lo)
-		for (const TxEntry &e : q)
-			bytes += (e.span + 15) & ~(size_t)15;
-	// (the burst server measured slower on TX flushes: they keep the launch)
-	const BurstLayout L = burst_layout(bytes, n);
-	int rc;
-	if ((rc = grow_host((void **)&c->h_stage, &c->h_stage_cap, L.v_off)))
-		return rc;
-	uint8_t *h = c->h_stage;
-	cgck_desc_t *d = (cgck_desc_t *)(h + L.d_off);
-	uint32_t *o = (uint32_t *)(h + L.o_off);
-	size_t at = 0;
-	for (uint64_t i = 0; i < n; i++) {
-		if (reg.lo) {
-			d[i].frame_off = (uint64_t)(q[i].ip - reg.lo);
-		} else {
-			memcpy(h + at, q[i].ip, q[i].span);
-			d[i].frame_off = at;
-			at += (q[i].span + 15) & ~(size_t)15;
-		}
-		d[i].l3_off = 0;
-		d[i].ip_len = (uint16_t)q[i].span;
-	}
-	// Both kinds in one launch: IP entries ask for the header checksum, L4
-	// entries for the segment checksum; both read their fields as zero, as
-	// the reference's callers have just stored them (ip_output.c:61,
-	// tcp_subr.c:75 / gbtcp/tcp.c:426,436).
-	KParams p = {reg.lo ? reg.dev : c->h_stage, d, n, 0, 0, 0, CGCK_IP | CGCK_L4 | CGCK_ZERO_FIELDS, o, nullptr,
-		     nullptr, 0, nullptr};
-	if ((rc = run(c, p, 1500, c->stream)))
-		return rc;
-	HIP_TRY(hipStreamSynchronize(c->stream));
-	int written = 0;
-	for (uint64_t i = 0; i < n; i++) {
-		uint16_t v;
-		uint8_t *dst;
-		if (q[i].fo < 0) {
-			v = (uint16_t)o[i];
-			dst = q[i].ip + 10;
-		} else {
-			v = (uint16_t)(o[i] >> 16);
-			dst = q[i].ip + q[i].hl + q[i].fo;
-		}
-		memcpy(dst, &v, 2);
-		written++;
-	}
-	return written;
-}
-
 // --------------------------------------------------------------------------
 // Toeplitz RSS hash and the dst-cache build
 // --------------------------------------------------------------------------
-
-static constexpr uint32_t kRssMaxCnt = 65536;
 
 // Byte tables of a key: T[i][v] = XOR of W(8i+b) over the set bits b of v
 // (MSB first), where W(p) is the 32-bit window of the key bit stream at bit
@@ -872,17 +706,65 @@ static void rss_tables(const uint8_t *key, int key_size, uint32_t cnt, uint32_t 
 	}
 }
 
+// Streams that launched kernels reading d_rss_tab, each with an event
+// recorded after its last such launch: a key change waits for all of them
+// before the tables are rewritten (a caller may hash on several streams).
+namespace {
+struct RssUsers {
+	std::vector<std::pair<hipStream_t, hipEvent_t>> ev;
+};
+} // namespace
+
+int cgck::rss_note_use(cgck_ctx *c, hipStream_t st)
+{
+	if (!c->rss_users)
+		c->rss_users = new RssUsers;
+	RssUsers *u = (RssUsers *)c->rss_users;
+	hipEvent_t e = nullptr;
+	for (auto &x : u->ev)
+		if (x.first == st)
+			e = x.second;
+	if (!e) {
+		HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+		u->ev.push_back({st, e});
+	}
+	HIP_TRY(hipEventRecord(e, st));
+	return 0;
+}
+
+static int rss_wait_users(cgck_ctx *c)
+{
+	RssUsers *u = (RssUsers *)c->rss_users;
+	if (!u)
+		return 0;
+	for (auto &x : u->ev)
+		HIP_TRY(hipEventSynchronize(x.second));
+	return 0;
+}
+
+static void rss_users_free(cgck_ctx *c)
+{
+	RssUsers *u = (RssUsers *)c->rss_users;
+	if (!u)
+		return;
+	for (auto &x : u->ev)
+		(void)hipEventDestroy(x.second);
+	delete u;
+	c->rss_users = nullptr;
+}
+
 // Make d_rss_tab hold the tables of (key, key_size) for `cnt` bytes.  A key
-// change waits for the last launch that read the old tables.
-static int rss_prepare(cgck_ctx *c, const uint8_t *key, int key_size, uint32_t cnt, hipStream_t st)
+// change first waits for every launch that read the old tables, on any stream.
+int cgck::rss_prepare(cgck_ctx *c, const uint8_t *key, int key_size, uint32_t cnt, hipStream_t st)
 {
 	const int klen = key_size > 4 ? key_size : 4;
 	if (c->rss_valid && c->rss_key_len == klen && c->rss_cnt >= cnt && !memcmp(c->rss_key, key, klen))
 		return 0;
 	const uint32_t tcnt = cnt < 12 ? 12 : cnt; // rss_hash4's 12 bytes are always there
 	const size_t tbytes = (size_t)tcnt * 256 * 4;
-	if (c->rss_valid && c->rss_stream)
-		HIP_TRY(hipStreamSynchronize(c->rss_stream));
+	int rc;
+	if (c->rss_valid && (rc = rss_wait_users(c)))
+		return rc;
 	c->rss_valid = false;
 	if (tbytes > c->h_rss_tab_cap) {
 		free(c->h_rss_tab);
@@ -891,7 +773,6 @@ static int rss_prepare(cgck_ctx *c, const uint8_t *key, int key_size, uint32_t c
 		if (!c->h_rss_tab)
 			return set_err(-ENOMEM, "rss tables: out of memory");
 	}
-	int rc;
 	if ((rc = grow_dev((void **)&c->d_rss_tab, &c->d_rss_tab_cap, tbytes)))
 		return rc;
 	uint8_t *nk = (uint8_t *)realloc(c->rss_key, klen);
@@ -928,8 +809,8 @@ extern "C" int cgck_toeplitz(cgck_ctx_t *c, const void *data, uint64_t n, uint64
 		return rc;
 	RssParams p = {(const uint8_t *)data, n, stride, cnt, mask, c->d_rss_tab, out};
 	HIP_TRY(launch_toeplitz(p, c->num_cus, st));
-	c->rss_stream = st;
-	return 0;
+	c->last_kernel = t_kernel;
+	return rss_note_use(c, st);
 }
 
 extern "C" int cgck_dst_cache(cgck_ctx_t *c, const cgck_dst_params_t *prm, cgck_dst_entry_t *out, uint32_t cap,
@@ -988,9 +869,8 @@ extern "C" int cgck_dst_cache(cgck_ctx_t *c, const cgck_dst_params_t *prm, cgck_
 	p.status = (uint64_t *)(c->d_dst + 16);
 	HIP_TRY(hipMemsetAsync(c->d_dst, 0, sbytes, st));
 	HIP_TRY(launch_dst_cache(p, c->num_cus, st));
-	if (filter)
-		c->rss_stream = st;
-	return 0;
+	c->last_kernel = t_kernel;
+	return filter ? rss_note_use(c, st) : 0;
 }
 
 extern "C" int cgck_dst_cache_host(cgck_ctx_t *c, const cgck_dst_params_t *prm, cgck_dst_entry_t *out,
@@ -1023,56 +903,6 @@ extern "C" int cgck_dst_cache_host(cgck_ctx_t *c, const cgck_dst_params_t *prm, 
 		HIP_TRY(hipMemcpy(out, c->d_bytes, (size_t)got * sizeof(cgck_dst_entry_t), hipMemcpyDeviceToHost));
 	*count = got;
 	return 0;
-}
-
-namespace {
-
-// One toeplitz_hash on the calling thread's context: the data is staged in
-// pinned memory, which the kernel reads over the fabric.
-uint32_t one_toeplitz(const uint8_t *data, uint32_t cnt, const uint8_t *key, int key_size, uint32_t mask)
-{
-	cgck_ctx *c = tls_ctx();
-	if (grow_host((void **)&c->h_stage, &c->h_stage_cap, cnt + 16) ||
-	    grow_host((void **)&c->h_out, &c->h_out_cap, 64))
-		die("staging allocation");
-	if (cnt)
-		memcpy(c->h_stage, data, cnt);
-	if (hipSetDevice(c->device) != hipSuccess || rss_prepare(c, key, key_size, cnt, c->stream) != 0)
-		die("rss tables");
-	RssParams p = {c->h_stage, 1, 0, cnt, mask, c->d_rss_tab, c->h_out};
-	hipError_t e = launch_toeplitz(p, c->num_cus, c->stream);
-	if (e == hipSuccess)
-		e = hipStreamSynchronize(c->stream);
-	if (e != hipSuccess) {
-		set_err(-EIO, "toeplitz: %s", hipGetErrorString(e));
-		die("toeplitz kernel");
-	}
-	c->rss_stream = c->stream;
-	return c->h_out[0];
-}
-
-} // namespace
-
-extern "C" uint32_t toeplitz_hash(const unsigned char *data, int cnt, const unsigned char *key, int key_size)
-{
-	if (cnt > (int)kRssMaxCnt) {
-		set_err(-EINVAL, "toeplitz_hash: cnt %d above %u", cnt, kRssMaxCnt);
-		die("toeplitz_hash");
-	}
-	// cnt <= 0: the reference's loop does not run and returns 0 (subr.c:490).
-	return one_toeplitz(data, cnt > 0 ? (uint32_t)cnt : 0, key, key_size, 0xffffffffu);
-}
-
-extern "C" uint32_t rss_hash4(uint32_t laddr, uint32_t faddr, uint16_t lport, uint16_t fport, unsigned char *key,
-			      int key_size)
-{
-	// subr.c:513-521: faddr, laddr, fport, lport as stored (network order).
-	uint8_t d[12];
-	memcpy(d + 0, &faddr, 4);
-	memcpy(d + 4, &laddr, 4);
-	memcpy(d + 8, &fport, 2);
-	memcpy(d + 10, &lport, 2);
-	return one_toeplitz(d, 12, key, key_size, 0x7Fu); // subr.c:523
 }
 
 // --------------------------------------------------------------------------

@@ -107,9 +107,14 @@ __device__ __forceinline__ uint32_t finish(uint32_t f)
 	return r ? r : 0xffffu;
 }
 
+__device__ __forceinline__ bool l4_nopseudo(uint32_t proto, uint32_t flags)
+{
+	return (flags & CGCK_L4_NOPSEUDO) || ((flags & kFlagL4Auto) && proto == 1);
+}
+
 __device__ __forceinline__ int l4_field(uint32_t proto, uint32_t flags)
 {
-	if (flags & CGCK_L4_NOPSEUDO)
+	if (l4_nopseudo(proto, flags))
 		return proto == 1 ? 2 : -1;
 	return proto == 6 ? 16 : (proto == 17 ? 6 : -1);
 }

@@ -1,28 +1,62 @@
 // cgck_dispatch.cpp — picks the kernel family and launch shape for a batch.
+//
+// The product library (libcgck.so) carries only the families the dispatcher
+// picks by itself: group (>= 1 KiB typical length, drop-in and window calls),
+// lpa (aligned fixed-length 20..64-byte strided batches), lpp (small
+// unaligned or descriptor packets) and slot2 (mid-size / mixed lengths).  The
+// A/B-only variants measured against them (slot, lppp, the other lpp shapes,
+// the LDS-DMA stream kernels, the probe kernels) are compiled only into
+// libcgck_lab.so (-DCGCK_LAB, tools/Makefile) for tools/ab_inproc.py and
+// tools/sweep.py.
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <mutex>
+
 #include "cgck_internal.h"
 
 namespace cgck {
 
+thread_local const char *t_kernel = "";
+
+const char *intern(const char *fmt, ...)
+{
+	// called once per launch site (function-local static): the strings live
+	// for the process
+	static std::mutex mu;
+	char buf[128];
+	va_list ap;
+	va_start(ap, fmt);
+	vsnprintf(buf, sizeof(buf), fmt, ap);
+	va_end(ap);
+	std::lock_guard<std::mutex> lk(mu);
+	return strdup(buf);
+}
+
 hipError_t launch_group(const KParams &p, uint32_t max_len, int num_cus, bool nt, hipStream_t st);
 hipError_t launch_lpp(const KParams &p, int num_cus, bool nt, int shape, hipStream_t st);
-hipError_t launch_slot(const KParams &p, int num_cus, bool nt, hipStream_t st);
-hipError_t launch_lppp(const KParams &p, int num_cus, bool nt, hipStream_t st);
 hipError_t launch_slot2(const KParams &p, int num_cus, bool nt, hipStream_t st);
 hipError_t launch_lpa(const KParams &p, int num_cus, bool nt, hipStream_t st);
+#if CGCK_LAB
+hipError_t launch_slot(const KParams &p, int num_cus, bool nt, hipStream_t st);
+hipError_t launch_lppp(const KParams &p, int num_cus, bool nt, hipStream_t st);
 hipError_t launch_stream(const KParams &p, int num_cus, hipStream_t st);
 bool stream_ok(const KParams &p);
+#endif
 
 // `kernel` = variant | flags (include/cgck.h is agnostic of this; $CGCK_KERNEL
 // overrides it for A/B runs):
 //   variant (bits 0-3): 0 auto, 1 group (G lanes per packet), 2 lane per
-//     packet, 3 lane per 128-byte slot, 4 software-pipelined lane per packet,
-//     5..8 lane per packet shapes 1..3, 0 (6 clamped, 6 predicated,
-//     4 predicated, 4 clamped chunks up front), 9 lane per 128-byte slot
-//     pipelined two deep (the default for mid-size packets), 10 lane per
-//     packet for aligned fixed-length strided 20..64-byte packets, A/B
-//     pipelined (the default there), 11 the lane-group kernel fed by
-//     LDS-DMA (strided 20..1520-byte packets, no in-place writes; the
-//     default for the 1500 B config);
+//     packet (lpp), 9 lane per 128-byte slot pipelined two deep (slot2, the
+//     default for mid-size packets), 10 lane per packet for aligned
+//     fixed-length strided 20..64-byte packets, A/B pipelined (lpa, the
+//     default there).  libcgck_lab.so only: 3 lane per 128-byte slot, 4
+//     software-pipelined lane per packet, 5..8 lpp shapes 1..3, 0, 11 the
+//     lane-group kernel fed by LDS-DMA.  A variant this build lacks falls
+//     back to the automatic choice; one whose preconditions a batch fails
+//     falls back to lpp or group;
 //   kNT (bit 4) nontemporal loads, kContig (bit 5) contiguous block ranges,
 //   kExplicit (bit 6) take bits 4-5 as given instead of the measured defaults.
 // len_hint = the batch's packet length (strided) or typical length (descriptors).
@@ -31,22 +65,26 @@ hipError_t launch_cksum(const KParams &p0, uint32_t len_hint, int num_cus, int k
 	if (p0.n == 0)
 		return hipSuccess;
 	KParams p = p0;
-	const bool lane_ok = !(p.flags & kFlagNoLenCheck);
+	const bool lane_ok = !(p.flags & (kFlagNoLenCheck | kFlagL4Auto));
 	int variant = kernel & 15;
 	// aligned fixed-length strided batch of 20..64-byte packets (the 64 B config)
 	const bool lpa_ok = lane_ok && !p.desc && p.ip_len >= 20 && p.ip_len <= 64 &&
 			    ((reinterpret_cast<uintptr_t>(p.base) | p.stride | p.l3_off) & 15) == 0;
-	if (variant == 0) {
+#if CGCK_LAB
+	const bool known = variant <= 11;
+#else
+	const bool known = variant == 1 || variant == 2 || variant == 9 || variant == 10;
+#endif
+	if (variant == 0 || !known)
 		variant = !lane_ok ? 1 : lpa_ok ? 10 : len_hint >= kGroupFromLen ? 1 : len_hint <= kLppUpToLen ? 2 : 9;
-		if (variant == 1 && len_hint >= kGroupFromLen && kDefaultStream && stream_ok(p))
-			variant = 11;
-	}
 	if (variant >= 2 && !lane_ok)
 		variant = 1;
 	if (variant == 10 && !lpa_ok)
 		variant = 2;
+#if CGCK_LAB
 	if (variant == 11 && !stream_ok(p))
 		variant = 1;
+#endif
 	bool nt, contig;
 	if (kernel & kExplicit) {
 		nt = kernel & kNT;
@@ -62,8 +100,15 @@ hipError_t launch_cksum(const KParams &p0, uint32_t len_hint, int num_cus, int k
 	switch (variant) {
 	case 2:
 		return launch_lpp(p, num_cus, nt, kDefaultLppShape, st);
+	case 9:
+		return launch_slot2(p, num_cus, nt, st);
+	case 10:
+		return launch_lpa(p, num_cus, nt, st);
+#if CGCK_LAB
 	case 3:
 		return launch_slot(p, num_cus, nt, st);
+	case 4:
+		return launch_lppp(p, num_cus, nt, st);
 	case 5:
 		return launch_lpp(p, num_cus, nt, 1, st);
 	case 6:
@@ -72,14 +117,9 @@ hipError_t launch_cksum(const KParams &p0, uint32_t len_hint, int num_cus, int k
 		return launch_lpp(p, num_cus, nt, 3, st);
 	case 8:
 		return launch_lpp(p, num_cus, nt, 0, st);
-	case 4:
-		return launch_lppp(p, num_cus, nt, st);
-	case 9:
-		return launch_slot2(p, num_cus, nt, st);
-	case 10:
-		return launch_lpa(p, num_cus, nt, st);
 	case 11:
 		return launch_stream(p, num_cus, st);
+#endif
 	default:
 		return launch_group(p, len_hint, num_cus, nt, st);
 	}

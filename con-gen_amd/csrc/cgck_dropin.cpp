@@ -1,0 +1,569 @@
+// cgck_dropin.cpp — the drop-in symbols of subr.h:370-374 (in_cksum,
+// udp_cksum, toeplitz_hash, rss_hash4) and the two per-thread windows that
+// let the stack's own call sites batch without being edited:
+//
+//  * the RX window (cgck_rx_begin .. cgck_rx_end): at the transport's receive
+//    burst one launch computes every frame's header and L4 checksum with the
+//    checksum fields read as zero; the stack's verifiers (ip_input.c:45-58,
+//    tcp_input.c:75-85, udp_usrreq.c:86-94, ip_icmp.c:187-193,
+//    gbtcp/inet.c:142-153 and 319-330) then call in_cksum / udp_cksum on the
+//    same header or segment, after zeroing the field themselves, and get the
+//    precomputed value back.  Their count / drop policy (t_*_do_incksum
+//    0/1/2) runs unchanged;
+//  * the TX window (cgck_tx_begin .. cgck_tx_flush): the finalisers'
+//    (ip_output.c:61-64, tcp_output.c:416-418, tcp_subr.c:122,
+//    gbtcp/tcp.c:370-379) calls on registered ring memory are queued and
+//    filled in one launch before the NIC kick.
+//
+// A call that neither window answers runs the kernel synchronously on the
+// thread's own context.  No value is ever computed on the host.
+#include <hip/hip_runtime.h>
+
+#include <errno.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <atomic>
+#include <vector>
+
+#include "cgck_host.h"
+
+using namespace cgck;
+
+namespace {
+
+// --------------------------------------------------------------------------
+// Error handler (cgck_set_error_handler)
+// --------------------------------------------------------------------------
+
+std::atomic<cgck_error_fn> g_err_fn{nullptr};
+std::atomic<void *> g_err_arg{nullptr};
+
+// Open-addressing map from a non-zero key (a pointer, or a pointer times two
+// plus a kind bit) to a u32; sized to twice the entries.
+struct PtrMap {
+	std::vector<uintptr_t> key;
+	std::vector<uint32_t> val;
+	size_t used = 0;
+
+	static size_t hash(uintptr_t k)
+	{
+		k ^= k >> 31;
+		k *= 0xbf58476d1ce4e5b9ull;
+		return (size_t)(k ^ (k >> 29));
+	}
+	void reset(size_t n)
+	{
+		size_t cap = 16;
+		while (cap < 2 * n)
+			cap <<= 1;
+		key.assign(cap, 0);
+		val.resize(cap);
+		used = 0;
+	}
+	void put(uintptr_t k, uint32_t v)
+	{
+		if (2 * (used + 1) > key.size()) {
+			std::vector<uintptr_t> ok;
+			std::vector<uint32_t> ov;
+			ok.swap(key);
+			ov.swap(val);
+			reset(used + 1 < 8 ? 8 : 2 * (used + 1));
+			for (size_t i = 0; i < ok.size(); i++)
+				if (ok[i])
+					put(ok[i], ov[i]);
+		}
+		const size_t m = key.size() - 1;
+		for (size_t i = hash(k) & m;; i = (i + 1) & m)
+			if (key[i] == 0 || key[i] == k) {
+				used += key[i] == 0;
+				key[i] = k;
+				val[i] = v;
+				return;
+			}
+	}
+	bool get(uintptr_t k, uint32_t *v) const
+	{
+		if (key.empty())
+			return false;
+		const size_t m = key.size() - 1;
+		for (size_t i = hash(k) & m;; i = (i + 1) & m) {
+			if (key[i] == k) {
+				*v = val[i];
+				return true;
+			}
+			if (key[i] == 0)
+				return false;
+		}
+	}
+};
+
+struct TxEntry {
+	uint8_t *ip;   // IPv4 header in registered (ring) memory
+	uint32_t span; // bytes from ip the checksum covers
+	uint16_t hl;
+	int16_t fo; // -1: IP header entry (field ip+10); else L4 field offset after the header
+};
+
+enum { kRxIp = 1, kRxL4 = 2 };
+
+struct RxEntry {
+	const uint8_t *ip;
+	uint32_t out;   // lo16 header checksum, hi16 L4 checksum (ICMP: no pseudo-header)
+	uint16_t hl;    // ip_hl * 4 at rx_begin
+	uint16_t l4len; // ntohs(ip_len) - hl: the length the stack passes (ip_input.c:63,98; inet.c:313)
+	uint8_t proto;
+	uint8_t ok; // kRxIp | kRxL4: which values are valid
+};
+
+struct ThreadState {
+	cgck_ctx *ctx = nullptr;
+	// TX window
+	bool tx_open = false;
+	std::vector<TxEntry> txq;
+	PtrMap txidx; // (ip << 1 | is_l4) -> txq index
+	// RX window
+	bool rx_open = false;
+	std::vector<RxEntry> rx;
+	size_t rx_cur = 0;    // the entry the last answered call matched
+	bool rx_map = false;  // rxidx built (on the first call off the cursor)
+	PtrMap rxidx; // ip -> entry << 1; ip + hl (ICMP message) -> entry << 1 | 1
+	std::vector<cgck_desc_t> rxd;
+	std::vector<uint32_t> rxo;
+	uint64_t rx_served0 = 0; // stats[0] at rx_begin
+	uint64_t stats[4] = {0, 0, 0, 0};
+};
+
+thread_local ThreadState t_state;
+
+uint32_t sync_region(const void *src, uint32_t span, uint32_t ip_len, uint32_t flags)
+{
+	cgck_ctx *c = thread_ctx();
+	if (!c)
+		die("no gfx950 context for the drop-in checksum");
+	uint32_t out = 0;
+	if (one_region(c, src, span, ip_len, flags, &out) != 0)
+		die("drop-in checksum kernel");
+	return out;
+}
+
+// The window entry a pointer names: (entry << 1) for an IPv4 header, (entry
+// << 1 | 1) for the ICMP message after it.  The stack walks a burst in slot
+// order and asks for each frame's header and then its segment, so the entry
+// of the previous answer or the one after it almost always matches; a map
+// of every entry is built only on the first call that matches neither.
+bool rx_find(ThreadState &t, const uint8_t *p, uint32_t *v)
+{
+	const size_t n = t.rx.size();
+	for (size_t i = t.rx_cur; i < t.rx_cur + 2 && i < n; i++) {
+		const RxEntry &e = t.rx[i];
+		if (e.ip == p) {
+			*v = (uint32_t)(i << 1);
+			t.rx_cur = i;
+			return true;
+		}
+		if (e.proto == 1 && e.ip + e.hl == p) {
+			*v = (uint32_t)(i << 1 | 1);
+			t.rx_cur = i;
+			return true;
+		}
+	}
+	if (!t.rx_map) {
+		t.rxidx.reset(2 * n);
+		for (size_t i = 0; i < n; i++) {
+			const RxEntry &e = t.rx[i];
+			t.rxidx.put((uintptr_t)e.ip, (uint32_t)(i << 1));
+			if (e.proto == 1 && (e.ok & kRxL4))
+				t.rxidx.put((uintptr_t)(e.ip + e.hl), (uint32_t)(i << 1 | 1));
+		}
+		t.rx_map = true;
+	}
+	if (!t.rxidx.get((uintptr_t)p, v))
+		return false;
+	t.rx_cur = *v >> 1;
+	return true;
+}
+
+void tx_queue(ThreadState &t, uint8_t *ip, uint32_t span, uint16_t hl, int16_t fo)
+{
+	const uintptr_t k = ((uintptr_t)ip << 1) | (fo >= 0 ? 1u : 0u);
+	uint32_t i;
+	if (t.txidx.get(k, &i)) { // the same header / segment again: the later call wins
+		t.txq[i] = {ip, span, hl, fo};
+		return;
+	}
+	t.txidx.put(k, (uint32_t)t.txq.size());
+	t.txq.push_back({ip, span, hl, fo});
+}
+
+} // namespace
+
+// --------------------------------------------------------------------------
+// Per-thread context and failure reporting
+// --------------------------------------------------------------------------
+
+cgck_ctx *cgck::thread_ctx()
+{
+	if (!t_state.ctx) {
+		const char *e = getenv("CGCK_DEVICE");
+		const int dev = e ? atoi(e) : 0;
+		cgck_ctx *c = nullptr;
+		if (cgck_ctx_create(dev, &c) != 0)
+			return nullptr;
+		t_state.ctx = c;
+	}
+	return t_state.ctx;
+}
+
+cgck_ctx *cgck::thread_ctx_if_any() { return t_state.ctx; }
+
+[[noreturn]] void cgck::die(const char *what)
+{
+	const cgck_error_fn fn = g_err_fn.load(std::memory_order_acquire);
+	void *arg = g_err_arg.load(std::memory_order_acquire);
+	if (fn)
+		fn(what, err_text(), arg);
+	fprintf(stderr, "libcgck: %s: %s\n", what, err_text());
+	abort();
+}
+
+extern "C" void cgck_set_error_handler(cgck_error_fn fn, void *arg)
+{
+	g_err_arg.store(arg, std::memory_order_release);
+	g_err_fn.store(fn, std::memory_order_release);
+}
+
+extern "C" cgck_ctx_t *cgck_thread_ctx(void) { return thread_ctx(); }
+
+extern "C" int cgck_thread_release(void)
+{
+	ThreadState &t = t_state;
+	t.txq.clear();
+	t.tx_open = false;
+	t.rx.clear();
+	t.rx_open = false;
+	if (t.ctx) {
+		cgck_ctx_destroy(t.ctx);
+		t.ctx = nullptr;
+	}
+	return 0;
+}
+
+extern "C" int cgck_window_stats(uint64_t stats[4])
+{
+	if (!stats)
+		return set_err(-EINVAL, "cgck_window_stats: NULL");
+	memcpy(stats, t_state.stats, sizeof(t_state.stats));
+	return 0;
+}
+
+// --------------------------------------------------------------------------
+// Drop-in symbols (subr.h:373-374; bodies subr.c:186-195, 212-223)
+// --------------------------------------------------------------------------
+
+extern "C" uint16_t in_cksum(void *data, int len)
+{
+	if (len < 0) {
+		// The reference's cksum_raw never terminates sensibly on a negative
+		// size (subr.c:164 compares it as size_t); refuse loudly instead.
+		set_err(-EINVAL, "in_cksum: negative length %d", len);
+		die("in_cksum");
+	}
+	ThreadState &t = t_state;
+	const uint8_t *b = (const uint8_t *)data;
+	if (t.rx_open) {
+		// ip_cksum(ip) at ip_input.c:51 / inet.c:322, or the ICMP message at
+		// ip_icmp.c:189, after the caller zeroed the field
+		uint32_t v;
+		if (rx_find(t, b, &v)) {
+			const RxEntry &e = t.rx[v >> 1];
+			if (!(v & 1) && (e.ok & kRxIp) && len == e.hl) {
+				t.stats[0]++;
+				return (uint16_t)e.out;
+			}
+			if ((v & 1) && (e.ok & kRxL4) && len == e.l4len) {
+				t.stats[0]++;
+				return (uint16_t)(e.out >> 16);
+			}
+		}
+		t.stats[1]++;
+	}
+	if (t.tx_open && len >= 20 && (b[0] >> 4) == 4 && len == (b[0] & 15) * 4) {
+		RegRange r;
+		if (reg_find(data, (size_t)len, &r)) {
+			tx_queue(t, (uint8_t *)data, (uint32_t)len, (uint16_t)len, -1);
+			t.stats[2]++;
+			return 0;
+		}
+		t.stats[3]++;
+	}
+	return (uint16_t)sync_region(data, (uint32_t)len, (uint32_t)len, CGCK_RAW);
+}
+
+extern "C" uint16_t udp_cksum(struct ip *ipp, int len)
+{
+	const uint8_t *ip = (const uint8_t *)ipp;
+	if (len < 0) {
+		set_err(-EINVAL, "udp_cksum: negative length %d", len);
+		die("udp_cksum");
+	}
+	ThreadState &t = t_state;
+	const uint32_t hl = (ip[0] & 15) * 4;
+	const uint32_t ip_len = hl + (uint32_t)len;
+	if (t.rx_open) {
+		// tcp_cksum(ip, ip->ip_len) at tcp_input.c:78 / inet.c:145, or
+		// udp_cksum(ip, len) at udp_usrreq.c:89
+		uint32_t v;
+		if (rx_find(t, ip, &v) && !(v & 1)) {
+			const RxEntry &e = t.rx[v >> 1];
+			if ((e.ok & kRxL4) && e.proto != 1 && (uint32_t)len == e.l4len && hl == e.hl) {
+				t.stats[0]++;
+				return (uint16_t)(e.out >> 16);
+			}
+		}
+		t.stats[1]++;
+	}
+	if (t.tx_open && hl >= 20 && ip_len <= 0xffff && (ip[9] == 6 || ip[9] == 17)) {
+		const int fo = ip[9] == 6 ? 16 : 6;
+		RegRange r;
+		if ((uint32_t)len >= (uint32_t)fo + 2) {
+			if (reg_find(ip, ip_len, &r)) {
+				tx_queue(t, (uint8_t *)ip, ip_len, (uint16_t)hl, (int16_t)fo);
+				t.stats[2]++;
+				return 0;
+			}
+			t.stats[3]++;
+		}
+	}
+	// The pseudo-header reads ip+9 and ip+12..19 whatever ip_hl says
+	// (subr.c:205-207), so at least 20 bytes are staged.
+	const uint32_t span = ip_len < 20 ? 20 : ip_len;
+	return (uint16_t)(sync_region(ip, span, ip_len, CGCK_L4 | kFlagNoLenCheck) >> 16);
+}
+
+// --------------------------------------------------------------------------
+// RX window
+// --------------------------------------------------------------------------
+
+extern "C" int cgck_rx_begin(void *base, size_t bytes, const cgck_desc_t *desc, uint64_t n)
+{
+	ThreadState &t = t_state;
+	if (t.rx_open)
+		return set_err(-EBUSY, "cgck_rx_begin: an RX window is already open on this thread");
+	if (n && (!base || !desc))
+		return set_err(-EINVAL, "cgck_rx_begin: NULL base or descriptors");
+	if (n > 0xffffffffull / 2)
+		return set_err(-EINVAL, "cgck_rx_begin: burst of %llu frames", (unsigned long long)n);
+	cgck_ctx *c = thread_ctx();
+	if (!c)
+		return -ENODEV; // thread_ctx set the message
+	t.rx.clear();
+	t.rxd.clear();
+	const uint8_t *b = (const uint8_t *)base;
+	for (uint64_t i = 0; i < n; i++) {
+		const uint64_t at = desc[i].frame_off + desc[i].l3_off;
+		if (at + desc[i].ip_len > bytes || at < desc[i].frame_off)
+			return set_err(-EINVAL, "cgck_rx_begin: descriptor %llu reaches past the %zu bytes given",
+				       (unsigned long long)i, bytes);
+		// Which calls the stack can make on this frame.  ip_input.c:28-44 and
+		// inet.c:282-306 drop before the header checksum unless 20 <= hl <=
+		// len; the L4 checksum runs only when the frame holds ntohs(ip_len)
+		// bytes (ip_input.c:76, inet.c:314) and the segment its header
+		// (tcp_input.c:67, udp_usrreq.c:65, ip_icmp.c:177).
+		const uint32_t avail = desc[i].ip_len;
+		if (avail < 20)
+			continue;
+		const uint8_t *ip = b + at;
+		const uint32_t hl = (ip[0] & 15) * 4;
+		if (hl < 20 || hl > avail)
+			continue;
+		const uint32_t total = (uint32_t)ip[2] << 8 | ip[3];
+		const uint8_t proto = ip[9];
+		uint32_t cover = total < avail ? total : avail; // bytes the kernel reads
+		if (cover < hl)
+			cover = hl;
+		uint8_t ok = kRxIp;
+		const uint32_t l4len = total >= hl ? total - hl : 0;
+		const uint32_t need = proto == 6 ? 18 : proto == 17 ? 8 : proto == 1 ? 4 : 0xffffffffu;
+		if (total >= hl && total <= avail && l4len >= need)
+			ok |= kRxL4;
+		t.rx.push_back({ip, 0, (uint16_t)hl, (uint16_t)l4len, proto, ok});
+		cgck_desc_t d;
+		d.frame_off = desc[i].frame_off;
+		d.l3_off = desc[i].l3_off;
+		d.ip_len = (uint16_t)cover;
+		t.rxd.push_back(d);
+	}
+	const uint64_t m = t.rx.size();
+	t.rxo.resize(m ? m : 1);
+	if (m) {
+		// header checksum + L4 checksum per frame, checksum fields read as
+		// zero; ICMP without the pseudo-header (kFlagL4Auto, group kernel)
+		const int rc = desc_host(c, base, bytes, t.rxd.data(), m,
+					 CGCK_IP | CGCK_L4 | CGCK_ZERO_FIELDS | kFlagL4Auto, t.rxo.data(), nullptr);
+		if (rc)
+			return rc;
+	}
+	for (uint64_t i = 0; i < m; i++)
+		t.rx[i].out = t.rxo[i];
+	t.rx_cur = 0;
+	t.rx_map = false;
+	t.rx_open = true;
+	t.rx_served0 = t.stats[0];
+	return (int)m;
+}
+
+extern "C" int cgck_rx_end(void)
+{
+	ThreadState &t = t_state;
+	if (!t.rx_open)
+		return set_err(-EINVAL, "cgck_rx_end: no open RX window on this thread");
+	t.rx_open = false;
+	t.rx.clear();
+	t.rx_map = false;
+	return (int)(t.stats[0] - t.rx_served0);
+}
+
+// --------------------------------------------------------------------------
+// TX window
+// --------------------------------------------------------------------------
+
+extern "C" int cgck_tx_begin(void)
+{
+	ThreadState &t = t_state;
+	if (t.tx_open)
+		return set_err(-EBUSY, "cgck_tx_begin: window already open on this thread");
+	t.tx_open = true;
+	t.txq.clear();
+	t.txidx.reset(256);
+	return 0;
+}
+
+extern "C" int cgck_tx_flush(void)
+{
+	ThreadState &t = t_state;
+	if (!t.tx_open)
+		return set_err(-EINVAL, "cgck_tx_flush: no open window on this thread");
+	t.tx_open = false;
+	std::vector<TxEntry> q;
+	q.swap(t.txq);
+	t.txidx.reset(0);
+	const uint64_t n = q.size();
+	if (n == 0)
+		return 0;
+	cgck_ctx *c = thread_ctx();
+	if (!c)
+		return -ENODEV;
+	HIP_TRY(hipSetDevice(c->device));
+	// Every entry lies in registered memory (the window queues nothing
+	// else).  When they all lie in one range (the transport's pool) the
+	// kernel reads them where they lie; otherwise each region is staged
+	// 16-byte aligned in pinned memory.  Descriptors and outputs follow.
+	RegRange reg{nullptr, nullptr, nullptr};
+	bool inplace = reg_find(q[0].ip, q[0].span, &reg);
+	for (uint64_t i = 1; inplace && i < n; i++)
+		inplace = q[i].ip >= reg.lo && q[i].ip + q[i].span <= reg.hi;
+	size_t bytes = 0; // staged bytes
+	if (!inplace)
+		for (const TxEntry &e : q)
+			bytes += (e.span + 15) & ~(size_t)15;
+	const size_t d_off = (bytes + 15) & ~(size_t)15;
+	const size_t o_off = (d_off + 12 * n + 15) & ~(size_t)15;
+	int rc;
+	if ((rc = grow_host((void **)&c->h_stage, &c->h_stage_cap, o_off + 4 * n)))
+		return rc;
+	uint8_t *h = c->h_stage;
+	cgck_desc_t *d = (cgck_desc_t *)(h + d_off);
+	uint32_t *o = (uint32_t *)(h + o_off);
+	size_t at = 0;
+	for (uint64_t i = 0; i < n; i++) {
+		if (inplace) {
+			d[i].frame_off = (uint64_t)(q[i].ip - reg.lo);
+		} else {
+			memcpy(h + at, q[i].ip, q[i].span);
+			d[i].frame_off = at;
+			at += (q[i].span + 15) & ~(size_t)15;
+		}
+		d[i].l3_off = 0;
+		d[i].ip_len = (uint16_t)q[i].span;
+	}
+	// Both kinds in one launch: IP entries ask for the header checksum, L4
+	// entries for the segment checksum; both read their fields as zero, as
+	// the reference's callers have just stored them (ip_output.c:61,
+	// tcp_subr.c:75 / gbtcp/tcp.c:426,436).  (The burst server measured
+	// slower on TX flushes: they keep the launch.)
+	KParams p = {inplace ? reg.dev : h, d, n, 0, 0, 0, CGCK_IP | CGCK_L4 | CGCK_ZERO_FIELDS, o, nullptr,
+		     nullptr, 0, nullptr};
+	if ((rc = run(c, p, 1500, c->stream)))
+		return rc;
+	HIP_TRY(hipStreamSynchronize(c->stream));
+	for (uint64_t i = 0; i < n; i++) {
+		uint16_t v;
+		uint8_t *dst;
+		if (q[i].fo < 0) {
+			v = (uint16_t)o[i];
+			dst = q[i].ip + 10;
+		} else {
+			v = (uint16_t)(o[i] >> 16);
+			dst = q[i].ip + q[i].hl + q[i].fo;
+		}
+		memcpy(dst, &v, 2);
+	}
+	return (int)n;
+}
+
+// --------------------------------------------------------------------------
+// Toeplitz drop-ins (subr.h:370-371; bodies subr.c:482-502, 506-530)
+// --------------------------------------------------------------------------
+
+namespace {
+
+// One toeplitz_hash on the calling thread's context: the data is staged in
+// pinned memory, which the kernel reads over the fabric.
+uint32_t one_toeplitz(const uint8_t *data, uint32_t cnt, const uint8_t *key, int key_size, uint32_t mask)
+{
+	cgck_ctx *c = thread_ctx();
+	if (!c)
+		die("no gfx950 context for the drop-in Toeplitz hash");
+	if (grow_host((void **)&c->h_stage, &c->h_stage_cap, cnt + 16) ||
+	    grow_host((void **)&c->h_out, &c->h_out_cap, 64))
+		die("staging allocation");
+	if (cnt)
+		memcpy(c->h_stage, data, cnt);
+	if (hipSetDevice(c->device) != hipSuccess || rss_prepare(c, key, key_size, cnt, c->stream) != 0)
+		die("rss tables");
+	RssParams p = {c->h_stage, 1, 0, cnt, mask, c->d_rss_tab, c->h_out};
+	hipError_t e = launch_toeplitz(p, c->num_cus, c->stream);
+	if (e == hipSuccess)
+		e = hipStreamSynchronize(c->stream);
+	if (e != hipSuccess) {
+		set_err(-EIO, "toeplitz: %s", hipGetErrorString(e));
+		die("toeplitz kernel");
+	}
+	return c->h_out[0];
+}
+
+} // namespace
+
+extern "C" uint32_t toeplitz_hash(const unsigned char *data, int cnt, const unsigned char *key, int key_size)
+{
+	if (cnt > (int)kRssMaxCnt) {
+		set_err(-EINVAL, "toeplitz_hash: cnt %d above %u", cnt, kRssMaxCnt);
+		die("toeplitz_hash");
+	}
+	// cnt <= 0: the reference's loop does not run and returns 0 (subr.c:490).
+	return one_toeplitz(data, cnt > 0 ? (uint32_t)cnt : 0, key, key_size, 0xffffffffu);
+}
+
+extern "C" uint32_t rss_hash4(uint32_t laddr, uint32_t faddr, uint16_t lport, uint16_t fport, unsigned char *key,
+			      int key_size)
+{
+	// subr.c:513-521: faddr, laddr, fport, lport as stored (network order).
+	uint8_t d[12];
+	memcpy(d + 0, &faddr, 4);
+	memcpy(d + 4, &laddr, 4);
+	memcpy(d + 8, &fport, 2);
+	memcpy(d + 10, &lport, 2);
+	return one_toeplitz(d, 12, key, key_size, 0x7Fu); // subr.c:523
+}

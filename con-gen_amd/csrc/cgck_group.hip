@@ -139,7 +139,7 @@ __device__ __forceinline__ void cksum_body(const KParams &p)
 					// L4 region = datagram minus header: one's-complement
 					// subtraction, tot + ~ip (mod 65535).
 					const uint32_t l4 = fold16(tot) + (0xffffu - fold16(ip));
-					if (flags & CGCK_L4_NOPSEUDO) {
+					if (l4_nopseudo(proto[u], flags)) {
 						uint32_t f = fold16(l4);
 						hi = finish(odd ? bswap16(f) : f);
 					} else {
@@ -275,10 +275,13 @@ static hipError_t launch_t(const KParams &p, int max_blocks, bool nt, hipStream_
 	int blocks = (int)(want < (uint64_t)max_blocks ? want : (uint64_t)max_blocks);
 	if (blocks < 1)
 		blocks = 1;
-	if (nt)
+	if (nt) {
+		CGCK_NOTE_KERNEL("cksum_kernel<%d, %d, %d, %s, true>", G, S, U, tf(DESC));
 		hipLaunchKernelGGL((cksum_kernel<G, S, U, DESC, true>), dim3(blocks), dim3(256), 0, st, p);
-	else
+	} else {
+		CGCK_NOTE_KERNEL("cksum_kernel<%d, %d, %d, %s, false>", G, S, U, tf(DESC));
 		hipLaunchKernelGGL((cksum_kernel<G, S, U, DESC, false>), dim3(blocks), dim3(256), 0, st, p);
+	}
 	return hipGetLastError();
 }
 

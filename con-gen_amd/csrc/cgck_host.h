@@ -1,0 +1,103 @@
+// cgck_host.h — host-side internals shared by cgck_api.cpp (contexts,
+// batches, rings, RSS, plumbing) and cgck_dropin.cpp (the drop-in symbols and
+// the per-thread RX / TX windows).  Not part of the C-ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "cgck_internal.h"
+
+struct cgck_ctx {
+	int device;
+	int num_cus;
+	hipStream_t stream;
+	uint32_t desc_len_hint;
+	int family; // kernel family: 0 auto, 1 group, 2 lane-per-packet ($CGCK_KERNEL)
+	const char *last_kernel; // cgck_ctx_last_kernel
+	// pinned host staging (drop-in calls, deferred TX)
+	uint8_t *h_stage;
+	size_t h_stage_cap;
+	uint32_t *h_out;
+	size_t h_out_cap;
+	// device scratch (host-resident batches)
+	uint8_t *d_bytes;
+	size_t d_bytes_cap;
+	uint8_t *d_aux; // descriptors | out | verdict
+	size_t d_aux_cap;
+	void *d_zero; // kZeroBytes zero bytes (KParams.zero)
+	// Toeplitz byte tables of the last key used (cgck_rss.hip)
+	uint32_t *d_rss_tab;
+	size_t d_rss_tab_cap;
+	uint32_t *h_rss_tab; // host copy (malloc)
+	size_t h_rss_tab_cap;
+	uint8_t *rss_key; // the key the tables were built from (malloc)
+	int rss_key_len;
+	uint32_t rss_cnt;
+	bool rss_valid;
+	void *rss_users; // RssUsers (cgck_api.cpp): one event per stream that read d_rss_tab
+	// dst-cache scratch: control words + look-back status (zeroed per launch)
+	uint8_t *d_dst;
+	size_t d_dst_cap;
+	// burst server (cgck_burst_open): mailbox and staging, host-coherent pinned
+	cgck::BurstBox *bbox; // nullptr: closed
+	uint8_t *bstage;      // [packets | descriptors | out | verdict]
+	size_t bstage_cap;
+	uint8_t *bstage_dev;        // device view of bstage
+	cgck::BurstBox *bbox_dev;   // device view of bbox
+	uint32_t bmax;              // packets per request
+	uint32_t bseq;
+	hipStream_t bstream; // the server's own stream (it stays resident)
+};
+
+namespace cgck {
+
+// Thread-local error text (cgck_last_error); returns `code`.
+int set_err(int code, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
+const char *err_text();
+
+#define HIP_TRY(expr)                                                                     \
+	do {                                                                              \
+		hipError_t e_ = (expr);                                                   \
+		if (e_ != hipSuccess)                                                     \
+			return ::cgck::set_err(-EIO, "%s: %s", #expr, hipGetErrorString(e_)); \
+	} while (0)
+
+int grow_host(void **p, size_t *cap, size_t need);
+int grow_dev(void **p, size_t *cap, size_t need);
+
+// One checksum launch on the context (KParams.zero filled in); records the
+// kernel's name in c->last_kernel.
+int run(cgck_ctx *c, const KParams &p, uint32_t len_hint, hipStream_t st);
+
+// cgck_desc_host without the public flag check (internal flags allowed).
+int desc_host(cgck_ctx *c, void *base, size_t bytes, const cgck_desc_t *desc, uint64_t n, uint32_t flags,
+	      uint32_t *out, uint8_t *verdict);
+
+// Staging path of one region for the drop-in symbols (burst server when open,
+// else a launch on the context stream and a synchronisation).
+int one_region(cgck_ctx *c, const void *src, uint32_t span, uint32_t ip_len, uint32_t flags, uint32_t *out);
+
+// A range registered with cgck_host_register: [lo, hi) and the device
+// pointer of lo.
+struct RegRange {
+	uint8_t *lo, *hi;
+	uint8_t *dev;
+};
+// Is [p, p + bytes) inside one registered range?  Fills *r when it is.
+bool reg_find(const void *p, size_t bytes, RegRange *r);
+
+// The calling thread's drop-in context (created on first use); nullptr with
+// the error text set when no gfx950 device can be used.
+cgck_ctx *thread_ctx();
+cgck_ctx *thread_ctx_if_any(); // the context if this thread made one, else nullptr
+// Report a failure of a call that has no error channel (the drop-in
+// symbols): the handler of cgck_set_error_handler, then abort.
+[[noreturn]] void die(const char *what);
+
+int rss_prepare(cgck_ctx *c, const uint8_t *key, int key_size, uint32_t cnt, hipStream_t st);
+int rss_note_use(cgck_ctx *c, hipStream_t st);
+constexpr uint32_t kRssMaxCnt = 65536;
+
+} // namespace cgck

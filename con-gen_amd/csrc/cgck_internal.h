@@ -11,6 +11,12 @@ namespace cgck {
 // drop-in udp_cksum keeps the pure-function semantics of subr.c:212-223 even
 // for malformed headers.
 constexpr uint32_t kFlagNoLenCheck = 1u << 15;
+// Internal flag of the RX window (cgck_rx_begin): the L4 result of each
+// packet follows its own protocol, as the stack's verifiers do — ICMP (ip_p 1)
+// is in_cksum(ip + hl, len - hl) with its field at +2 (ip_icmp.c:187-189),
+// everything else udp_cksum with the pseudo-header (tcp_input.c:75-78,
+// udp_usrreq.c:86-89).  Group kernel only.
+constexpr uint32_t kFlagL4Auto = 1u << 14;
 
 constexpr uint32_t kImixCycleBytes = 4252; // 7*64 + 4*576 + 1500
 
@@ -112,6 +118,18 @@ hipError_t launch_dst_cache(const DstParams &p, int num_cus, hipStream_t st);
 uint32_t dst_iters(uint32_t n, uint32_t cap, bool filter, uint64_t pass_lo, uint64_t pass_hi, int num_cus);
 
 hipError_t launch_cksum(const KParams &p, uint32_t len_hint, int num_cus, int kernel, hipStream_t st);
+
+// The kernel a launcher just launched, by the name rocprofv3 reports (without
+// namespace and argument list); cgck_ctx_last_kernel reads it back.  Each
+// launch site interns its name once (CGCK_NOTE_KERNEL) and stores the pointer.
+extern thread_local const char *t_kernel;
+const char *intern(const char *fmt, ...) __attribute__((format(printf, 1, 2)));
+#define CGCK_NOTE_KERNEL(...)                                                   \
+	do {                                                                    \
+		static const char *const note_ = ::cgck::intern(__VA_ARGS__);    \
+		::cgck::t_kernel = note_;                                       \
+	} while (0)
+constexpr const char *tf(bool b) { return b ? "true" : "false"; }
 hipError_t launch_synth_fill(uint8_t *base, uint64_t nbytes, uint64_t seed, int num_cus, hipStream_t st);
 hipError_t launch_synth_stamp(uint8_t *base, uint64_t n, uint64_t stride, uint32_t len, int num_cus,
 			      hipStream_t st);

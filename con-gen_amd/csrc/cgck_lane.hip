@@ -414,6 +414,7 @@ __global__ __launch_bounds__(256) void lpp_kernel(KParams p)
 // batches, the descriptors of iteration i+2), so a wave never waits for
 // memory between iterations.  Small packets only (nch <= S0 + the last
 // chunk; longer packets take the same streaming loop as lpp_kernel).
+#if CGCK_LAB // A/B-only: software-pipelined lpp (lpa replaced it)
 template <bool DESC, bool NT>
 __global__ __launch_bounds__(256) void lppp_kernel(KParams p)
 {
@@ -494,6 +495,8 @@ __global__ __launch_bounds__(256) void lppp_kernel(KParams p)
 		last = lastn;
 	}
 }
+
+#endif // CGCK_LAB
 
 // --------------------------------------------------------------------------
 // Lane per packet, aligned fixed-length strided batches (the 64 B config)
@@ -646,10 +649,13 @@ hipError_t launch_lpa(const KParams &p, int num_cus, bool nt, hipStream_t st)
 	const dim3 g((unsigned)(want < mb ? want : mb));
 #define CGCK_LPA(D)                                                                            \
 	do {                                                                                   \
-		if (nt)                                                                        \
+		if (nt) {                                                                      \
+			CGCK_NOTE_KERNEL("lpa_kernel<true, %d>", D);                           \
 			hipLaunchKernelGGL((lpa_kernel<true, D>), g, dim3(256), 0, st, p);      \
-		else                                                                           \
+		} else {                                                                       \
+			CGCK_NOTE_KERNEL("lpa_kernel<false, %d>", D);                          \
 			hipLaunchKernelGGL((lpa_kernel<false, D>), g, dim3(256), 0, st, p);     \
+		}                                                                              \
 	} while (0)
 	if (depth == 4)
 		CGCK_LPA(4);
@@ -699,6 +705,7 @@ __device__ __forceinline__ uint32_t jumbo_window(const uint4 *c0, int nch, int s
 	return r;
 }
 
+#if CGCK_LAB // A/B-only: the first lane-per-slot design (slot2 replaced it)
 template <bool DESC, bool NT>
 __global__ __launch_bounds__(256) void slot_kernel(KParams p)
 {
@@ -831,6 +838,8 @@ __global__ __launch_bounds__(256) void slot_kernel(KParams p)
 	if (r0 < r1)
 		wave_stage_flush(p, ws, r1);
 }
+
+#endif // CGCK_LAB
 
 // --------------------------------------------------------------------------
 // Lane per 128-byte slot, software-pipelined two deep
@@ -1104,62 +1113,33 @@ static hipError_t launch_lpp_t(const KParams &p, int max_blocks, bool nt, hipStr
 	int blocks = (int)(want < (uint64_t)max_blocks ? want : (uint64_t)max_blocks);
 	if (blocks < 1)
 		blocks = 1;
-	if (nt)
+	if (nt) {
+		CGCK_NOTE_KERNEL("lpp_kernel<%s, true, %d, %s>", tf(DESC), S0, tf(CLAMP));
 		hipLaunchKernelGGL((lpp_kernel<DESC, true, S0, CLAMP>), dim3(blocks), dim3(256), 0, st, p);
-	else
+	} else {
+		CGCK_NOTE_KERNEL("lpp_kernel<%s, false, %d, %s>", tf(DESC), S0, tf(CLAMP));
 		hipLaunchKernelGGL((lpp_kernel<DESC, false, S0, CLAMP>), dim3(blocks), dim3(256), 0, st, p);
+	}
 	return hipGetLastError();
 }
 
-template <bool DESC>
-static hipError_t launch_slot_t(const KParams &p, int max_blocks, bool nt, hipStream_t st)
-{
-	// each wave owns a contiguous packet range of >= ~64 packets
-	uint64_t want = (p.n + 4 * 64 - 1) / (4 * 64);
-	int blocks = (int)(want < (uint64_t)max_blocks ? want : (uint64_t)max_blocks);
-	if (blocks < 1)
-		blocks = 1;
-	if (nt)
-		hipLaunchKernelGGL((slot_kernel<DESC, true>), dim3(blocks), dim3(256), 0, st, p);
-	else
-		hipLaunchKernelGGL((slot_kernel<DESC, false>), dim3(blocks), dim3(256), 0, st, p);
-	return hipGetLastError();
-}
-
-template <bool DESC>
-static hipError_t launch_lppp_t(const KParams &p, int max_blocks, bool nt, hipStream_t st)
-{
-	uint64_t want = (p.n + 255) / 256;
-	int blocks = (int)(want < (uint64_t)max_blocks ? want : (uint64_t)max_blocks);
-	if (blocks < 1)
-		blocks = 1;
-	if (nt)
-		hipLaunchKernelGGL((lppp_kernel<DESC, true>), dim3(blocks), dim3(256), 0, st, p);
-	else
-		hipLaunchKernelGGL((lppp_kernel<DESC, false>), dim3(blocks), dim3(256), 0, st, p);
-	return hipGetLastError();
-}
-
-hipError_t launch_lppp(const KParams &p, int num_cus, bool nt, hipStream_t st)
-{
-	return p.desc ? launch_lppp_t<true>(p, num_cus * 8, nt, st) : launch_lppp_t<false>(p, num_cus * 8, nt, st);
-}
-
-// shape: 0 = 4 chunks up front, clamped; 1 = 6 clamped; 2 = 6 predicated;
-// 3 = 4 predicated
+// shape: 0 = 4 chunks up front, clamped; 1 = 6 clamped; 2 = 6 predicated
+// (the default, kDefaultLppShape; the only one in libcgck.so); 3 = 4 predicated
 hipError_t launch_lpp(const KParams &p, int num_cus, bool nt, int shape, hipStream_t st)
 {
 	const int mb = num_cus * 8;
 	const bool d = p.desc != nullptr;
 	switch (shape) {
+#if CGCK_LAB
 	case 1:
 		return d ? launch_lpp_t<true, 6, true>(p, mb, nt, st) : launch_lpp_t<false, 6, true>(p, mb, nt, st);
-	case 2:
-		return d ? launch_lpp_t<true, 6, false>(p, mb, nt, st) : launch_lpp_t<false, 6, false>(p, mb, nt, st);
 	case 3:
 		return d ? launch_lpp_t<true, 4, false>(p, mb, nt, st) : launch_lpp_t<false, 4, false>(p, mb, nt, st);
-	default:
+	case 0:
 		return d ? launch_lpp_t<true, 4, true>(p, mb, nt, st) : launch_lpp_t<false, 4, true>(p, mb, nt, st);
+#endif
+	default:
+		return d ? launch_lpp_t<true, 6, false>(p, mb, nt, st) : launch_lpp_t<false, 6, false>(p, mb, nt, st);
 	}
 }
 
@@ -1170,10 +1150,13 @@ static hipError_t launch_slot2_t(const KParams &p, int max_blocks, bool nt, hipS
 	int blocks = (int)(want < (uint64_t)max_blocks ? want : (uint64_t)max_blocks);
 	if (blocks < 1)
 		blocks = 1;
-	if (nt)
+	if (nt) {
+		CGCK_NOTE_KERNEL("slot2_kernel<%s, true>", tf(DESC));
 		hipLaunchKernelGGL((slot2_kernel<DESC, true>), dim3(blocks), dim3(256), 0, st, p);
-	else
+	} else {
+		CGCK_NOTE_KERNEL("slot2_kernel<%s, false>", tf(DESC));
 		hipLaunchKernelGGL((slot2_kernel<DESC, false>), dim3(blocks), dim3(256), 0, st, p);
+	}
 	return hipGetLastError();
 }
 
@@ -1191,9 +1174,51 @@ hipError_t launch_slot2(const KParams &p, int num_cus, bool nt, hipStream_t st)
 	return p.desc ? launch_slot2_t<true>(p, mb, nt, st) : launch_slot2_t<false>(p, mb, nt, st);
 }
 
+#if CGCK_LAB
+template <bool DESC>
+static hipError_t launch_slot_t(const KParams &p, int max_blocks, bool nt, hipStream_t st)
+{
+	// each wave owns a contiguous packet range of >= ~64 packets
+	uint64_t want = (p.n + 4 * 64 - 1) / (4 * 64);
+	int blocks = (int)(want < (uint64_t)max_blocks ? want : (uint64_t)max_blocks);
+	if (blocks < 1)
+		blocks = 1;
+	if (nt) {
+		CGCK_NOTE_KERNEL("slot_kernel<%s, true>", tf(DESC));
+		hipLaunchKernelGGL((slot_kernel<DESC, true>), dim3(blocks), dim3(256), 0, st, p);
+	} else {
+		CGCK_NOTE_KERNEL("slot_kernel<%s, false>", tf(DESC));
+		hipLaunchKernelGGL((slot_kernel<DESC, false>), dim3(blocks), dim3(256), 0, st, p);
+	}
+	return hipGetLastError();
+}
+
+template <bool DESC>
+static hipError_t launch_lppp_t(const KParams &p, int max_blocks, bool nt, hipStream_t st)
+{
+	uint64_t want = (p.n + 255) / 256;
+	int blocks = (int)(want < (uint64_t)max_blocks ? want : (uint64_t)max_blocks);
+	if (blocks < 1)
+		blocks = 1;
+	if (nt) {
+		CGCK_NOTE_KERNEL("lppp_kernel<%s, true>", tf(DESC));
+		hipLaunchKernelGGL((lppp_kernel<DESC, true>), dim3(blocks), dim3(256), 0, st, p);
+	} else {
+		CGCK_NOTE_KERNEL("lppp_kernel<%s, false>", tf(DESC));
+		hipLaunchKernelGGL((lppp_kernel<DESC, false>), dim3(blocks), dim3(256), 0, st, p);
+	}
+	return hipGetLastError();
+}
+
+hipError_t launch_lppp(const KParams &p, int num_cus, bool nt, hipStream_t st)
+{
+	return p.desc ? launch_lppp_t<true>(p, num_cus * 8, nt, st) : launch_lppp_t<false>(p, num_cus * 8, nt, st);
+}
+
 hipError_t launch_slot(const KParams &p, int num_cus, bool nt, hipStream_t st)
 {
 	return p.desc ? launch_slot_t<true>(p, num_cus * 8, nt, st) : launch_slot_t<false>(p, num_cus * 8, nt, st);
 }
+#endif // CGCK_LAB
 
 } // namespace cgck

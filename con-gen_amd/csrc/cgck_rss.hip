@@ -236,30 +236,43 @@ hipError_t launch_toeplitz(const RssParams &p0, int num_cus, hipStream_t st)
 		}();
 		const uint64_t capb = (uint64_t)num_cus * bpc;
 		const dim3 gb((unsigned)(want < capb ? want : capb));
+#define CGCK_RSS_AB(D)                                                                          \
+	do {                                                                                    \
+		CGCK_NOTE_KERNEL("toeplitz12x4_ab_kernel<%d>", D);                              \
+		hipLaunchKernelGGL(toeplitz12x4_ab_kernel<D>, gb, dim3(256), 12 * 256 * 4, st, p, ng); \
+	} while (0)
+#if CGCK_LAB
 		if (var == 2 && depth == 16)
-			hipLaunchKernelGGL(toeplitz12x4_ab_kernel<16>, gb, dim3(256), 12 * 256 * 4, st, p, ng);
+			CGCK_RSS_AB(16);
 		else if (var == 2 && depth == 12)
-			hipLaunchKernelGGL(toeplitz12x4_ab_kernel<12>, gb, dim3(256), 12 * 256 * 4, st, p, ng);
+			CGCK_RSS_AB(12);
 		else if (var == 2 && depth == 10)
-			hipLaunchKernelGGL(toeplitz12x4_ab_kernel<10>, gb, dim3(256), 12 * 256 * 4, st, p, ng);
+			CGCK_RSS_AB(10);
 		else if (var == 2 && depth == 8)
-			hipLaunchKernelGGL(toeplitz12x4_ab_kernel<8>, gb, dim3(256), 12 * 256 * 4, st, p, ng);
+			CGCK_RSS_AB(8);
 		else if (var == 2 && depth == 6)
-			hipLaunchKernelGGL(toeplitz12x4_ab_kernel<6>, gb, dim3(256), 12 * 256 * 4, st, p, ng);
+			CGCK_RSS_AB(6);
 		else if (var == 2 && depth == 5)
-			hipLaunchKernelGGL(toeplitz12x4_ab_kernel<5>, gb, dim3(256), 12 * 256 * 4, st, p, ng);
+			CGCK_RSS_AB(5);
 		else if (var == 2 && depth == 4)
-			hipLaunchKernelGGL(toeplitz12x4_ab_kernel<4>, gb, dim3(256), 12 * 256 * 4, st, p, ng);
+			CGCK_RSS_AB(4);
 		else if (var == 2 && depth == 3)
-			hipLaunchKernelGGL(toeplitz12x4_ab_kernel<3>, gb, dim3(256), 12 * 256 * 4, st, p, ng);
+			CGCK_RSS_AB(3);
 		else if (var == 2)
-			hipLaunchKernelGGL(toeplitz12x4_ab_kernel<2>, gb, dim3(256), 12 * 256 * 4, st, p, ng);
-		else if (var == 1)
-			hipLaunchKernelGGL(toeplitz12x4_kernel<true>, dim3((unsigned)(want < capb ? want : capb)),
-					   dim3(256), 24 * 16 * 4, st, p, ng);
-		else
-			hipLaunchKernelGGL(toeplitz12x4_kernel<false>, dim3((unsigned)(want < capb ? want : capb)),
-					   dim3(256), 12 * 256 * 4, st, p, ng);
+			CGCK_RSS_AB(2);
+		else if (var == 1) {
+			CGCK_NOTE_KERNEL("toeplitz12x4_kernel<true>");
+			hipLaunchKernelGGL(toeplitz12x4_kernel<true>, gb, dim3(256), 24 * 16 * 4, st, p, ng);
+		} else {
+			CGCK_NOTE_KERNEL("toeplitz12x4_kernel<false>");
+			hipLaunchKernelGGL(toeplitz12x4_kernel<false>, gb, dim3(256), 12 * 256 * 4, st, p, ng);
+		}
+#else
+		(void)var;
+		(void)depth;
+		CGCK_RSS_AB(12); // the measured default; the other depths and forms are lab builds
+#endif
+#undef CGCK_RSS_AB
 		hipError_t e = hipGetLastError();
 		if (e != hipSuccess || ng * 4 == p.n)
 			return e;
@@ -273,14 +286,25 @@ hipError_t launch_toeplitz(const RssParams &p0, int num_cus, hipStream_t st)
 	const bool aligned = ((uintptr_t)p.data & 3) == 0 && (p.stride & 3) == 0;
 	const bool lds = p.cnt <= kRssLdsMaxCnt;
 	const size_t sh = lds ? (size_t)p.cnt * 256 * 4 : 0;
-	if (aligned && p.cnt == 12)
+	// (after the x4 kernel this is the n % 4 tail: the x4 kernel keeps the name)
+	const bool note = p.n == p0.n;
+	if (aligned && p.cnt == 12) {
+		if (note)
+			CGCK_NOTE_KERNEL("toeplitz_kernel<3, true>");
 		hipLaunchKernelGGL((toeplitz_kernel<3, true>), g, b, sh, st, p);
-	else if (aligned && p.cnt == 36)
+	} else if (aligned && p.cnt == 36) {
+		if (note)
+			CGCK_NOTE_KERNEL("toeplitz_kernel<9, true>");
 		hipLaunchKernelGGL((toeplitz_kernel<9, true>), g, b, sh, st, p);
-	else if (lds)
+	} else if (lds) {
+		if (note)
+			CGCK_NOTE_KERNEL("toeplitz_kernel<0, true>");
 		hipLaunchKernelGGL((toeplitz_kernel<0, true>), g, b, sh, st, p);
-	else
+	} else {
+		if (note)
+			CGCK_NOTE_KERNEL("toeplitz_kernel<0, false>");
 		hipLaunchKernelGGL((toeplitz_kernel<0, false>), g, b, 0, st, p);
+	}
 	return hipGetLastError();
 }
 
@@ -605,10 +629,13 @@ hipError_t launch_dst_cache(const DstParams &p, int num_cus, hipStream_t st)
 	g = g > gmax ? gmax : g;
 	g = g > p.ntiles ? p.ntiles : g;
 	const size_t lds = (p.filter ? 12 * 256 * 4 : 0) + kDstMaskBytes + 64;
-	if (p.filter)
+	if (p.filter) {
+		CGCK_NOTE_KERNEL("dst_cache_kernel<true>");
 		hipLaunchKernelGGL(dst_cache_kernel<true>, dim3((unsigned)g), dim3(256), lds, st, p);
-	else
+	} else {
+		CGCK_NOTE_KERNEL("dst_cache_kernel<false>");
 		hipLaunchKernelGGL(dst_cache_kernel<false>, dim3((unsigned)g), dim3(256), lds, st, p);
+	}
 	return hipGetLastError();
 }
 

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define CGCK_ABI_VERSION 1
+#define CGCK_ABI_VERSION 2
 
 /* ------------------------------------------------------------------------ */
 /* 1. Drop-in symbols (subr.h:373-374; bodies subr.c:186-195, 212-223).     */
@@ -146,18 +146,68 @@ int cgck_host_register(void *ptr, size_t bytes);
 int cgck_host_unregister(void *ptr);
 
 /* The drop-in symbols run on a per-thread context created on first use
- * (device from $CGCK_DEVICE, default 0).  A worker thread that exits calls
- * this to release it. */
+ * (device from $CGCK_DEVICE, default 0).  cgck_thread_ctx returns that
+ * context (creating it), so a worker's batched calls (cgck_desc_host,
+ * cgck_dst_cache_host, ...) share its stream and staging with the drop-ins;
+ * NULL on failure (cgck_last_error says why).  A worker thread that exits
+ * calls cgck_thread_release to free it. */
+cgck_ctx_t *cgck_thread_ctx(void);
 int cgck_thread_release(void);
+
+/* The drop-in symbols have no error channel (their prototypes are the
+ * reference's).  When one cannot produce a result (no device, a launch or
+ * synchronisation failure) it calls the handler set here with what failed
+ * and cgck_last_error()'s text — con-gen passes a function that ends in its
+ * panic3() (subr.c:238-261), which prints the stats and exits.  If the
+ * handler returns, or none is set, the library prints the message and
+ * aborts.  Process-wide; NULL restores the default. */
+typedef void (*cgck_error_fn)(const char *what, const char *msg, void *arg);
+void cgck_set_error_handler(cgck_error_fn fn, void *arg);
+
+/* RX window at the transport's receive burst.
+ * cgck_rx_begin computes, for every frame of the burst in one launch, the
+ * values the stack's own verifiers are about to ask for — ip_cksum of the
+ * header with ip_sum read as zero (ip_input.c:49-51, gbtcp/inet.c:319-322)
+ * and the L4 checksum with its field read as zero: tcp_cksum / udp_cksum of
+ * the segment (tcp_input.c:75-78, udp_usrreq.c:86-89, gbtcp/inet.c:142-145)
+ * or, for ICMP, in_cksum of the message (ip_icmp.c:187-189).  Until
+ * cgck_rx_end, this thread's drop-in in_cksum / udp_cksum calls on those
+ * headers and segments (same pointer, same length) return the precomputed
+ * value without touching the GPU; any other call is computed synchronously
+ * as outside the window.  The stack's verify, count and drop code
+ * (t_*_do_incksum 0/1/2) therefore runs unchanged.
+ *
+ * desc[i] = {frame offset from base, l3_off (14 for Ethernet), bytes
+ * received after l3_off (ip_input's `len`)}; [base, base + bytes) must hold
+ * every frame and stay unchanged (apart from the checksum fields the stack
+ * zeroes and rewrites) until cgck_rx_end.  The L4 value covers
+ * ntohs(ip_len) - ip_hl*4 bytes when the frame holds them.  Registered
+ * memory (cgck_host_register) is read in place.  Returns the number of
+ * frames precomputed, or a negative errno (-EBUSY: a window is already
+ * open).  cgck_rx_end returns how many calls the window answered. */
+int cgck_rx_begin(void *base, size_t bytes, const cgck_desc_t *desc, uint64_t n);
+int cgck_rx_end(void);
 
 /* Deferred TX fill.  Between begin and flush, the
  * drop-in in_cksum/udp_cksum calls of THIS thread that target an IPv4
- * header (len == ip_hl*4) or a TCP/UDP segment return 0 and are queued; the
- * flush computes them in one launch and writes each result into its field
- * (ip+10; TCP +16 / UDP +6 after the header).  Returns the number of
- * fields written, or a negative errno. */
+ * header (len == ip_hl*4) or a TCP/UDP segment lying inside memory
+ * registered with cgck_host_register (the transport's ring or mempool,
+ * whose slots stay owned by the stack until the kick) return 0 and are
+ * queued; a second call for the same header or segment replaces the first.
+ * Calls on any other memory (a stack-local struct packet, pkt_body) are
+ * computed synchronously, as outside the window.  The flush computes the
+ * queue in one launch and writes each result into its field (ip+10; TCP +16
+ * / UDP +6 after the header); it must run before the transport hands the
+ * slots to the NIC.  Returns the number of fields written, or a negative
+ * errno. */
 int cgck_tx_begin(void);
 int cgck_tx_flush(void);
+
+/* Per-thread window counters since the thread's first call:
+ * [0] drop-in calls answered by an RX window, [1] calls inside an RX window
+ * computed synchronously (no match), [2] calls queued by a TX window, [3]
+ * calls inside a TX window computed synchronously (memory not registered). */
+int cgck_window_stats(uint64_t stats[4]);
 
 /* Burst server (latency).  Keeps one workgroup
  * resident on `ctx` (NULL: this thread's drop-in context) that serves small
@@ -245,6 +295,11 @@ int cgck_host_alloc(size_t bytes, void **ptr); /* pinned */
 int cgck_host_free(void *ptr);
 int cgck_memcpy(void *dst, const void *src, size_t bytes, void *stream); /* async, any direction */
 int cgck_memset(void *dst, int value, size_t bytes, void *stream);
+
+/* Name of the last checksum / hash kernel the context's dispatcher launched,
+ * as rocprofv3 reports it (e.g. "cksum_kernel<16, 6, 1, false, true>");
+ * "" before the first launch. */
+const char *cgck_ctx_last_kernel(cgck_ctx_t *ctx);
 
 /* HIP-event timing on a given stream (NULL = context stream). */
 typedef struct cgck_event cgck_event_t;

@@ -101,6 +101,10 @@ class Port:
                                        ctypes.c_uint8, ctypes.c_void_p, ctypes.c_int,
                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32]
         L.oracle_fn_rss_hash4.restype = ctypes.c_void_p
+        # RX call-sequence replay (oracle/stack_replay.c)
+        L.oracle_replay_rx.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                       ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                       ctypes.c_void_p, ctypes.c_void_p]
 
     # -- pure functions (subr.c:186-195, 212-223) --
     def in_cksum(self, buf, off=0, n=None):
@@ -210,6 +214,20 @@ class Port:
 
     def fn_rss_hash4(self):
         return self.lib.oracle_fn_rss_hash4()
+
+    # outcome codes and counter slots of oracle_replay_rx (oracle/stack_replay.c)
+    R_ACCEPT, R_DROP, R_DROP_IP, R_DROP_L4, R_BYPASS = range(5)
+    COUNTERS = ("ips_badsum", "tcps_rcvbadsum", "udps_badsum", "icps_checksum", "in_calls", "udp_calls")
+
+    def replay_rx(self, fin, fudp, base, desc12, n, stack, ip_in, tcp_in):
+        """Replay the reference stack's RX call sequence (stack 0 bsd44, 1
+        gbtcp) over a burst, with the given in_cksum / udp_cksum pointers.
+        Mutates `base` as the reference does; returns (outcomes, counters)."""
+        res = np.zeros(max(n, 1), np.uint8)
+        ctr = np.zeros(6, np.uint64)
+        self.lib.oracle_replay_rx(fin, fudp, base.ctypes.data, desc12.ctypes.data, n, stack, ip_in, tcp_in,
+                                  res.ctypes.data, ctr.ctypes.data)
+        return res[:n], ctr
 
     def cpu_bench(self, fin, fudp, base, n, stride, ip_len, threads=1, reps=1):
         sink = ctypes.c_uint64()

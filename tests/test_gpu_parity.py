@@ -209,7 +209,7 @@ def test_fuzz_strided_vs_oracle(engine, port, stride, l3, ln, flags):
 # Every kernel family forced through $CGCK_KERNEL (read at context creation),
 # on the strided shapes each one accepts; a family falls back to the group
 # kernel where its preconditions fail, so every cell is a valid comparison.
-FAMILIES = ["group", "lpp", "lpa", "slot2", "str"]
+FAMILIES = ["group", "lpp", "lpa", "slot2"]   # every family libcgck.so dispatches to
 FAMILY_SHAPES = [  # (stride, l3_off, ip_len, packets); odd counts: every ip_hl = 5
     (64, 0, 64, 3000), (64, 0, 64, 4097), (64, 16, 64, 999), (64, 0, 48, 333), (32, 0, 20, 333), (128, 16, 64, 333), (72, 2, 60, 333),
     (256, 0, 255, 333), (1500, 0, 1500, 3000), (1504, 4, 1500, 333), (1520, 0, 1517, 333),
@@ -452,7 +452,9 @@ def test_burst_server_dropin_and_tx(port):
             row[14 + 36:14 + 38] = np.frombuffer(np.uint16(v).tobytes(), np.uint8)
             v = cgck.ip_cksum(row, 14)
             row[14 + 10:14 + 12] = np.frombuffer(np.uint16(v).tobytes(), np.uint8)
-        assert cgck.tx_flush() == 2 * len(want)
+        # the ring is not registered: every call was answered synchronously
+        # (through the server) and nothing is left for the flush
+        assert cgck.tx_flush() == 0
         for i, (ln, ref) in enumerate(want):
             assert np.array_equal(ring[i, 14:14 + ln], ref), i
     finally:
@@ -475,7 +477,8 @@ def test_deferred_tx_fill(engine, port, registered):
     """Deferred TX window: the stack's own call pattern (tcp_output.c:416-418
     then ip_output.c:61-64, each storing the return value) inside
     cgck_tx_begin/flush yields the same bytes as the synchronous reference
-    sequence — staged, or read in place from a registered ring."""
+    sequence — queued and read in place from a registered ring, or answered
+    synchronously when the memory is not registered."""
     rng = np.random.default_rng(23)
     raw = np.zeros(256 * 2048 + 4096, np.uint8)
     off = (-raw.ctypes.data) % 4096
@@ -508,7 +511,7 @@ def test_deferred_tx_fill(engine, port, registered):
         v = cgck.ip_cksum(row, 14)                              # ip->ip_sum = ip_cksum(ip)
         row[14 + 10:14 + 12] = np.frombuffer(np.uint16(v).tobytes(), np.uint8)
     try:
-        assert cgck.tx_flush() == 2 * len(want)
+        assert cgck.tx_flush() == (2 * len(want) if registered else 0)
     finally:
         if registered:
             cgck.load().cgck_host_unregister(ring.ctypes.data)

@@ -1,0 +1,246 @@
+"""GPU tests of the per-thread windows (include/cgck.h, cgck_dropin.cpp).
+
+RX window: a receive burst goes through cgck_rx_begin,
+then the reference stack's own RX call sequence (oracle/stack_replay.c:
+ip_input.c:20-112, tcp_input.c:60-85, udp_usrreq.c:53-94, ip_icmp.c:160-193;
+gbtcp/inet.c:118-159, 275-352) runs over the same ring calling libcgck.so's
+drop-in in_cksum / udp_cksum.  A second copy replays with the reference's
+own subr.c functions (oracle/_ref; the restatement where that build is
+absent).  Outcomes, the badsum counter increments, the number of checksum
+calls and every byte of the ring afterwards must match, for both stacks and
+every t_ip_do_incksum x t_tcp_do_incksum in {0, 1, 2} (con-gen.c:733-736).
+
+TX window (rank 2): only registered ring memory is queued; other memory is
+computed synchronously; a header or segment queued twice keeps the later call.
+"""
+import itertools
+import threading
+
+import numpy as np
+import pytest
+
+import cgck
+import oracle
+import rxcorpus
+
+pytestmark = pytest.mark.gpu
+
+FLAGS = list(itertools.product((0, 1), (0, 1, 2), (0, 1, 2)))   # stack, ip_in, tcp_in
+
+
+def referee(port):
+    R = oracle.reference()
+    return R if R is not None else port
+
+
+def replay_pair(port, buf, desc, stack, ip_in, tcp_in, gpu_ring=None):
+    """(reference replay, GPU-window replay, window counters, served)."""
+    R = referee(port)
+    ref = buf.copy()
+    a = port.replay_rx(*R.fn_pointers(), ref, desc.view(np.uint8), len(desc), stack, ip_in, tcp_in)
+    got = gpu_ring if gpu_ring is not None else buf.copy()
+    if gpu_ring is not None:
+        got[:len(buf)] = buf
+    s0 = cgck.window_stats()
+    m = cgck.rx_begin(got, desc)
+    try:
+        b = port.replay_rx(*cgck.fn_pointers(), got, desc.view(np.uint8), len(desc), stack, ip_in, tcp_in)
+    finally:
+        served = cgck.rx_end()
+    s1 = cgck.window_stats()
+    return (a, ref), (b, got[:len(buf)]), m, served, [y - x for x, y in zip(s0, s1)]
+
+
+@pytest.mark.parametrize("clean", [True, False])
+@pytest.mark.parametrize("registered", [False, True])
+def test_rx_window_replay(port, clean, registered):
+    rng = np.random.default_rng(101 + clean + 2 * registered)
+    frames = rxcorpus.corpus(rng, referee(port), 400, clean=clean)
+    buf, desc = rxcorpus.ring(frames)
+    L = cgck.load()
+    raw = ring = None
+    if registered:
+        raw, ring, size = rxcorpus.registered_copy(buf)
+        assert L.cgck_host_register(ring.ctypes.data, size) == 0
+    try:
+        for stack, ip_in, tcp_in in FLAGS:
+            (a, ref), (b, got), m, served, d = replay_pair(port, buf, desc, stack, ip_in, tcp_in, ring)
+            cell = (stack, ip_in, tcp_in)
+            assert np.array_equal(a[0], b[0]), (cell, np.nonzero(a[0] != b[0])[0][:8])
+            assert np.array_equal(a[1], b[1]), (cell, a[1], b[1])
+            assert np.array_equal(ref, got), cell
+            calls = int(b[1][4] + b[1][5])
+            assert served == d[0] and served + d[1] == calls, (cell, served, d, calls)
+            if clean:
+                assert m == len(frames) and d[1] == 0, (cell, m, d)   # every call from the window
+            else:
+                assert served >= 0.9 * calls, (cell, served, calls)
+            assert d[2] == 0 and d[3] == 0
+    finally:
+        if registered:
+            L.cgck_host_unregister(ring.ctypes.data)
+
+
+def test_rx_window_fixture_frames(port, golden_verify):
+    """The reference-made verify fixtures (tests/golden/verify.json) as one
+    burst: verdicts through the window equal the fixtures' own."""
+    frames = [np.frombuffer(bytes.fromhex(c["hex"]), np.uint8).copy() for c in golden_verify["cases"]]
+    buf, desc = rxcorpus.ring(frames)
+    for stack, ip_in, tcp_in in FLAGS:
+        (a, ref), (b, got), m, served, d = replay_pair(port, buf, desc, stack, ip_in, tcp_in)
+        assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and np.array_equal(ref, got)
+    # with both flags at 1 on bsd44 every IP verdict is the fixture's bsd_ip
+    (a, _), (b, _), _, _, _ = replay_pair(port, buf, desc, 0, 1, 1)
+    assert int(b[1][0]) == sum(1 - c["bsd_ip"] for c in golden_verify["cases"])
+    assert all((r == oracle.Port.R_DROP_IP) == (c["bsd_ip"] == 0) for r, c in zip(b[0], golden_verify["cases"]))
+
+
+def test_rx_window_errors_and_reuse(port):
+    rng = np.random.default_rng(7)
+    buf, desc = rxcorpus.ring(rxcorpus.corpus(rng, port, 8, clean=True))
+    assert cgck.rx_begin(buf, desc) == 8
+    with pytest.raises(cgck.CgckError, match="already open"):
+        cgck.rx_begin(buf, desc)
+    assert cgck.rx_end() == 0
+    with pytest.raises(cgck.CgckError, match="no open RX window"):
+        cgck.rx_end()
+    bad = desc.copy()
+    bad[7]["ip_len"] = 60000                        # past the ring
+    with pytest.raises(cgck.CgckError, match="reaches past"):
+        cgck.rx_begin(buf, bad)
+    assert cgck.rx_begin(buf, desc[:0]) == 0        # empty burst
+    assert cgck.rx_end() == 0
+    # outside a window the same calls are synchronous and still exact
+    ip = buf[rxcorpus.L2:]
+    assert cgck.ip_cksum(ip, 0) == referee(port).in_cksum(ip, 0, (int(ip[0]) & 15) * 4)
+
+
+def test_rx_window_threads(port):
+    """Windows are per thread: four threads, four bursts, one window each."""
+    errs = []
+
+    def work(t):
+        try:
+            rng = np.random.default_rng(500 + t)
+            buf, desc = rxcorpus.ring(rxcorpus.corpus(rng, referee(port), 200, clean=True))
+            for stack, ip_in, tcp_in in FLAGS[::3]:
+                (a, ref), (b, got), m, served, d = replay_pair(port, buf, desc, stack, ip_in, tcp_in)
+                assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and np.array_equal(ref, got)
+                assert d[1] == 0
+        except Exception as e:  # noqa: BLE001 — reported below
+            errs.append(repr(e))
+        finally:
+            cgck.thread_release()
+
+    th = [threading.Thread(target=work, args=(t,)) for t in range(4)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs, errs
+
+
+# ---------------------------------------------------------------------------
+# TX window
+# ---------------------------------------------------------------------------
+
+def tx_calls(row, ln, fo):
+    """tcp_output.c:416-418 then ip_output.c:61-64 on the packet at row+14."""
+    row[14 + 20 + fo:14 + 20 + fo + 2] = 0
+    v = cgck.udp_cksum(row, 14, ln - 20)
+    row[14 + 20 + fo:14 + 20 + fo + 2] = np.frombuffer(np.uint16(v).tobytes(), np.uint8)
+    row[14 + 10:14 + 12] = 0
+    v = cgck.ip_cksum(row, 14)
+    row[14 + 10:14 + 12] = np.frombuffer(np.uint16(v).tobytes(), np.uint8)
+
+
+def expected(port, pkt, fo):
+    ref = pkt.copy()
+    ref[20 + fo:22 + fo] = 0
+    ref[20 + fo:22 + fo] = np.frombuffer(np.uint16(port.udp_cksum(ref, 0, len(ref) - 20)).tobytes(), np.uint8)
+    ref[10:12] = 0
+    ref[10:12] = np.frombuffer(np.uint16(port.in_cksum(ref, 0, 20)).tobytes(), np.uint8)
+    return ref
+
+
+def tcp_pkt(rng, ln):
+    p = rng.integers(0, 256, ln, dtype=np.uint8)
+    p[0] = 0x45
+    p[9] = 6
+    return p
+
+
+def test_tx_window_queues_only_registered_memory(port):
+    """A stack-local struct packet (tcp_output.c:330-359, pkt_body) is not
+    ring memory: its calls are answered synchronously inside the window and
+    the flush never touches it; ring slots are queued and filled."""
+    rng = np.random.default_rng(61)
+    raw, ring, size = rxcorpus.registered_copy(np.zeros(64 * 2048, np.uint8))
+    slots = ring[:64 * 2048].reshape(64, 2048)
+    local = np.zeros((64, 2048), np.uint8)
+    L = cgck.load()
+    assert L.cgck_host_register(ring.ctypes.data, size) == 0
+    try:
+        want = []
+        for i in range(64):
+            ln = int(rng.integers(40, 523))
+            pkt = tcp_pkt(rng, ln)
+            tgt = slots if i % 2 else local
+            tgt[i, 14:14 + ln] = pkt
+            want.append((tgt, i, ln, expected(port, pkt, 16)))
+        s0 = cgck.window_stats()
+        cgck.tx_begin()
+        for tgt, i, ln, _ in want:
+            tx_calls(tgt[i], ln, 16)
+        s1 = cgck.window_stats()
+        for tgt, i, ln, ref in want:   # synchronous ones are already final
+            if tgt is local:
+                assert np.array_equal(tgt[i, 14:14 + ln], ref), i
+        assert cgck.tx_flush() == 64          # 32 registered packets x 2 fields
+        assert s1[2] - s0[2] == 64 and s1[3] - s0[3] == 64
+        for tgt, i, ln, ref in want:
+            assert np.array_equal(tgt[i, 14:14 + ln], ref), i
+    finally:
+        L.cgck_host_unregister(ring.ctypes.data)
+
+
+def test_tx_window_slot_reused_before_flush(port):
+    """toy_flush reuses one struct packet (gbtcp/tcp.c:615-626): a slot that
+    gets a second packet before the flush is filled for the second one."""
+    rng = np.random.default_rng(62)
+    raw, ring, size = rxcorpus.registered_copy(np.zeros(8 * 2048, np.uint8))
+    slots = ring[:8 * 2048].reshape(8, 2048)
+    L = cgck.load()
+    assert L.cgck_host_register(ring.ctypes.data, size) == 0
+    try:
+        cgck.tx_begin()
+        first = tcp_pkt(rng, 300)
+        slots[0, 14:14 + 300] = first
+        tx_calls(slots[0], 300, 16)
+        second = tcp_pkt(rng, 120)                 # a shorter packet in the same slot
+        slots[0, 14:14 + 300] = 0
+        slots[0, 14:14 + 120] = second
+        tx_calls(slots[0], 120, 16)
+        other = tcp_pkt(rng, 522)
+        slots[1, 14:14 + 522] = other
+        tx_calls(slots[1], 522, 16)
+        assert cgck.tx_flush() == 4                # 2 fields x 2 distinct packets
+        assert np.array_equal(slots[0, 14:14 + 120], expected(port, second, 16))
+        assert not slots[0, 14 + 120:14 + 300].any()
+        assert np.array_equal(slots[1, 14:14 + 522], expected(port, other, 16))
+    finally:
+        L.cgck_host_unregister(ring.ctypes.data)
+
+
+def test_last_kernel_names(engine):
+    """cgck_ctx_last_kernel reports the dispatcher's choice by the name
+    rocprofv3 shows."""
+    n = 4096
+    buf = cgck.DeviceBuffer(n * 1500)
+    out = cgck.DeviceBuffer(4 * n)
+    engine.synth_strided(buf.ptr, n, 1500, 1500, 5)
+    engine.strided(buf.ptr, n, 1500, 0, 1500, cgck.GEN_BOTH, out.ptr)
+    assert engine.last_kernel == "cksum_kernel<16, 6, 1, false, true>"
+    engine.strided(buf.ptr, n, 64, 0, 64, cgck.GEN_BOTH, out.ptr)
+    assert engine.last_kernel.startswith("lpa_kernel<false, ")
+    engine.sync()

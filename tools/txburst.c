@@ -6,19 +6,25 @@
  *               ring (2048-byte slots, IPv4 header at +14) with the BSD
  *               verify semantics (ip_input.c:45-58, tcp_input.c:75-85);
  *               verdicts and results come back to host memory.
- *   tx_fill   — the deferred TX window: per packet the stack's own calls,
- *               udp_cksum(ip, len - 20) then in_cksum(ip, 20), queued between
- *               cgck_tx_begin() and cgck_tx_flush() (glue.c:15-41 batch point),
- *               the flush writing every field in place.
+ *   rx_window — the RX window: cgck_rx_begin() over the burst, then per
+ *               packet the stack's own verify calls, in_cksum(ip, 20) and
+ *               udp_cksum(ip, len - 20) with the fields zeroed and restored
+ *               (gbtcp/inet.c:319-330, 142-153), answered from the window,
+ *               then cgck_rx_end().
+ *   tx_fill   — the deferred TX window on the registered ring: per packet
+ *               the stack's own calls, udp_cksum(ip, len - 20) then
+ *               in_cksum(ip, 20), queued between cgck_tx_begin() and
+ *               cgck_tx_flush() (glue.c:15-41 batch point), the flush writing
+ *               every field in place.
  *
  * RX is measured four ways: the launch path on pageable ring memory, the
  * ring registered (cgck_host_register: read where it lies), the resident
  * burst server (cgck_burst_open: no launch or stream sync per call), and
- * both; TX the first two; plus one synchronous drop-in in_cksum without and
- * with the server.
- * Prints one JSON line per (mode, packet length, burst).  Parity of both
- * paths is covered by tests/test_gpu_parity.py; here each run also checks
- * that the verify pass flags exactly the packets it corrupted.
+ * both; TX on the registered ring (the window queues only registered
+ * memory); plus one synchronous drop-in in_cksum without and with the
+ * server.  Prints one JSON line per (mode, packet length, burst).  Parity of
+ * every path is covered by tests/; here each run also checks that the
+ * verify passes flag exactly the packets it corrupted.
  *
  *   tools/txburst [seconds per cell, default 0.4]
  */
@@ -109,8 +115,9 @@ int main(int argc, char **argv)
 			const int reg = pass & 1, srv = pass >= 2;
 			static const char *rx_name[4] = {"rx_verify", "rx_verify_registered", "rx_verify_server",
 							 "rx_verify_registered_server"};
-			static const char *tx_name[2] = {"tx_fill", "tx_fill_registered"};
-			if (pass == 1 || pass == 2) /* the previous pass's TX cells refilled the fields: toggle the corruption back */
+			static const char *win_name[4] = {"rx_window", "rx_window_registered", "rx_window_server",
+							  "rx_window_registered_server"};
+			if (pass == 2) /* pass 1's TX cells refilled the fields: toggle the corruption back */
 				for (int i = 0; i < maxb; i += 64)
 					ring[(size_t)i * SLOT + L3 + len - 1] ^= 0x5A;
 			if (reg && cgck_host_register(ring, (size_t)maxb * SLOT)) {
@@ -149,7 +156,48 @@ int main(int argc, char **argv)
 				       rx_name[pass], len, R, it, us, R / us, bad_ip, bad_l4, (R + 63) / 64);
 				fflush(stdout);
 			}
-			for (int bi = 0; bi < 3 && !srv; bi++) { /* TX flushes do not use the server */
+			for (int bi = 0; bi < 3; bi++) {
+				const int R = bursts[bi];
+				int it = 0, w = 0, bad_ip = 0, bad_l4 = 0;
+				double t0 = now();
+				while (it < maxit && now() - t0 < budget + 0.05) {
+					double a = now();
+					int bi_ = 0, bl_ = 0;
+					if (cgck_rx_begin(ring, (size_t)R * SLOT, desc, R) != R) {
+						fprintf(stderr, "txburst: rx_begin failed: %s\n", cgck_last_error());
+						return 1;
+					}
+					for (int i = 0; i < R; i++) {
+						uint8_t *ip = ring + (size_t)i * SLOT + L3;
+						uint16_t saved, v;
+						memcpy(&saved, ip + 10, 2); /* inet.c:319-330 */
+						ip[10] = ip[11] = 0;
+						v = in_cksum(ip, 20);
+						bi_ += v != saved;
+						memcpy(ip + 10, &saved, 2);
+						memcpy(&saved, ip + 20 + 16, 2); /* inet.c:142-153 */
+						ip[20 + 16] = ip[20 + 17] = 0;
+						v = udp_cksum((struct ip *)ip, len - 20);
+						bl_ += v != saved;
+						memcpy(ip + 20 + 16, &saved, 2);
+					}
+					if (cgck_rx_end() != 2 * R) {
+						fprintf(stderr, "txburst: the window answered fewer than %d calls\n", 2 * R);
+						return 1;
+					}
+					bad_ip = bi_;
+					bad_l4 = bl_;
+					if (w++ >= 20)
+						t[it++] = now() - a;
+				}
+				const double us = median(t, it) * 1e6;
+				printf("{\"mode\": \"%s\", \"pkt_len\": %d, \"burst\": %d, \"iters\": %d, "
+				       "\"us_median\": %.2f, \"mpkt_s\": %.3f, \"bad_ip\": %d, \"bad_l4\": %d, "
+				       "\"bad_l4_expected\": %d}\n",
+				       win_name[pass], len, R, it, us, R / us, bad_ip, bad_l4, (R + 63) / 64);
+				fflush(stdout);
+			}
+			for (int bi = 0; bi < 3 && pass == 1; bi++) { /* TX: registered ring, launch path */
 				const int R = bursts[bi];
 				int it = 0, w = 0;
 				double t0 = now();
@@ -178,7 +226,7 @@ int main(int argc, char **argv)
 				const double us = median(t, it) * 1e6;
 				printf("{\"mode\": \"%s\", \"pkt_len\": %d, \"burst\": %d, \"iters\": %d, "
 				       "\"us_median\": %.2f, \"mpkt_s\": %.3f}\n",
-				       tx_name[reg], len, R, it, us, R / us);
+				       "tx_fill_registered", len, R, it, us, R / us);
 				fflush(stdout);
 			}
 			if (srv) {
