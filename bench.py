@@ -7,17 +7,23 @@ over one batch of synthetic packets already resident in HBM.  The headline
 workload is BASELINE.json configs[2]: 16M x 1500 B packets on each GPU
 (configs[4] = 128M x 1500 B over 8 GPUs, i.e. weak scaling at 16M per GPU).
 The 64 B (configs[1]) and IMIX (configs[3]) batches are timed the same way and
-reported under "extra".
+reported as top-level value_64B / roofline_64B and value_imix / roofline_imix;
+BASELINE configs[0] (1M x 64 B through the reference's CPU loop) is
+cpu_baseline_cfg0.
 
     python bench.py --gpus N --steps K --warmup W
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
-Rank 0 prints one JSON line.  The cpu_baseline leg (rank 0) is the only part
-that touches oracle/: as the checker (parity of this run's first outputs,
-checker_leg) and, at N = 1, as the CPU baseline timing the reference's own
-subr.c checksum unit (oracle/_ref, when built) or the oracle restatement on a
-bounded sample of the same workload.  Host-resident burst rates of SURVEY
-§8(f) ranks 1-2 (tools/txburst, N = 1) are reported under extra.burst.
+Rank 0 prints one JSON line.  One process per GPU: WORLD_SIZE above the
+visible device count is refused unless --allow-shared-devices (rehearsals on
+a one-GPU box).  The checker leg is the only part that touches oracle/: every
+rank checks a sample of its own shard's outputs of this run against the
+oracle referee (the mismatch total is summed over ranks), and at N = 1 rank 0
+times the reference's own subr.c checksum unit (oracle/_ref, when built) or
+the oracle restatement on a bounded sample of the same workload as the CPU
+baseline.  Host-resident burst rates of SURVEY §8(f) ranks 1-2 (tools/txburst,
+N = 1) are summarised under extra.burst; the full rows go to
+gpurun_out/bench_burst.json.
 """
 import argparse
 import json
@@ -39,6 +45,18 @@ def shard_plan(rank, world, n_per_gpu):
     return {"first": rank * n_per_gpu, "n": n_per_gpu, "seed": SEED + rank, "world": world}
 
 
+def device_for(local_rank, world, ndev, allow_shared=False):
+    """One process per GPU: local rank r drives device r.  More ranks than
+    visible devices is refused (a line claiming N GPUs must run on N GPUs)
+    unless a rehearsal asks for shared devices."""
+    if ndev < 1:
+        raise SystemExit("bench.py: no GPU visible (an MI355X is required)")
+    if world > ndev and not allow_shared:
+        raise SystemExit(f"bench.py: WORLD_SIZE {world} > {ndev} visible GPUs "
+                         "(one rank per GPU; --allow-shared-devices for a rehearsal)")
+    return local_rank % ndev
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -52,6 +70,9 @@ def parse():
     ap.add_argument("--no-burst", action="store_true", help="skip the host-resident burst lines")
     ap.add_argument("--only", choices=["1500", "64", "imix", "rss"], default=None,
                     help="time one workload only (profiling runs)")
+    ap.add_argument("--allow-shared-devices", action="store_true",
+                    help="let ranks share GPUs when WORLD_SIZE exceeds the visible devices "
+                         "(rehearsals only: the line then says so)")
     return ap.parse_args()
 
 
@@ -79,6 +100,22 @@ class Dist:
         t = torch.tensor([float(x)], dtype=torch.float64)
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return float(t.item())
+
+    def sum(self, x):
+        if self.world == 1:
+            return x
+        import torch
+        t = torch.tensor([float(x)], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
+        return float(t.item())
+
+    def gather(self, obj):
+        """Every rank's `obj`, in rank order (on every rank)."""
+        if self.world == 1:
+            return [obj]
+        out = [None] * self.world
+        self.dist.all_gather_object(out, obj)
+        return out
 
     def close(self):
         if self.world > 1:
@@ -116,13 +153,14 @@ def bench_strided(torch, dist, eng, cgck, n, size, plan, steps, warmup):
         eng.strided(buf.ptr, n, size, 0, size, cgck.GEN_BOTH, out.ptr)
 
     wall, ev_ms = timed(torch, dist, eng, cgck, step, steps, warmup)
-    # spot parity of this very run (first/last packets) against the fixtures' generator
-    o = __import__("numpy").zeros(n, "uint32")
+    kernel = eng.last_kernel
+    # this run's first outputs, for the checker leg
+    o = __import__("numpy").zeros(min(n, 65536), "uint32")
     out.download(o, stream=eng.stream)
     eng.sync()
     buf.free()
     out.free()
-    return wall, ev_ms, o
+    return wall, ev_ms, o, kernel
 
 
 def bench_imix(torch, dist, eng, cgck, n, plan, steps, warmup):
@@ -138,11 +176,15 @@ def bench_imix(torch, dist, eng, cgck, n, plan, steps, warmup):
         eng.desc(buf.ptr, desc.ptr, n, cgck.GEN_BOTH, out.ptr)
 
     wall, ev_ms = timed(torch, dist, eng, cgck, step, steps, warmup)
+    kernel = eng.last_kernel
     eng.set_desc_len_hint(1500)
+    o = __import__("numpy").zeros(min(n, 65536), "uint32")
+    out.download(o, stream=eng.stream)
+    eng.sync()
     buf.free()
     desc.free()
     out.free()
-    return wall, ev_ms, nbytes
+    return wall, ev_ms, nbytes, o, kernel
 
 
 RSS_KEY = bytes.fromhex("6d5a56da255b0ec24167253d43a38fb0d0ca2bcbae7b30b477cb2da38030f20c6a42b73bbeac01fa")
@@ -165,6 +207,7 @@ def bench_rss(torch, dist, eng, cgck, plan, steps, warmup):
     wall_h, ev_h = timed(torch, dist, eng, cgck,
                          lambda: eng.toeplitz(d.ptr, n, 12, 12, RSS_KEY, o.ptr, mask=0x7F),
                          steps, warmup)
+    k_hash = eng.last_kernel
     # this run's first 4096 tuples and results, for the parity check of the checker leg
     host = np.zeros(4096 * 12, np.uint8)
     got = np.zeros(4096, np.uint32)
@@ -185,12 +228,14 @@ def bench_rss(torch, dist, eng, cgck, plan, steps, warmup):
     cap = tuples // qn * 2
     wall_d, ev_d = timed(torch, dist, eng, cgck, lambda: eng.dst_cache(prm, out.ptr, cap, cnt.ptr),
                          steps, warmup)
+    k_dst = eng.last_kernel
     c = np.zeros(1, np.uint32)
     cnt.download(c, stream=eng.stream)
     eng.sync()
     out.free()
     cnt.free()
-    return {"hash": (wall_h, ev_h, n), "hash_sample": (host, got), "dst": (wall_d, ev_d, tuples, int(c[0]))}
+    return {"hash": (wall_h, ev_h, n, k_hash), "hash_sample": (host, got),
+            "dst": (wall_d, ev_d, tuples, int(c[0]), k_dst)}
 
 
 BURSTS = (32, 256, 2048)   # receive / transmit burst sizes (netmap-like 2048 B slots)
@@ -199,34 +244,60 @@ BURSTS = (32, 256, 2048)   # receive / transmit burst sizes (netmap-like 2048 B 
 def bench_burst():
     """SURVEY §8(f) ranks 1 and 2 at the transport's burst granularity, through
     the C-ABI from C (tools/txburst.c): a BSD-verify cgck_desc_host per RX
-    burst, and the deferred TX window (per packet udp_cksum + in_cksum queued,
-    one cgck_tx_flush).  Host-resident, so PCIe/latency bound: never `value`."""
+    burst, the RX window (cgck_rx_begin + the stack's per-packet verify calls
+    + cgck_rx_end), and the deferred TX window on a registered ring.
+    Host-resident, so PCIe/latency bound: never `value`.  Returns all rows."""
     import subprocess
     exe = os.path.join(ROOT, "tools", "txburst")
     if not os.path.exists(exe):
         return None
-    r = subprocess.run([exe, "0.3"], capture_output=True, text=True, timeout=180)
+    r = subprocess.run([exe, "0.3"], capture_output=True, text=True, timeout=240)
     if r.returncode != 0:
         return {"error": r.stderr.strip()[-300:]}
     return [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
 
 
+BURST_COLS = ["pkt_len", "burst", "rx_window_reg_us", "rx_verify_reg_us", "tx_fill_reg_us", "cpu_ref_us"]
+
+
+def burst_summary(rows, cpu):
+    """At most 10 rows for the JSON line (columns BURST_COLS): per packet size
+    and burst, the RX window, the one-call RX verify and the TX window on a
+    registered ring, against the reference CPU loop over the same burst
+    (us per burst)."""
+    if not isinstance(rows, list):
+        return rows
+    by = {(r["mode"], r["pkt_len"], r["burst"]): r["us_median"] for r in rows}
+    cpu_by = {(r["pkt_len"], r["burst"]): round(r["us_per_burst"], 2) for r in (cpu or {}).get("rows", [])}
+    return [[ln, b, by.get(("rx_window_registered", ln, b)), by.get(("rx_verify_registered", ln, b)),
+             by.get(("tx_fill_registered", ln, b)), cpu_by.get((ln, b))]
+            for ln in (64, 1500) for b in (32, 256, 2048)]
+
+
 def checker_leg(res, plan, cgck):
-    """Parity of this run's outputs against the oracle (rank 0; the oracle is
-    only the checker here): the first 65536 1500 B packets (every 16th) and
-    the first 4096 hashed tuples."""
+    """Parity of this rank's outputs of this run against the oracle (the
+    oracle is only the checker here), on its own shard (seed 0xC0C0 + rank):
+    the first 65536 packets of each workload, every 16th, and the first 4096
+    hashed tuples.  Returns {workload: [checked, mismatches]}."""
     import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     P = oracle.port()
-    if "out_1500" in res:
-        o = res["out_1500"]
-        bad, chk = P.check_synth_strided(len(o), 1500, 1500, plan["seed"], cgck.GEN_BOTH, o, 16)
-        res["parity_1500"] = {"checked": chk, "mismatches": bad}
+    par = {}
+    for key, size in (("1500", 1500), ("64", 64)):
+        if key in res:
+            o = res[key]["out"]
+            bad, chk = P.check_synth_strided(len(o), size, size, plan["seed"], cgck.GEN_BOTH, o, 16)
+            par[key] = [chk, bad]
+    if "imix" in res:
+        o = res["imix"]["out"]
+        bad, chk = P.check_synth_imix(len(o), plan["seed"], cgck.GEN_BOTH, o, 16)
+        par["imix"] = [chk, bad]
     if "rss" in res:
         host, got = res["rss"]["hash_sample"]
         exp = P.toeplitz_batch(host, 4096, 12, 12, np.frombuffer(RSS_KEY, np.uint8), mask=0x7F)
-        res["parity_rss"] = {"checked": 4096, "mismatches": int(np.count_nonzero(got != exp))}
+        par["rss"] = [4096, int(np.count_nonzero(got != exp))]
+    return par
 
 
 def cpu_burst():
@@ -360,6 +431,10 @@ def cpu_baseline_64(seconds):
             "gbps": rate * 64 / 1e9}
 
 
+TRAFFIC_SOURCE = ("profiles/pmc_latest.json: FETCH_SIZE x 2 + WRITE_SIZE per launch from separate "
+                  "rocprofv3 --pmc passes of this bench (tools/gpu_prof.sh), not measured in this run")
+
+
 def load_traffic(key="1500"):
     """Per-launch HBM bytes of a workload's kernel from the committed PMC
     summary (profiles/pmc_latest.json, written by tools/pmc_traffic.py from
@@ -372,42 +447,52 @@ def load_traffic(key="1500"):
         return None
 
 
+def roofline(n, size, ev_ms, kernel, traffic_key, extra_bytes=0):
+    """HBM roofline of one workload's kernel: algorithmic bytes per launch
+    (n x (L + 4) [+ descriptors]) over its HIP-event time per launch."""
+    algo = n * (size + 4) + extra_bytes
+    ach = algo / (ev_ms * 1e-3)
+    return {"bound": "hbm", "achieved": ach / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+            "frac": ach / HBM_PEAK, "traffic": load_traffic(traffic_key), "kernel": kernel,
+            "algorithmic_bytes_per_launch": algo, "kernel_ms_hip_events": ev_ms}
+
+
 def main():
     args = parse()
     import torch   # first: the process then shares torch's HIP runtime
     dist = Dist()
-    # one rank per GPU; ranks past the visible devices share them, which only
-    # happens when N>1 is rehearsed on a one-GPU box
-    ndev = torch.cuda.device_count()
-    dev = dist.local % ndev if ndev else dist.local
+    # one rank per GPU (SURVEY §8(e)); a rehearsal on fewer GPUs must say so
+    dev = device_for(dist.local, dist.world, torch.cuda.device_count(), args.allow_shared_devices)
     torch.cuda.set_device(dev)
     import cgck
-    import numpy as np
     eng = cgck.Engine(dev)
     plan = shard_plan(dist.rank, dist.world, args.packets)
     n = plan["n"]
     res = {}
 
     if args.only in (None, "1500"):
-        wall, ev_ms, o = bench_strided(torch, dist, eng, cgck, n, 1500, plan, args.steps, args.warmup)
-        res["1500"] = (wall, ev_ms)
-        res["out_1500"] = o[:min(n, 65536)].copy()   # checked by the checker leg
+        wall, ev_ms, o, k = bench_strided(torch, dist, eng, cgck, n, 1500, plan, args.steps, args.warmup)
+        res["1500"] = {"wall": wall, "ev": ev_ms, "out": o, "kernel": k}
     if not args.no_extra and args.only in (None, "64"):
-        wall, ev_ms, _ = bench_strided(torch, dist, eng, cgck, n, 64, plan, args.steps, args.warmup)
-        res["64"] = (wall, ev_ms)
+        wall, ev_ms, o, k = bench_strided(torch, dist, eng, cgck, n, 64, plan, args.steps, args.warmup)
+        res["64"] = {"wall": wall, "ev": ev_ms, "out": o, "kernel": k}
     if not args.no_extra and args.only in (None, "imix"):
-        wall, ev_ms, nbytes = bench_imix(torch, dist, eng, cgck, n, plan, args.steps, args.warmup)
-        res["imix"] = (wall, ev_ms, nbytes)
-
+        wall, ev_ms, nbytes, o, k = bench_imix(torch, dist, eng, cgck, n, plan, args.steps, args.warmup)
+        res["imix"] = {"wall": wall, "ev": ev_ms, "bytes": nbytes, "out": o, "kernel": k}
     if not args.no_rss and args.only in (None, "rss"):
         res["rss"] = bench_rss(torch, dist, eng, cgck, plan, args.steps, args.warmup)
+
+    # every rank checks its own shard; the totals are summed over ranks
+    par = checker_leg(res, plan, cgck)
+    parity = {k: {"checked": int(dist.sum(v[0])), "mismatches": int(dist.sum(v[1])), "ranks": dist.world}
+              for k, v in sorted(par.items())}
+    devices = dist.gather({"rank": dist.rank, "local_rank": dist.local, "device": dev,
+                           "pci_bus": torch.cuda.get_device_properties(dev).pci_bus_id
+                           if hasattr(torch.cuda.get_device_properties(dev), "pci_bus_id") else None})
 
     burst = None
     if dist.rank == 0 and dist.world == 1 and not args.no_burst and args.only is None:
         burst = bench_burst()
-    if dist.rank == 0:
-        checker_leg(res, plan, cgck)
-
     cpu = cpu_r = cpu_64 = cpu_b = None
     if dist.rank == 0 and dist.world == 1 and not args.no_cpu:
         if burst:
@@ -422,83 +507,82 @@ def main():
     if dist.rank == 0:
         W = dist.world
         K = args.steps
-
-        def line(size, wall, ev_ms, extra_bytes=0):
-            pkts = n * W * K
-            gpkt = pkts / wall / 1e9
-            algo = n * (size + 4) + extra_bytes       # bytes per launch per GPU
-            ach = algo / (ev_ms * 1e-3)
-            return {"gpkt_s": gpkt, "gb_s": gpkt * size, "ms_per_step": wall / K * 1e3,
-                    "kernel_ms": ev_ms, "hbm_frac": ach / HBM_PEAK, "achieved_gbs": ach / 1e9}
-
+        shared = len({d["device"] for d in devices}) < W
         out = {"metric": METRIC, "unit": "Gpkt/s", "n_gpus": W, "steps": K, "warmup": args.warmup,
                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u16",
                "data": "synthetic (device-generated splitmix64 IPv4+TCP packets, SURVEY §8(d))"}
+        if shared:
+            out["shared_devices"] = "REHEARSAL: ranks share GPUs; not an N-GPU measurement"
         if "1500" in res:
-            wall, ev_ms = res["1500"]
-            L = line(1500, wall, ev_ms)
-            algo = n * 1504
-            traffic = load_traffic()
+            r = res["1500"]
+            gpkt = n * W * K / r["wall"] / 1e9
             out.update({
-                "value": L["gpkt_s"], "ms_per_step": L["ms_per_step"],
+                "value": gpkt, "ms_per_step": r["wall"] / K * 1e3,
                 "config": {"workload": f"{n} x 1500 B IPv4+TCP per GPU, dense stride 1500, "
                                        "ip_cksum + tcp_cksum per packet (BASELINE configs[2]; "
                                        "configs[4] at 8 GPUs)",
                            "packets_per_gpu": n, "packet_bytes": 1500, "parallelism": f"batch-split x{W}",
-                           "gb_s": L["gb_s"]},
-                "roofline": {"bound": "hbm", "achieved": L["achieved_gbs"], "peak": HBM_PEAK / 1e9,
-                             "unit": "GB/s", "frac": L["hbm_frac"],
-                             "traffic": traffic,
-                             "kernel": "cksum_kernel<16, 6, 1, false, true>",
-                             "algorithmic_bytes_per_launch": algo,
-                             "kernel_ms_hip_events": ev_ms},
-                "parity": res.get("parity_1500"),
+                           "gb_s": gpkt * 1500, "devices": [d["device"] for d in devices]},
+                "roofline": roofline(n, 1500, r["ev"], r["kernel"], "1500"),
             })
-        extra = {}
+            out["roofline"]["traffic_source"] = TRAFFIC_SOURCE
         if "64" in res:
-            extra["64B"] = line(64, *res["64"])
-            extra["64B"].update({"kernel": "lpa_kernel<false, 4>", "traffic": load_traffic("64")})
-            if cpu_64:
-                extra["64B"]["cpu_baseline"] = cpu_64
+            r = res["64"]
+            gpkt = n * W * K / r["wall"] / 1e9
+            out.update({"value_64B": gpkt, "gb_s_64B": gpkt * 64, "ms_per_step_64B": r["wall"] / K * 1e3,
+                        "config_64B": f"{n} x 64 B IPv4+TCP per GPU, dense stride 64 (BASELINE configs[1])",
+                        "roofline_64B": roofline(n, 64, r["ev"], r["kernel"], "64")})
         if "imix" in res:
-            wall, ev_ms, nbytes = res["imix"]
-            extra["imix"] = line(0, wall, ev_ms, nbytes + 16 * n)
-            extra["imix"]["gb_s"] = nbytes * W * K / wall / 1e9
-            extra["imix"].update({"kernel": "slot2_kernel<true, false>", "traffic": load_traffic("imix")})
+            r = res["imix"]
+            gpkt = n * W * K / r["wall"] / 1e9
+            out.update({"value_imix": gpkt, "gb_s_imix": r["bytes"] * W * K / r["wall"] / 1e9,
+                        "ms_per_step_imix": r["wall"] / K * 1e3,
+                        "config_imix": f"{n} IMIX packets per GPU (64/576/1500 at 7:4:1, 12-byte "
+                                       "descriptors; BASELINE configs[3])",
+                        "roofline_imix": roofline(n, 0, r["ev"], r["kernel"], "imix", r["bytes"] + 16 * n)})
+        out["parity"] = parity
+        if cpu:
+            out["cpu_baseline"] = cpu
+        if cpu_64:
+            out["cpu_baseline_cfg0"] = cpu_64
+        extra = {}
         if "rss" in res:
-            wall_h, ev_h, nt = res["rss"]["hash"]
-            wall_d, ev_d, td, written = res["rss"]["dst"]
+            wall_h, ev_h, nt, k_hash = res["rss"]["hash"]
+            wall_d, ev_d, td, written, k_dst = res["rss"]["dst"]
             ach = nt * 16 / (ev_h * 1e-3)
             extra["rss_hash"] = {
-                "workload": f"{nt} dense 12-byte tuples per GPU, rss_hash4 (Toeplitz, 40-byte key, "
-                            "mask 0x7F) each", "kernel": "toeplitz12x4_ab_kernel<12>",
-                "gtuple_s": nt * W * K / wall_h / 1e9, "ms_per_step": wall_h / K * 1e3,
-                "kernel_ms": ev_h, "achieved_gbs": ach / 1e9, "hbm_frac": ach / HBM_PEAK,
-                "algorithmic_bytes_per_launch": nt * 16, "traffic": load_traffic("rss_hash"),
-                "parity": res.get("parity_rss")}
+                "workload": f"{nt} dense 12-byte tuples per GPU, rss_hash4 (mask 0x7F)", "kernel": k_hash,
+                "gtuple_s": nt * W * K / wall_h / 1e9, "kernel_ms": ev_h, "achieved_gbs": ach / 1e9,
+                "hbm_frac": ach / HBM_PEAK, "algorithmic_bytes_per_launch": nt * 16,
+                "traffic": load_traffic("rss_hash")}
             extra["dst_cache"] = {
-                "workload": f"thread_init_dst_cache enumeration of {td} tuples per GPU "
-                            f"({RSS_DST[0]} laddrs x {RSS_DST[1]} faddrs x 60536 ports), "
-                            f"{RSS_DST[2]} RSS queues, no early cap", "kernel": "dst_cache_kernel<true>",
-                "gtuple_s": td * W * K / wall_d / 1e9, "ms_per_step": wall_d / K * 1e3,
-                "kernel_ms": ev_d, "entries_written": written}
+                "workload": f"thread_init_dst_cache over {td} tuples per GPU ({RSS_DST[0]} laddrs x "
+                            f"{RSS_DST[1]} faddrs x 60536 ports, {RSS_DST[2]} queues)", "kernel": k_dst,
+                "gtuple_s": td * W * K / wall_d / 1e9, "kernel_ms": ev_d, "entries_written": written}
             if cpu_r:
                 extra["dst_cache"]["cpu_baseline"] = cpu_r
         if burst:
-            extra["burst"] = {"what": "SURVEY §8(f) rank 1 (rx_verify: cgck_desc_host, BSD verify flags, "
-                                      "per RX burst) and rank 2 (tx_fill: cgck_tx_begin, per packet "
-                                      "udp_cksum + in_cksum, cgck_tx_flush) on host-resident 2048 B ring "
-                                      "slots, called from C (tools/txburst.c)", "rows": burst}
-            if cpu_b:
-                extra["burst"]["cpu_baseline"] = cpu_b
+            path = os.path.join(ROOT, "gpurun_out", "bench_burst.json")
+            try:
+                os.makedirs(os.path.dirname(path), exist_ok=True)
+                with open(path, "w") as f:
+                    json.dump({"rows": burst, "cpu_baseline": cpu_b}, f, indent=0)
+            except OSError:
+                path = None
+            extra["burst"] = {"what": "us per burst, 2048 B ring slots registered with cgck_host_register, "
+                                      "from C (tools/txburst.c): RX window, one-call RX verify, TX window; "
+                                      "cpu_ref = the reference in_cksum+udp_cksum per packet, 1 core",
+                              "cols": BURST_COLS, "rows": burst_summary(burst, cpu_b),
+                              "all_rows": path and "gpurun_out/bench_burst.json"}
         if extra:
             out["extra"] = extra
         if "value" not in out:   # --only 64 / imix / rss profiling runs
-            k = "64B" if "64B" in extra else "imix" if "imix" in extra else "rss_hash"
-            out["value"] = extra[k]["gpkt_s"]
-            out["config"] = {"workload": k}
-        if cpu:
-            out["cpu_baseline"] = cpu
+            if "value_64B" in out:
+                out["value"], out["config"] = out["value_64B"], {"workload": "64B"}
+            elif "value_imix" in out:
+                out["value"], out["config"] = out["value_imix"], {"workload": "imix"}
+            else:
+                out["value"], out["config"] = extra["rss_hash"]["gtuple_s"], {"workload": "rss_hash"}
         print(json.dumps(out), flush=True)
     eng.close()
     dist.close()

@@ -122,6 +122,8 @@ struct ThreadState {
 	// TX window
 	bool tx_open = false;
 	std::vector<TxEntry> txq;
+	const uint8_t *tx_max = nullptr; // highest header address queued so far
+	bool tx_map = false;             // txidx built (the first call below tx_max)
 	PtrMap txidx; // (ip << 1 | is_l4) -> txq index
 	// RX window
 	bool rx_open = false;
@@ -135,7 +137,20 @@ struct ThreadState {
 	uint64_t stats[4] = {0, 0, 0, 0};
 };
 
-thread_local ThreadState t_state;
+// The drop-ins read this on every call, so it is a plain pointer in the
+// initial-exec TLS model (one fs-relative load; a thread_local object with a
+// constructor costs a TLS wrapper call and an init guard per access).  The
+// state itself is allocated on the thread's first use and lives as long as
+// the thread's context does not need it any more (cgck_thread_release keeps
+// it for the counters).
+__attribute__((tls_model("initial-exec"))) thread_local ThreadState *t_st = nullptr;
+
+ThreadState &tstate()
+{
+	if (__builtin_expect(!t_st, 0))
+		t_st = new ThreadState;
+	return *t_st;
+}
 
 uint32_t sync_region(const void *src, uint32_t span, uint32_t ip_len, uint32_t flags)
 {
@@ -185,16 +200,42 @@ bool rx_find(ThreadState &t, const uint8_t *p, uint32_t *v)
 	return true;
 }
 
+// Queue one field; a header or segment queued again replaces its entry (the
+// later call wins).  The transport hands out ring slots in address order, so
+// while every call is at or above the highest header queued so far a
+// duplicate can only be one of the last entries; the first call below it
+// (ring wrap, a slot handed out again) switches to a map of every entry.
 void tx_queue(ThreadState &t, uint8_t *ip, uint32_t span, uint16_t hl, int16_t fo)
 {
+	const TxEntry e = {ip, span, hl, fo};
+	if (!t.tx_map) {
+		if (ip > t.tx_max) {
+			t.tx_max = ip;
+			t.txq.push_back(e);
+			return;
+		}
+		if (ip == t.tx_max) {
+			for (size_t i = t.txq.size(); i-- > 0 && t.txq[i].ip == ip;)
+				if ((t.txq[i].fo < 0) == (fo < 0)) {
+					t.txq[i] = e;
+					return;
+				}
+			t.txq.push_back(e);
+			return;
+		}
+		t.txidx.reset(2 * t.txq.size() + 64);
+		for (size_t i = 0; i < t.txq.size(); i++)
+			t.txidx.put(((uintptr_t)t.txq[i].ip << 1) | (t.txq[i].fo >= 0 ? 1u : 0u), (uint32_t)i);
+		t.tx_map = true;
+	}
 	const uintptr_t k = ((uintptr_t)ip << 1) | (fo >= 0 ? 1u : 0u);
 	uint32_t i;
-	if (t.txidx.get(k, &i)) { // the same header / segment again: the later call wins
-		t.txq[i] = {ip, span, hl, fo};
+	if (t.txidx.get(k, &i)) {
+		t.txq[i] = e;
 		return;
 	}
 	t.txidx.put(k, (uint32_t)t.txq.size());
-	t.txq.push_back({ip, span, hl, fo});
+	t.txq.push_back(e);
 }
 
 } // namespace
@@ -205,18 +246,19 @@ void tx_queue(ThreadState &t, uint8_t *ip, uint32_t span, uint16_t hl, int16_t f
 
 cgck_ctx *cgck::thread_ctx()
 {
-	if (!t_state.ctx) {
+	ThreadState &t = tstate();
+	if (!t.ctx) {
 		const char *e = getenv("CGCK_DEVICE");
 		const int dev = e ? atoi(e) : 0;
 		cgck_ctx *c = nullptr;
 		if (cgck_ctx_create(dev, &c) != 0)
 			return nullptr;
-		t_state.ctx = c;
+		t.ctx = c;
 	}
-	return t_state.ctx;
+	return t.ctx;
 }
 
-cgck_ctx *cgck::thread_ctx_if_any() { return t_state.ctx; }
+cgck_ctx *cgck::thread_ctx_if_any() { return t_st ? t_st->ctx : nullptr; }
 
 [[noreturn]] void cgck::die(const char *what)
 {
@@ -238,7 +280,7 @@ extern "C" cgck_ctx_t *cgck_thread_ctx(void) { return thread_ctx(); }
 
 extern "C" int cgck_thread_release(void)
 {
-	ThreadState &t = t_state;
+	ThreadState &t = tstate();
 	t.txq.clear();
 	t.tx_open = false;
 	t.rx.clear();
@@ -254,7 +296,7 @@ extern "C" int cgck_window_stats(uint64_t stats[4])
 {
 	if (!stats)
 		return set_err(-EINVAL, "cgck_window_stats: NULL");
-	memcpy(stats, t_state.stats, sizeof(t_state.stats));
+	memcpy(stats, tstate().stats, sizeof(tstate().stats));
 	return 0;
 }
 
@@ -270,7 +312,7 @@ extern "C" uint16_t in_cksum(void *data, int len)
 		set_err(-EINVAL, "in_cksum: negative length %d", len);
 		die("in_cksum");
 	}
-	ThreadState &t = t_state;
+	ThreadState &t = tstate();
 	const uint8_t *b = (const uint8_t *)data;
 	if (t.rx_open) {
 		// ip_cksum(ip) at ip_input.c:51 / inet.c:322, or the ICMP message at
@@ -308,7 +350,7 @@ extern "C" uint16_t udp_cksum(struct ip *ipp, int len)
 		set_err(-EINVAL, "udp_cksum: negative length %d", len);
 		die("udp_cksum");
 	}
-	ThreadState &t = t_state;
+	ThreadState &t = tstate();
 	const uint32_t hl = (ip[0] & 15) * 4;
 	const uint32_t ip_len = hl + (uint32_t)len;
 	if (t.rx_open) {
@@ -348,7 +390,7 @@ extern "C" uint16_t udp_cksum(struct ip *ipp, int len)
 
 extern "C" int cgck_rx_begin(void *base, size_t bytes, const cgck_desc_t *desc, uint64_t n)
 {
-	ThreadState &t = t_state;
+	ThreadState &t = tstate();
 	if (t.rx_open)
 		return set_err(-EBUSY, "cgck_rx_begin: an RX window is already open on this thread");
 	if (n && (!base || !desc))
@@ -416,7 +458,7 @@ extern "C" int cgck_rx_begin(void *base, size_t bytes, const cgck_desc_t *desc, 
 
 extern "C" int cgck_rx_end(void)
 {
-	ThreadState &t = t_state;
+	ThreadState &t = tstate();
 	if (!t.rx_open)
 		return set_err(-EINVAL, "cgck_rx_end: no open RX window on this thread");
 	t.rx_open = false;
@@ -431,24 +473,24 @@ extern "C" int cgck_rx_end(void)
 
 extern "C" int cgck_tx_begin(void)
 {
-	ThreadState &t = t_state;
+	ThreadState &t = tstate();
 	if (t.tx_open)
 		return set_err(-EBUSY, "cgck_tx_begin: window already open on this thread");
 	t.tx_open = true;
 	t.txq.clear();
-	t.txidx.reset(256);
+	t.tx_max = nullptr;
+	t.tx_map = false;
 	return 0;
 }
 
 extern "C" int cgck_tx_flush(void)
 {
-	ThreadState &t = t_state;
+	ThreadState &t = tstate();
 	if (!t.tx_open)
 		return set_err(-EINVAL, "cgck_tx_flush: no open window on this thread");
 	t.tx_open = false;
-	std::vector<TxEntry> q;
-	q.swap(t.txq);
-	t.txidx.reset(0);
+	std::vector<TxEntry> &q = t.txq; // stays queued until the flush is done
+	t.tx_map = false;
 	const uint64_t n = q.size();
 	if (n == 0)
 		return 0;
@@ -510,6 +552,7 @@ extern "C" int cgck_tx_flush(void)
 		}
 		memcpy(dst, &v, 2);
 	}
+	q.clear();
 	return (int)n;
 }
 

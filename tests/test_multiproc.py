@@ -48,6 +48,58 @@ def test_two_rank_shard_plan_and_max():
     assert m0 == m1 == 1.0                               # max over ranks
 
 
+def _worker4(rank, world, port, q):
+    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port),
+                       "RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank)})
+    d = bench.Dist()
+    plan = bench.shard_plan(d.rank, d.world, 4096)
+    tot = d.sum(rank + 1)                   # per-rank parity counts are summed
+    devs = d.gather({"rank": rank, "device": rank})
+    q.put((rank, plan, tot, devs))
+    d.close()
+
+
+def test_four_rank_plan_covers_batch_disjointly():
+    """configs[4] at 4 ranks: the shards tile [0, 4n) exactly once, each rank
+    has its own seed, the checker's totals are summed and every rank's device
+    id is gathered (the line records them)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker4, args=(r, 4, port, q)) for r in range(4)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=120) for _ in procs), key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    covered = []
+    for rank, plan, tot, devs in res:
+        covered.extend(range(plan["first"], plan["first"] + plan["n"]))
+        assert tot == 1 + 2 + 3 + 4
+        assert [d["device"] for d in devs] == [0, 1, 2, 3]
+    assert sorted(covered) == list(range(4 * 4096))
+    assert len({plan["seed"] for _, plan, _, _ in res}) == 4
+
+
+def test_device_for_refuses_oversubscription():
+    assert [bench.device_for(r, 8, 8) for r in range(8)] == list(range(8))
+    with pytest.raises(SystemExit, match="WORLD_SIZE 2 > 1 visible GPUs"):
+        bench.device_for(1, 2, 1)
+    assert bench.device_for(1, 2, 1, allow_shared=True) == 0
+    with pytest.raises(SystemExit, match="no GPU visible"):
+        bench.device_for(0, 1, 0)
+
+
+def test_burst_summary_is_compact():
+    rows = [{"mode": m, "pkt_len": ln, "burst": b, "us_median": 1.0}
+            for m in ("rx_window_registered", "rx_verify_registered", "tx_fill_registered", "rx_verify")
+            for ln in (64, 1500) for b in (32, 256, 2048)]
+    cpu = {"rows": [{"pkt_len": ln, "burst": b, "us_per_burst": 2.0} for ln in (64, 1500) for b in (32, 256, 2048)]}
+    s = bench.burst_summary(rows, cpu)
+    assert len(s) <= 10 and all(len(r) == len(bench.BURST_COLS) and r[-1] == 2.0 and r[2] == 1.0 for r in s)
+
+
 def test_single_rank_is_noop():
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
         os.environ.pop(k, None)

@@ -15,6 +15,6 @@ cp $G/prof_trace/run_kernel_trace.csv $D/rocprof/kernel_trace.csv
 grep '^{"metric"' $G/prof_trace.log | tail -n 1 > $D/rocprof/bench_under_trace.json
 cp $G/prof_fetch/run_counter_collection.csv $D/rocprof/pmc_fetch_size.csv
 cp $G/prof_write/run_counter_collection.csv $D/rocprof/pmc_write_size.csv
-python3 tools/pmc_traffic.py $G/prof_fetch $G/prof_write profiles/pmc_latest.json > /dev/null
+python3 tools/pmc_traffic.py $G/prof_fetch $G/prof_write profiles/pmc_latest.json $D/rocprof/bench_under_trace.json > /dev/null
 python3 tools/prof_check.py $D/rocprof/kernel_stats.csv $D/rocprof/bench_under_trace.json > $D/rocprof/kernel_vs_events.txt || true
 echo "collected into $D"

@@ -5,7 +5,10 @@ MI355X_MICROARCH.md's HBM section prescribes: FETCH_SIZE (KB) reads exactly
 half the bytes of a wide coalesced streaming read on gfx950, so it is
 doubled; WRITE_SIZE (KB) is exact for 16-B/lane streaming stores.
 
-    python tools/pmc_traffic.py gpurun_out/prof_fetch gpurun_out/prof_write OUT.json
+    python tools/pmc_traffic.py gpurun_out/prof_fetch gpurun_out/prof_write OUT.json [BENCH.json]
+
+With BENCH.json (a bench.py line) the kernel of each workload is the one the
+dispatcher reported in that run (roofline*.kernel, extra.*.kernel).
 """
 import csv
 import json
@@ -36,11 +39,27 @@ def per_kernel(path, counter):
     return out
 
 
+def kernels_from_bench(path):
+    b = json.loads(open(path).read().strip().splitlines()[-1])
+    k = dict(KERNELS)
+    for key, field in (("1500", "roofline"), ("64", "roofline_64B"), ("imix", "roofline_imix")):
+        if field in b and b[field].get("kernel"):
+            k[key] = b[field]["kernel"]
+    for key in ("rss_hash", "dst_cache"):
+        v = b.get("extra", {}).get(key, {})
+        if v.get("kernel"):
+            k[key] = v["kernel"]
+    return k
+
+
 def main():
+    global KERNELS
+    if len(sys.argv) > 4:
+        KERNELS = kernels_from_bench(sys.argv[4])
     fetch = per_kernel(sys.argv[1], "FETCH_SIZE")
     write = per_kernel(sys.argv[2], "WRITE_SIZE")
     res = {"method": "median per dispatch; bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024",
-           "source": [sys.argv[1], sys.argv[2]]}
+           "source": [sys.argv[1], sys.argv[2]], "kernels": KERNELS}
     for key, frag in KERNELS.items():
         f = [v for k, v in fetch.items() if frag in k]
         w = [v for k, v in write.items() if frag in k]

@@ -12,7 +12,10 @@ import sys
 def main():
     stats = {r["Name"]: float(r["AverageNs"]) / 1e6 for r in csv.DictReader(open(sys.argv[1]))}
     b = json.loads(open(sys.argv[2]).read())
-    rows = [("1500", b["roofline"]["kernel"], b["roofline"]["kernel_ms_hip_events"])]
+    rows = []
+    for key, field in (("1500", "roofline"), ("64B", "roofline_64B"), ("imix", "roofline_imix")):
+        if field in b:
+            rows.append((key, b[field]["kernel"], b[field]["kernel_ms_hip_events"]))
     for k, v in b.get("extra", {}).items():
         if "kernel" in v and "kernel_ms" in v:
             rows.append((k, v["kernel"], v["kernel_ms"]))
