@@ -301,6 +301,9 @@ hipError_t launch_group(const KParams &p, uint32_t max_len, int num_cus, bool nt
 	if (max_len <= 256)
 		return d ? launch_t<16, 2, 2, true>(p, max_blocks, nt, st)
 			 : launch_t<16, 2, 2, false>(p, max_blocks, nt, st);
+	if (max_len <= 768) // 576 B (IMIX's middle class): 48 chunks per group, two packets per group step
+		return d ? launch_t<16, 3, 2, true>(p, max_blocks, nt, st)
+			 : launch_t<16, 3, 2, false>(p, max_blocks, nt, st);
 	if (max_len <= 1600)
 		return d ? launch_t<16, 6, 1, true>(p, max_blocks, nt, st)
 			 : launch_t<16, 6, 1, false>(p, max_blocks, nt, st);

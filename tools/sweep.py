@@ -43,24 +43,41 @@ def main():
     e_probe = cgck.Engine(0)   # default family: probe variant 0 (plain streaming read)
     e0 = next(iter(engines.values()))
     work = {}
+    nmax = n
     for w in args.workloads.split(","):
-        if w == "imix":
+        if w.startswith("d"):
+            # dense descriptor batch of one length: "d576" or "d576:NPACKETS"
+            L, _, cnt = w[1:].partition(":")
+            L, m = int(L), int(cnt) if cnt else n
+            buf = cgck.DeviceBuffer(m * L)
+            e0.synth_strided(buf.ptr, m, L, L, 0xC0C0)
+            import numpy as np
+            dh = np.zeros(m, cgck.DESC_DTYPE)
+            dh["frame_off"] = np.arange(m, dtype=np.uint64) * L
+            dh["ip_len"] = L
+            desc = cgck.DeviceBuffer(12 * m)
+            desc.upload(dh, stream=e0.stream)
+            e0.sync()
+            nmax = max(nmax, m)
+            work[w] = (lambda e, f, o, buf=buf, desc=desc, m=m, L=L: (e.set_desc_len_hint(L),
+                                                                       e.desc(buf.ptr, desc.ptr, m, f, o)),
+                       m * (L + 12) + (4 * m if "out" in out_list else 0), [buf, desc])
+        elif w == "imix":
             nbytes = cgck.load().cgck_imix_bytes(n)
             buf = cgck.DeviceBuffer(nbytes)
             desc = cgck.DeviceBuffer(12 * n)
             e0.synth_imix(buf.ptr, desc.ptr, n, 0xC0C0)
             algo = nbytes + 12 * n + (4 * n if "out" in out_list else 0)
-            for e in engines.values():
-                e.set_desc_len_hint(nbytes // n)
-            work[w] = (lambda e, f, o, buf=buf, desc=desc: e.desc(buf.ptr, desc.ptr, n, f, o), algo,
-                       [buf, desc])
+            work[w] = (lambda e, f, o, buf=buf, desc=desc, h=nbytes // n: (e.set_desc_len_hint(h),
+                                                                            e.desc(buf.ptr, desc.ptr, n, f, o)),
+                       algo, [buf, desc])
         else:
             L = int(w)
             buf = cgck.DeviceBuffer(n * L)
             e0.synth_strided(buf.ptr, n, L, L, 0xC0C0)
             work[w] = (lambda e, f, o, buf=buf, L=L: e.strided(buf.ptr, n, L, 0, L, f, o),
                        n * L + (4 * n if "out" in out_list else 0), [buf])
-    out = cgck.DeviceBuffer(4 * n)
+    out = cgck.DeviceBuffer(4 * nmax)
     # streaming-read ceiling on the 1500 B buffer (or the first one)
     pb = work.get("1500", next(iter(work.values())))[2][0]
     sink = cgck.DeviceBuffer(4)
@@ -94,7 +111,7 @@ def main():
         med, best = statistics.median(xs), max(xs)
         table[f"{w}/{v}"] = {"median_GBs": med / 1e9, "best_GBs": best / 1e9,
                              "median_frac": med / HBM}
-        print(f"{w:>5} {v:>22}: median {med / 1e9:8.1f} GB/s ({med / HBM:6.1%})  best {best / 1e9:8.1f}",
+        print(f"{w:>12} {v:>22}: median {med / 1e9:8.1f} GB/s ({med / HBM:6.1%})  best {best / 1e9:8.1f}",
               flush=True)
     print(json.dumps(table))
 
