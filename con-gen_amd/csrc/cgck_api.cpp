@@ -118,6 +118,7 @@ extern "C" int cgck_ctx_create(int device, cgck_ctx_t **out)
 	if (const char *kf = getenv("CGCK_KERNEL"))
 		c->family = !strcmp(kf, "group") ? 1 : !strcmp(kf, "lpp") ? 2 : !strcmp(kf, "slot") ? 3
 			  : !strcmp(kf, "slot2") ? 9 : !strcmp(kf, "lpa") ? 10 : !strcmp(kf, "str") ? 11
+			  : !strcmp(kf, "span") ? 12
 			  : !strncmp(kf, "lpp", 3) ? atoi(kf + 3) : atoi(kf);
 	hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
 	if (e != hipSuccess) {
@@ -184,6 +185,16 @@ extern "C" int cgck_set_desc_len_hint(cgck_ctx_t *c, uint32_t max_ip_len)
 	return 0;
 }
 
+extern "C" int cgck_set_desc_layout(cgck_ctx_t *c, uint32_t layout)
+{
+	if (!c)
+		return set_err(-EINVAL, "cgck_set_desc_layout: NULL context");
+	if (layout > CGCK_LAYOUT_PACKED)
+		return set_err(-EINVAL, "cgck_set_desc_layout: unknown layout %u", layout);
+	c->desc_layout = layout;
+	return 0;
+}
+
 static inline hipStream_t pick(cgck_ctx *c, void *stream)
 {
 	return stream ? (hipStream_t)stream : c->stream;
@@ -211,7 +222,7 @@ int cgck::run(cgck_ctx *c, const KParams &p0, uint32_t len_hint, hipStream_t st)
 	HIP_TRY(hipSetDevice(c->device));
 	KParams p = p0;
 	p.zero = c->d_zero;
-	hipError_t e = launch_cksum(p, len_hint, c->num_cus, c->family, st);
+	hipError_t e = launch_cksum(p, len_hint, c->num_cus, c->family | (c->desc_layout ? kPacked : 0), st);
 	if (e != hipSuccess)
 		return set_err(-EIO, "cksum launch: %s", hipGetErrorString(e));
 	if (p.n)

@@ -14,6 +14,7 @@ struct cgck_ctx {
 	int num_cus;
 	hipStream_t stream;
 	uint32_t desc_len_hint;
+	uint32_t desc_layout; // CGCK_LAYOUT_*
 	int family; // kernel family: 0 auto, 1 group, 2 lane-per-packet ($CGCK_KERNEL)
 	const char *last_kernel; // cgck_ctx_last_kernel
 	// pinned host staging (drop-in calls, deferred TX)

@@ -66,6 +66,7 @@ hipError_t launch_burst_server(BurstBox *box, const void *zero, hipStream_t st);
 // (1500 B: 5.79 -> 6.18 TB/s); the lane kernels re-touch each line from
 // several instructions, so they want cached loads (NT: -30..-50 %).
 constexpr int kNT = 16, kContig = 32, kExplicit = 64;
+constexpr int kPacked = 128; // the context's descriptor layout hint is CGCK_LAYOUT_PACKED
 constexpr uint32_t kGroupFromLen = 1024; // typical length from which the group kernel is used
 constexpr uint32_t kLppUpToLen = 128;    // lane-per-packet up to here, lane-per-slot above
 constexpr int kDefaultLppShape = 2;       // see launch_lpp (6 chunks up front, predicated: best on 64 B)

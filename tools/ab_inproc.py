@@ -49,12 +49,15 @@ def main():
     work = {}
     keep = []
     for w in args.workloads.split(","):
-        if w == "imix":
+        if w in ("imix", "imixp"):
+            # imixp: the packed layout hint on both contexts (span kernel)
             nbytes = cgck.load().cgck_imix_bytes(n)
             buf, desc = cgck.DeviceBuffer(nbytes), cgck.DeviceBuffer(12 * n)
             e0.synth_imix(buf.ptr, desc.ptr, n, 0xC0C0)
             for L, c in zip(libs, ctxs):
                 L.cgck_set_desc_len_hint(c, nbytes // n)
+                if w == "imixp":
+                    L.cgck_set_desc_layout(c, cgck.LAYOUT_PACKED)
             work[w] = (lambda L, c, buf=buf, desc=desc: L.cgck_desc(c, buf.ptr, desc.ptr, n, cgck.GEN_BOTH,
                                                                      out.ptr, None, None, None),
                        nbytes + 16 * n)

@@ -1,6 +1,6 @@
 #!/bin/sh
-# Build a variant of libcgck.so for A/B runs into con-gen_amd/<name>.so
-# (git-ignored).  Host side only.
+# Build a variant of the lab library (every csrc source, -DCGCK_LAB) for A/B
+# runs into con-gen_amd/<name>.so (git-ignored).  Host side only.
 #   tools/build_variant.sh NAME FILE 'SED-EXPR'   working tree + one sed edit
 #   tools/build_variant.sh NAME --rev REV         the sources of git revision REV
 set -eu
@@ -19,8 +19,7 @@ else
 fi
 cd "$T/con-gen_amd"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -Wall -Werror -mcode-object-version=5 \
-	-I"$T/include" -shared -o "$R/con-gen_amd/$NAME.so" \
-	csrc/cgck_group.hip csrc/cgck_lane.hip csrc/cgck_stream.hip csrc/cgck_synth.hip csrc/cgck_rss.hip \
-	csrc/cgck_dispatch.cpp csrc/cgck_api.cpp
+	-I"$T/include" -DCGCK_LAB=1 ${VARIANT_FLAGS:-} -shared -o "$R/con-gen_amd/$NAME.so" \
+	csrc/*.hip csrc/*.cpp
 rm -rf "$T"
 echo "built con-gen_amd/$NAME.so"

@@ -62,15 +62,19 @@ def main():
             work[w] = (lambda e, f, o, buf=buf, desc=desc, m=m, L=L: (e.set_desc_len_hint(L),
                                                                        e.desc(buf.ptr, desc.ptr, m, f, o)),
                        m * (L + 12) + (4 * m if "out" in out_list else 0), [buf, desc])
-        elif w == "imix":
+        elif w in ("imix", "imixp"):
+            # imixp: the SAME batch (same allocation: a different one can land
+            # in another HBM state) with the packed layout hint
             nbytes = cgck.load().cgck_imix_bytes(n)
-            buf = cgck.DeviceBuffer(nbytes)
-            desc = cgck.DeviceBuffer(12 * n)
-            e0.synth_imix(buf.ptr, desc.ptr, n, 0xC0C0)
+            if "imix_bufs" not in locals():
+                imix_bufs = (cgck.DeviceBuffer(nbytes), cgck.DeviceBuffer(12 * n))
+                e0.synth_imix(imix_bufs[0].ptr, imix_bufs[1].ptr, n, 0xC0C0)
+            buf, desc = imix_bufs
             algo = nbytes + 12 * n + (4 * n if "out" in out_list else 0)
-            work[w] = (lambda e, f, o, buf=buf, desc=desc, h=nbytes // n: (e.set_desc_len_hint(h),
-                                                                            e.desc(buf.ptr, desc.ptr, n, f, o)),
-                       algo, [buf, desc])
+            lay = cgck.LAYOUT_PACKED if w == "imixp" else cgck.LAYOUT_ANY
+            work[w] = (lambda e, f, o, buf=buf, desc=desc, h=nbytes // n, lay=lay: (
+                e.set_desc_len_hint(h), e.set_desc_layout(lay), e.desc(buf.ptr, desc.ptr, n, f, o),
+                e.set_desc_layout(cgck.LAYOUT_ANY)), algo, [buf, desc])
         else:
             L = int(w)
             buf = cgck.DeviceBuffer(n * L)
