@@ -39,9 +39,9 @@ hipError_t launch_group(const KParams &p, uint32_t max_len, int num_cus, bool nt
 hipError_t launch_lpp(const KParams &p, int num_cus, bool nt, int shape, hipStream_t st);
 hipError_t launch_slot2(const KParams &p, int num_cus, bool nt, hipStream_t st);
 hipError_t launch_lpa(const KParams &p, int num_cus, bool nt, hipStream_t st);
+#if CGCK_LAB
 hipError_t launch_span(const KParams &p, int num_cus, bool nt, hipStream_t st);
 bool span_ok(const KParams &p);
-#if CGCK_LAB
 hipError_t launch_slot(const KParams &p, int num_cus, bool nt, hipStream_t st);
 hipError_t launch_lppp(const KParams &p, int num_cus, bool nt, hipStream_t st);
 hipError_t launch_stream(const KParams &p, int num_cus, hipStream_t st);
@@ -54,16 +54,16 @@ bool stream_ok(const KParams &p);
 //     packet (lpp), 9 lane per 128-byte slot pipelined two deep (slot2, the
 //     default for mid-size packets), 10 lane per packet for aligned
 //     fixed-length strided 20..64-byte packets, A/B pipelined (lpa, the
-//     default there), 12 packed span (descriptor batches whose frames lie
-//     back to back: coalesced stream + prefix sums, cgck_span.hip; the
-//     default under CGCK_LAYOUT_PACKED).  libcgck_lab.so only: 3 lane per 128-byte slot, 4
+//     default there).  libcgck_lab.so only: 3 lane per 128-byte slot, 4
 //     software-pipelined lane per packet, 5..8 lpp shapes 1..3, 0, 11 the
-//     lane-group kernel fed by LDS-DMA.  A variant this build lacks falls
+//     lane-group kernel fed by LDS-DMA, 12 the packed span (descriptor
+//     batches whose frames lie back to back: coalesced stream + prefix sums,
+//     cgck_span.hip; picked under the lab's packed layout hint).  A variant this build lacks falls
 //     back to the automatic choice; one whose preconditions a batch fails
 //     falls back to lpp or group;
 //   kNT (bit 4) nontemporal loads, kContig (bit 5) contiguous block ranges,
 //   kExplicit (bit 6) take bits 4-5 as given instead of the measured defaults,
-//   kPacked (bit 7) the context's layout hint is CGCK_LAYOUT_PACKED.
+//   kPacked (bit 7) the context's (lab-only) layout hint says packed.
 // len_hint = the batch's packet length (strided) or typical length (descriptors).
 hipError_t launch_cksum(const KParams &p0, uint32_t len_hint, int num_cus, int kernel, hipStream_t st)
 {
@@ -77,10 +77,11 @@ hipError_t launch_cksum(const KParams &p0, uint32_t len_hint, int num_cus, int k
 			    ((reinterpret_cast<uintptr_t>(p.base) | p.stride | p.l3_off) & 15) == 0;
 #if CGCK_LAB
 	const bool known = variant <= 12;
-#else
-	const bool known = variant == 1 || variant == 2 || variant == 9 || variant == 10 || variant == 12;
-#endif
 	const bool packed = (kernel & kPacked) && span_ok(p);
+#else
+	const bool known = variant == 1 || variant == 2 || variant == 9 || variant == 10;
+	const bool packed = false;
+#endif
 	if (variant == 0 || !known)
 		variant = !lane_ok ? 1 : lpa_ok ? 10 : packed ? 12 : len_hint >= kGroupFromLen ? 1
 			: len_hint <= kLppUpToLen ? 2 : 9;
@@ -88,9 +89,9 @@ hipError_t launch_cksum(const KParams &p0, uint32_t len_hint, int num_cus, int k
 		variant = 1;
 	if (variant == 10 && !lpa_ok)
 		variant = 2;
+#if CGCK_LAB
 	if (variant == 12 && !span_ok(p))
 		variant = 1;
-#if CGCK_LAB
 	if (variant == 11 && !stream_ok(p))
 		variant = 1;
 #endif
@@ -113,9 +114,9 @@ hipError_t launch_cksum(const KParams &p0, uint32_t len_hint, int num_cus, int k
 		return launch_slot2(p, num_cus, nt, st);
 	case 10:
 		return launch_lpa(p, num_cus, nt, st);
+#if CGCK_LAB
 	case 12:
 		return launch_span(p, num_cus, nt, st);
-#if CGCK_LAB
 	case 3:
 		return launch_slot(p, num_cus, nt, st);
 	case 4:

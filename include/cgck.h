@@ -128,16 +128,6 @@ int cgck_desc(cgck_ctx_t *ctx, void *base, const cgck_desc_t *desc, uint64_t n,
  * handled correctly; the hint only picks the faster kernel. */
 int cgck_set_desc_len_hint(cgck_ctx_t *ctx, uint32_t max_ip_len);
 
-/* Layout hint for descriptor batches.  CGCK_LAYOUT_PACKED: the frames lie
- * back to back in descriptor order (frame k+1 starts where frame k's
- * l3_off + ip_len ends, e.g. cgck_synth_imix's batches); the kernel then
- * streams the packed bytes with fully coalesced loads and separates packets
- * by prefix sums.  Results are exact for any layout whatever the hint (a
- * stretch that is not packed is read packet by packet); the hint only picks
- * the faster kernel, and batches with CGCK_STORE ignore it. */
-enum { CGCK_LAYOUT_ANY = 0, CGCK_LAYOUT_PACKED = 1 };
-int cgck_set_desc_layout(cgck_ctx_t *ctx, uint32_t layout);
-
 /* Host-resident batch (ring memory), synchronous.  Registered memory
  * (cgck_host_register) is read where it lies and in-place stores land there;
  * a small pageable burst (packet bytes <= 512 KiB) is copied packet by packet

@@ -1,8 +1,12 @@
-"""Packed-span kernel (cgck_span.hip) under cgck_set_desc_layout(PACKED):
-bit-exact against the oracle referee (oracle/cksum_oracle.c) on packed
-batches of every length class and alignment, on batches that are NOT packed
-(its gap / lane-per-packet fallbacks must stay exact whatever the hint says),
-and on the full-size IMIX batch (BASELINE configs[3])."""
+"""Packed-span kernel (cgck_span.hip, an A/B family of libcgck_lab.so picked
+by the lab's layout hint): bit-exact against the oracle referee
+(oracle/cksum_oracle.c) on packed batches of every length class and
+alignment, on batches that are NOT packed (its gap / lane-per-packet
+fallbacks must stay exact whatever the hint says), and on the full-size IMIX
+batch (BASELINE configs[3]).  The module runs against the lab build: it swaps
+the binding for its own duration."""
+import os
+
 import numpy as np
 import pytest
 
@@ -10,6 +14,22 @@ import cgck
 from test_gpu_parity import FLAG_SETS, random_batch
 
 pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def engine():
+    if not os.path.exists(cgck.LAB_PATH):
+        pytest.skip("libcgck_lab.so not built (make -C tools lab)")
+    saved = cgck.load()
+    cgck._lib = cgck.bind(cgck.LAB_PATH)
+    try:
+        if cgck.device_count() < 1:
+            pytest.fail("no HIP device visible: the -m gpu tests need an MI355X")
+        e = cgck.Engine(0)
+        yield e
+        e.close()
+    finally:
+        cgck._lib = saved
 
 MIXES = {
     "imix": [64] * 7 + [576] * 4 + [1500],

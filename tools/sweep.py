@@ -71,10 +71,13 @@ def main():
                 e0.synth_imix(imix_bufs[0].ptr, imix_bufs[1].ptr, n, 0xC0C0)
             buf, desc = imix_bufs
             algo = nbytes + 12 * n + (4 * n if "out" in out_list else 0)
-            lay = cgck.LAYOUT_PACKED if w == "imixp" else cgck.LAYOUT_ANY
-            work[w] = (lambda e, f, o, buf=buf, desc=desc, h=nbytes // n, lay=lay: (
-                e.set_desc_len_hint(h), e.set_desc_layout(lay), e.desc(buf.ptr, desc.ptr, n, f, o),
-                e.set_desc_layout(cgck.LAYOUT_ANY)), algo, [buf, desc])
+            if w == "imixp":   # the lab build's layout hint (CGCK_LIB=.../libcgck_lab.so)
+                work[w] = (lambda e, f, o, buf=buf, desc=desc, h=nbytes // n: (
+                    e.set_desc_len_hint(h), e.set_desc_layout(cgck.LAYOUT_PACKED), e.desc(buf.ptr, desc.ptr, n, f, o),
+                    e.set_desc_layout(cgck.LAYOUT_ANY)), algo, [buf, desc])
+            else:
+                work[w] = (lambda e, f, o, buf=buf, desc=desc, h=nbytes // n: (
+                    e.set_desc_len_hint(h), e.desc(buf.ptr, desc.ptr, n, f, o)), algo, [buf, desc])
         else:
             L = int(w)
             buf = cgck.DeviceBuffer(n * L)
