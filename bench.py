@@ -238,7 +238,8 @@ def bench_rss(torch, dist, eng, cgck, plan, steps, warmup):
             "dst": (wall_d, ev_d, tuples, int(c[0]), k_dst)}
 
 
-BURSTS = (32, 256, 2048)   # receive / transmit burst sizes (netmap-like 2048 B slots)
+BURSTS = (32, 64, 128, 256, 512, 1024, 2048)   # receive / transmit burst sizes (netmap-like 2048 B slots)
+BURST_LENS = (1500, 576, 64)   # MTU frames, con-gen's MTU-522 frames (con-gen.c:741) as 576 B, minimum frames
 
 
 def bench_burst():
@@ -251,7 +252,7 @@ def bench_burst():
     exe = os.path.join(ROOT, "tools", "txburst")
     if not os.path.exists(exe):
         return None
-    r = subprocess.run([exe, "0.3"], capture_output=True, text=True, timeout=240)
+    r = subprocess.run([exe, "0.15"], capture_output=True, text=True, timeout=240)
     if r.returncode != 0:
         return {"error": r.stderr.strip()[-300:]}
     return [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
@@ -271,7 +272,38 @@ def burst_summary(rows, cpu):
     cpu_by = {(r["pkt_len"], r["burst"]): round(r["us_per_burst"], 2) for r in (cpu or {}).get("rows", [])}
     return [[ln, b, by.get(("rx_window_registered", ln, b)), by.get(("rx_verify_registered", ln, b)),
              by.get(("tx_fill_registered", ln, b)), cpu_by.get((ln, b))]
-            for ln in (64, 1500) for b in (32, 256, 2048)]
+            for ln in sorted(BURST_LENS) for b in (32, 256, 2048)]
+
+
+def burst_crossover(rows, cpu):
+    """Per packet length, the smallest measured burst from which the RX window
+    (launch path or burst server, registered ring) and the TX window beat the
+    reference CPU loop over the same burst on one core, and stay ahead at every
+    larger measured burst; None when the GPU never wins up to max(BURSTS).
+    INTEGRATION.md quotes these as the threshold below which a window should
+    not be opened."""
+    if not isinstance(rows, list) or not cpu:
+        return None
+    by = {(r["mode"], r["pkt_len"], r["burst"]): r["us_median"] for r in rows}
+    cpu_by = {(r["pkt_len"], r["burst"]): r["us_per_burst"] for r in cpu.get("rows", [])}
+    res = {}
+    for ln in sorted(BURST_LENS):
+        cell = {}
+        for what, modes in (("rx_window", ("rx_window_registered", "rx_window_registered_server")),
+                            ("tx_window", ("tx_fill_registered",))):
+            wins = []
+            for b in BURSTS:
+                g = [by[(m, ln, b)] for m in modes if (m, ln, b) in by]
+                c = cpu_by.get((ln, b))
+                wins.append(bool(g) and c is not None and min(g) < c)
+            first = None
+            for i in range(len(BURSTS) - 1, -1, -1):
+                if not wins[i]:
+                    break
+                first = BURSTS[i]
+            cell[what] = first
+        res[str(ln)] = cell
+    return res
 
 
 def checker_leg(res, plan, cgck):
@@ -315,7 +347,7 @@ def cpu_burst():
     rows = []
     try:
         os.sched_setaffinity(0, {cpus[len(cpus) // 2]})
-        for ln in (1500, 64):
+        for ln in BURST_LENS:
             ring = P.stream_bytes(0, max(BURSTS) * 2048, SEED)
             P.stamp_strided(ring[14:], max(BURSTS) - 1, 2048, ln)
             for b in BURSTS:
@@ -573,6 +605,7 @@ def main():
                                       "from C (tools/txburst.c): RX window, one-call RX verify, TX window; "
                                       "cpu_ref = the reference in_cksum+udp_cksum per packet, 1 core",
                               "cols": BURST_COLS, "rows": burst_summary(burst, cpu_b),
+                              "crossover_burst": burst_crossover(burst, cpu_b),
                               "all_rows": path and "gpurun_out/bench_burst.json"}
         if extra:
             out["extra"] = extra

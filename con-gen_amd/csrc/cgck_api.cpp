@@ -283,7 +283,8 @@ static double now_s()
 static int burst_launch(cgck_ctx *c)
 {
 	__atomic_store_n(&c->bbox->alive, 1u, __ATOMIC_RELEASE);
-	hipError_t e = launch_burst_server(c->bbox_dev, c->d_zero, c->bstream);
+	hipError_t e = launch_burst_server(c->bbox_dev, c->bstage_dev, c->bscratch, (uint32_t *)c->bresp_dev,
+					   c->bresp_dev + c->bresp_ver, c->d_zero, c->bstream);
 	if (e != hipSuccess) {
 		__atomic_store_n(&c->bbox->alive, 0u, __ATOMIC_RELEASE);
 		return set_err(-EIO, "burst server launch: %s", hipGetErrorString(e));
@@ -291,52 +292,65 @@ static int burst_launch(cgck_ctx *c)
 	return 0;
 }
 
-// The server is one workgroup reading host memory over the fabric, one pass
-// of at most 64 packets per request (each pass costs dependent host round
-// trips: descriptor, packet bytes, outputs).  It wins on single calls and
-// small bursts (one in_cksum 10.8 vs 13.8 us, 32 x 64 B RX verify 15.0 vs
-// 18.0 us) and loses beyond one pass (256 x 1500 B RX verify: 80 vs 29 us
-// before this cap), where the launch path spreads the batch over the GPU;
-// TX flushes (mixed 20 B / full-size entries) measured slower through it and
-// keep the launch path (tools/txburst.c, profiles/r01/txburst.log).
-static constexpr size_t kServerBytes = 64 << 10;
-static constexpr uint64_t kServerPkts = 64;
-
-// Does a request of n packets, `data` packet bytes of which `staged` are
-// copied into the staging (0 when read in place), go to the server?
-static bool burst_fits(const cgck_ctx *c, uint64_t n, size_t staged, size_t data)
+// The server is one workgroup: a request costs the poll, one wide read of
+// the request block and the outputs' write acknowledgements (~5 us of host
+// round trips, tools/pingpong) instead of a launch and a stream
+// synchronisation (~9.4 us for an empty kernel).  One CU's reads over the
+// fabric are slow in bulk, though (a 73 KiB block: +12 us), so only small
+// requests go to it: at most one pass of its lane shape (64 packets, or 256
+// of at most 80 bytes) and 96 KiB of packet bytes; registered packets are
+// copied into the block up to 32 KiB of block and read in place above.  The
+// caps are where the server stopped beating the launch path on the registered
+// RX window at 64 / 576 / 1500 B (tools/txburst, profiles/r02/burst).  TX
+// flushes (mixed 20 B / full-size entries) keep the launch path.
+// $CGCK_SERVER_PKTS / _BYTES / _COPY override the caps for A/B runs.
+static size_t env_size(const char *name, size_t dflt)
 {
-	return c->bbox && n <= c->bmax && n <= kServerPkts && staged + 17 * n + 64 <= c->bstage_cap &&
-	       data <= kServerBytes;
+	const char *v = getenv(name);
+	return v && *v ? (size_t)strtoull(v, nullptr, 0) : dflt;
 }
+static const size_t kServerBytes = env_size("CGCK_SERVER_BYTES", 96 << 10);
+static const uint64_t kServerPkts = env_size("CGCK_SERVER_PKTS", 64); // 4x for packets <= 80 B
+static const size_t kServerCopy = env_size("CGCK_SERVER_COPY", 32 << 10);
 
-// Offsets in bstage of a request with `bytes` of packet data and n packets.
+// Offsets in the request block of n descriptors and `staged` packet bytes
+// copied into it (0: read in place).
 struct BurstLayout {
-	size_t d_off, o_off, v_off;
+	size_t d_off, p_off, bytes;
 };
 
-static BurstLayout burst_layout(size_t bytes, uint64_t n)
+static BurstLayout burst_layout(size_t staged, uint64_t n)
 {
 	BurstLayout L;
-	L.d_off = (bytes + 15) & ~(size_t)15;
-	L.o_off = (L.d_off + 12 * n + 15) & ~(size_t)15;
-	L.v_off = L.o_off + 4 * n;
+	L.d_off = sizeof(BurstReq);
+	L.p_off = (L.d_off + 12 * n + 15) & ~(size_t)15;
+	L.bytes = L.p_off + staged;
 	return L;
 }
 
-// Serve the request staged in bstage (base = packets at offset 0, or
-// `base_dev` for packets read in place) and wait for it.
+// Does a request of n packets of at most max_len bytes, `data` packet bytes
+// of which `staged` are copied into the block (0 when read in place), go to
+// the server?
+static bool burst_fits(const cgck_ctx *c, uint64_t n, uint32_t max_len, size_t staged, size_t data)
+{
+	return c->bbox && n <= c->bmax && n <= (max_len <= 80 ? 4 * kServerPkts : kServerPkts) &&
+	       burst_layout(staged, n).bytes <= c->bstage_cap && data <= kServerBytes;
+}
+
+// Serve the request whose descriptors (and, for base_dev == nullptr, packet
+// bytes) are in the block, and wait for it.  Outputs land in c->bresp.
 static int burst_serve(cgck_ctx *c, const uint8_t *base_dev, uint64_t n, uint32_t flags, uint32_t max_len,
 		       const BurstLayout &L)
 {
 	BurstBox *b = c->bbox;
-	b->n = (uint32_t)n;
-	b->flags = flags;
-	b->max_len = max_len;
-	b->base = base_dev ? base_dev : c->bstage_dev;
-	b->desc = (const cgck_desc_t *)(c->bstage_dev + L.d_off);
-	b->out = (uint32_t *)(c->bstage_dev + L.o_off);
-	b->verdict = c->bstage_dev + L.v_off;
+	BurstReq *r = (BurstReq *)c->bstage;
+	r->n = (uint32_t)n;
+	r->flags = flags;
+	r->max_len = max_len;
+	r->bytes = (uint32_t)L.bytes;
+	r->base = (uint64_t)(uintptr_t)base_dev;
+	r->d_off = (uint32_t)L.d_off;
+	r->p_off = (uint32_t)L.p_off;
 	const uint32_t seq = ++c->bseq;
 	__atomic_store_n(&b->seq_req, seq, __ATOMIC_RELEASE);
 	if (!__atomic_load_n(&b->alive, __ATOMIC_ACQUIRE)) {
@@ -430,33 +444,36 @@ int cgck::desc_host(cgck_ctx *c, void *base, size_t bytes, const cgck_desc_t *de
 	void *dev_base = reg_find(base, bytes, &rr) ? (void *)(rr.dev + ((uint8_t *)base - rr.lo))
 						    : registered_ptr(base, bytes);
 	int rc;
-	if (burst_fits(c, n, dev_base ? 0 : pkt_bytes, pkt_bytes)) {
-		// the resident server: same staging layout, no launch, no stream sync
-		const BurstLayout L = burst_layout(dev_base ? 0 : pkt_bytes, n);
+	// Server requests copy the packet bytes into the request block (one wide
+	// read) unless they are registered and either larger than that read or
+	// stored to in place; a pageable batch with in-place stores takes the
+	// launch path (the server's copy of the bytes is not written back).
+	const bool store = flags & CGCK_STORE;
+	const bool in_place = dev_base && (store || burst_layout(pkt_bytes, n).bytes > kServerCopy);
+	if ((in_place || !store) && burst_fits(c, n, max_len, in_place ? 0 : pkt_bytes, pkt_bytes)) {
+		// the resident server: no launch, no stream sync
+		const BurstLayout L = burst_layout(in_place ? 0 : pkt_bytes, n);
 		uint8_t *h = c->bstage;
 		cgck_desc_t *d = (cgck_desc_t *)(h + L.d_off);
-		if (dev_base) {
+		if (in_place) {
 			memcpy(d, desc, 12 * n);
 		} else {
 			size_t at = 0;
 			for (uint64_t i = 0; i < n; i++) {
-				memcpy(h + at, (const uint8_t *)base + desc[i].frame_off + desc[i].l3_off, desc[i].ip_len);
+				memcpy(h + L.p_off + at, (const uint8_t *)base + desc[i].frame_off + desc[i].l3_off,
+				       desc[i].ip_len);
 				d[i].frame_off = at;
 				d[i].l3_off = 0;
 				d[i].ip_len = desc[i].ip_len;
 				at += ((size_t)desc[i].ip_len + 15) & ~(size_t)15;
 			}
 		}
-		if ((rc = burst_serve(c, (const uint8_t *)dev_base, n, flags, max_len, L)))
+		if ((rc = burst_serve(c, in_place ? (const uint8_t *)dev_base : nullptr, n, flags, max_len, L)))
 			return rc;
 		if (out)
-			memcpy(out, h + L.o_off, 4 * n);
+			memcpy(out, c->bresp, 4 * n);
 		if (verdict)
-			memcpy(verdict, h + L.v_off, n);
-		if ((flags & CGCK_STORE) && !dev_base)
-			for (uint64_t i = 0; i < n; i++)
-				memcpy((uint8_t *)base + desc[i].frame_off + desc[i].l3_off, h + d[i].frame_off,
-				       desc[i].ip_len);
+			memcpy(verdict, c->bresp + c->bresp_ver, n);
 		return 0;
 	}
 	if (dev_base || pkt_bytes <= kStageBytes) {
@@ -613,18 +630,18 @@ extern "C" int cgck_host_unregister(void *ptr)
 int cgck::one_region(cgck_ctx *c, const void *src, uint32_t span, uint32_t ip_len, uint32_t flags, uint32_t *out)
 {
 	int rc;
-	if (ip_len <= 0xffff && burst_fits(c, 1, span, span)) {
+	if (ip_len <= 0xffff && !(flags & CGCK_STORE) && burst_fits(c, 1, ip_len, span, span)) {
 		// the resident server: one descriptor, no launch, no stream sync
 		const BurstLayout L = burst_layout(span, 1);
 		if (span)
-			memcpy(c->bstage, src, span);
+			memcpy(c->bstage + L.p_off, src, span);
 		cgck_desc_t *d = (cgck_desc_t *)(c->bstage + L.d_off);
 		d->frame_off = 0;
 		d->l3_off = 0;
 		d->ip_len = (uint16_t)ip_len;
 		if ((rc = burst_serve(c, nullptr, 1, flags, ip_len, L)))
 			return rc;
-		*out = *(const uint32_t *)(c->bstage + L.o_off);
+		*out = *(const uint32_t *)c->bresp;
 		return 0;
 	}
 	if ((rc = grow_host((void **)&c->h_stage, &c->h_stage_cap, span + 16)) ||
@@ -649,31 +666,47 @@ extern "C" int cgck_burst_open(cgck_ctx_t *c, uint32_t max_pkts, size_t max_byte
 	if (max_pkts == 0 || max_bytes == 0)
 		return set_err(-EINVAL, "cgck_burst_open: zero capacity");
 	HIP_TRY(hipSetDevice(c->device));
-	const size_t cap = ((max_bytes + 15) & ~(size_t)15) + 17 * (size_t)max_pkts + 64;
-	void *box = nullptr, *st = nullptr, *bd = nullptr, *sd = nullptr;
+	// the block holds the header, the descriptors and the packet bytes; the
+	// server's first read fetches kBurstFirst bytes whatever the request
+	size_t cap = burst_layout(((max_bytes + 15) & ~(size_t)15) + 16 * (size_t)max_pkts, max_pkts).bytes;
+	cap = (cap < kBurstFirst ? kBurstFirst : cap + 15) & ~(size_t)15;
+	const size_t ver_off = (4 * (size_t)max_pkts + 63) & ~(size_t)63;
+	void *box = nullptr, *st = nullptr, *rs = nullptr, *bd = nullptr, *sd = nullptr, *rd = nullptr, *sc = nullptr;
 	hipError_t e = hipHostMalloc(&box, sizeof(BurstBox), hipHostMallocCoherent);
 	if (e == hipSuccess)
 		e = hipHostMalloc(&st, cap, hipHostMallocCoherent);
+	if (e == hipSuccess)
+		e = hipHostMalloc(&rs, ver_off + max_pkts, hipHostMallocCoherent);
+	if (e == hipSuccess)
+		e = hipMalloc(&sc, cap);
 	if (e == hipSuccess)
 		e = hipHostGetDevicePointer(&bd, box, 0);
 	if (e == hipSuccess)
 		e = hipHostGetDevicePointer(&sd, st, 0);
 	if (e == hipSuccess)
+		e = hipHostGetDevicePointer(&rd, rs, 0);
+	if (e == hipSuccess)
 		e = hipStreamCreateWithFlags(&c->bstream, hipStreamNonBlocking);
 	if (e != hipSuccess) {
-		if (box)
-			(void)hipHostFree(box);
-		if (st)
-			(void)hipHostFree(st);
+		for (void *h : {box, st, rs})
+			if (h)
+				(void)hipHostFree(h);
+		if (sc)
+			(void)hipFree(sc);
 		return set_err(-EIO, "cgck_burst_open: %s", hipGetErrorString(e));
 	}
 	memset(box, 0, sizeof(BurstBox));
+	memset(st, 0, cap);
 	c->bbox = (BurstBox *)box;
 	c->bbox->idle_ticks = (uint64_t)(idle_ms ? idle_ms : 200) * 100000; // 100 MHz counter
 	c->bstage = (uint8_t *)st;
 	c->bstage_cap = cap;
 	c->bstage_dev = (uint8_t *)sd;
 	c->bbox_dev = (BurstBox *)bd;
+	c->bresp = (uint8_t *)rs;
+	c->bresp_dev = (uint8_t *)rd;
+	c->bresp_ver = ver_off;
+	c->bscratch = (uint8_t *)sc;
 	c->bmax = max_pkts;
 	c->bseq = 0;
 	return burst_launch(c);
@@ -691,9 +724,13 @@ extern "C" int cgck_burst_close(cgck_ctx_t *c)
 	(void)hipStreamDestroy(c->bstream);
 	(void)hipHostFree(c->bbox);
 	(void)hipHostFree(c->bstage);
+	(void)hipHostFree(c->bresp);
+	(void)hipFree(c->bscratch);
 	c->bbox = nullptr;
 	c->bstage = nullptr;
 	c->bstage_cap = 0;
+	c->bresp = nullptr;
+	c->bscratch = nullptr;
 	if (e != hipSuccess)
 		return set_err(-EIO, "cgck_burst_close: %s", hipGetErrorString(e));
 	return 0;

@@ -199,15 +199,19 @@ __global__ __launch_bounds__(256) void cksum_kernel(KParams p)
 
 // --------------------------------------------------------------------------
 // Burst server: one resident workgroup that serves small host-resident
-// batches (RX bursts, TX flushes) without a launch or a stream
-// synchronisation per batch.  The host writes a request into a host-coherent
-// mailbox (BurstBox, cgck_internal.h) and bumps seq_req; thread 0 polls it
-// with system-scope acquire loads, the workgroup runs the group kernel's body
-// over the batch (descriptors, packets and outputs in host-coherent staging),
-// and thread 0 publishes seq_done with a system-scope release.  Every poll
-// loop is bounded: the server exits on `stop`, or after idle_ticks of the
-// 100 MHz real-time counter without a request (the host relaunches it on
-// the next request), so no launch outlives its context for long.
+// batches (RX bursts, drop-in calls) without a launch or a stream
+// synchronisation per batch.  The host writes a request block (BurstReq,
+// descriptors, packet bytes) into host-coherent staging and bumps seq_req;
+// thread 0 polls it with system-scope acquire loads.  The workgroup then
+// copies the block into device scratch with one wide read (tools/pingpong:
+// every dependent host round trip costs ~1.3 us, so the block is fetched at
+// once instead of header -> descriptor -> packet bytes), runs the group
+// kernel's body over the scratch copy (or over registered ring memory in
+// place, for larger or in-place-store requests), writes the outputs to
+// host-coherent memory and publishes seq_done with a system-scope release.
+// Every poll loop is bounded: the server exits on `stop`, or after
+// idle_ticks of the 100 MHz real-time counter without a request (the host
+// relaunches it on the next request), so no launch outlives its context.
 // --------------------------------------------------------------------------
 
 __device__ __forceinline__ uint32_t sys_load(const uint32_t *p)
@@ -215,20 +219,31 @@ __device__ __forceinline__ uint32_t sys_load(const uint32_t *p)
 	return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-__global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const void *zero)
+__device__ __forceinline__ uint32_t sys_relaxed(const uint32_t *p)
+{
+	return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const uint8_t *req, uint8_t *scratch,
+							   uint32_t *out, uint8_t *verdict, const void *zero)
 {
 	__shared__ uint32_t cmd; // 1 run the pending request, 2 exit
-	uint32_t last = 0;       // thread 0: the last request served
-	if (threadIdx.x == 0)
+	__shared__ uint4 hdr_w[4];
+	const int t = threadIdx.x;
+	uint32_t last = 0; // thread 0: the last request served
+	if (t == 0)
 		last = sys_load(&box->seq_done);
+	const uint4 *src = reinterpret_cast<const uint4 *>(req);
+	uint4 *dst = reinterpret_cast<uint4 *>(scratch);
 	for (;;) {
-		if (threadIdx.x == 0) {
+		if (t == 0) {
 			const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
 			const uint64_t idle = box->idle_ticks;
 			uint32_t c = 0;
 			while (c == 0) {
-				const uint32_t r = sys_load(&box->seq_req);
-				if (sys_load(&box->stop))
+				// relaxed: an acquire load would invalidate the caches every poll
+				const uint32_t r = sys_relaxed(&box->seq_req);
+				if (sys_relaxed(&box->stop))
 					c = 2;
 				else if (r != last)
 					c = 1, last = r;
@@ -240,30 +255,69 @@ __global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const 
 			cmd = c;
 		}
 		__syncthreads();
-		const uint32_t c = cmd;
-		if (c == 2)
+		if (cmd == 2)
 			break;
-		__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); // the host's request writes, every thread
-		const KParams p = {box->base, box->desc, box->n, 0, 0, 0, box->flags, box->out, box->verdict,
-				   nullptr, 0, zero};
-		// many packets per pass: each pass costs host round trips (descriptor,
-		// then packet bytes), so the shapes carry 256 / 64 packets per pass
-		if (box->max_len <= 80)
+		// One system-scope acquire (no line of an earlier request, or of an
+		// earlier burst in a registered ring, is served from the cache), then
+		// the first kBurstFirst bytes of the block in one round trip: plain
+		// 16-byte loads, so every wave's read leaves as whole-line requests.
+		__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+		constexpr int W = kBurstFirst / 16 / 256;
+		uint4 v[W];
+#pragma unroll
+		for (int w = 0; w < W; ++w)
+			v[w] = src[w * 256 + t];
+#pragma unroll
+		for (int w = 0; w < W; ++w)
+			dst[w * 256 + t] = v[w];
+		if (t < 4)
+			hdr_w[t] = v[0];
+		__syncthreads();
+		const BurstReq &h = *reinterpret_cast<const BurstReq *>(hdr_w);
+		const uint32_t chunks = (h.bytes + 15) / 16;
+		// the rest of a larger block, 16 loads in flight per thread (64 KiB a
+		// round trip)
+		for (uint32_t at = kBurstFirst / 16; at < chunks; at += 16 * 256) {
+			uint4 x[16];
+#pragma unroll
+			for (int k = 0; k < 16; ++k) {
+				const uint32_t i = at + k * 256 + t;
+				x[k] = i < chunks ? src[i] : make_uint4(0, 0, 0, 0);
+			}
+#pragma unroll
+			for (int k = 0; k < 16; ++k) {
+				const uint32_t i = at + k * 256 + t;
+				if (i < chunks)
+					dst[i] = x[k];
+			}
+		}
+		// scratch stores visible to the workgroup (its waves share one CU's
+		// L1: workgroup scope)
+		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+		__syncthreads();
+		__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+		const KParams p = {h.base ? reinterpret_cast<const uint8_t *>(h.base) : scratch + h.p_off,
+				   reinterpret_cast<const cgck_desc_t *>(scratch + h.d_off),
+				   h.n, 0, 0, 0, h.flags, out, verdict, nullptr, 0, zero};
+		if (h.max_len <= 80)
 			cksum_body<4, 2, 4, true, false>(p);
 		else
 			cksum_body<16, 6, 4, true, false>(p);
-		__builtin_amdgcn_fence(__ATOMIC_RELEASE, ""); // this thread's outputs, system scope
+		// every thread's outputs (and in-place stores) performed; thread 0's
+		// system-scope release then writes them back ahead of seq_done
+		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
 		__syncthreads();
-		if (threadIdx.x == 0)
+		if (t == 0)
 			__hip_atomic_store(&box->seq_done, last, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 	}
-	if (threadIdx.x == 0)
+	if (t == 0)
 		__hip_atomic_store(&box->alive, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-hipError_t launch_burst_server(BurstBox *box, const void *zero, hipStream_t st)
+hipError_t launch_burst_server(BurstBox *box, const uint8_t *req, uint8_t *scratch, uint32_t *out, uint8_t *verdict,
+			       const void *zero, hipStream_t st)
 {
-	hipLaunchKernelGGL(burst_server_kernel, dim3(1), dim3(256), 0, st, box, zero);
+	hipLaunchKernelGGL(burst_server_kernel, dim3(1), dim3(256), 0, st, box, req, scratch, out, verdict, zero);
 	return hipGetLastError();
 }
 

@@ -41,12 +41,17 @@ struct cgck_ctx {
 	// dst-cache scratch: control words + look-back status (zeroed per launch)
 	uint8_t *d_dst;
 	size_t d_dst_cap;
-	// burst server (cgck_burst_open): mailbox and staging, host-coherent pinned
+	// burst server (cgck_burst_open): mailbox, request block and outputs in
+	// host-coherent pinned memory, the block's device copy in scratch
 	cgck::BurstBox *bbox; // nullptr: closed
-	uint8_t *bstage;      // [packets | descriptors | out | verdict]
+	uint8_t *bstage;      // request block: [BurstReq | descriptors | packet bytes]
 	size_t bstage_cap;
 	uint8_t *bstage_dev;        // device view of bstage
 	cgck::BurstBox *bbox_dev;   // device view of bbox
+	uint8_t *bresp;             // [out u32 x bmax | verdict u8 x bmax]
+	uint8_t *bresp_dev;
+	size_t bresp_ver;           // offset of the verdicts in bresp
+	uint8_t *bscratch;          // device: the server's copy of the block (bstage_cap bytes)
 	uint32_t bmax;              // packets per request
 	uint32_t bseq;
 	hipStream_t bstream; // the server's own stream (it stays resident)

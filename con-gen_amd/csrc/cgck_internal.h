@@ -40,25 +40,37 @@ struct KParams {
 };
 
 // Mailbox of the burst server (cgck_group.hip), in host-coherent pinned
-// memory: the host fills a request and bumps seq_req (release); the server
-// answers with seq_done (release) once the outputs are visible.
+// memory: the host writes a request block (BurstReq + descriptors + packet
+// bytes) into its staging and bumps seq_req (release); the server answers
+// with seq_done (release) once the outputs are visible.
 struct BurstBox {
 	uint32_t seq_req;    // host -> device: number of the pending request
 	uint32_t seq_done;   // device -> host: last request served
 	uint32_t stop;       // host -> device: exit now
 	uint32_t alive;      // host sets 1 at launch; the server clears it on exit
-	uint32_t n;          // request: packets
-	uint32_t flags;      // request: CGCK_* flags
-	uint32_t max_len;    // request: longest ip_len (picks the lane shape)
-	uint32_t pad;
 	uint64_t idle_ticks; // 100 MHz ticks without a request before the server exits
-	const uint8_t *base; // request: batch base (device view of the staging)
-	const cgck_desc_t *desc;
-	uint32_t *out;
-	uint8_t *verdict;
 };
 
-hipError_t launch_burst_server(BurstBox *box, const void *zero, hipStream_t st);
+// Header of a request block (the first 64 bytes of the burst staging).  The
+// server copies the block's first kBurstFirst bytes into device scratch with
+// one wide read — every thread's loads in flight together, one host round
+// trip for a small request's header, descriptors and packet bytes — and the
+// rest of a larger block in a second pass.
+struct BurstReq {
+	uint32_t n;       // packets
+	uint32_t flags;   // CGCK_* flags
+	uint32_t max_len; // longest ip_len (picks the lane shape)
+	uint32_t bytes;   // size of the request block, this header included
+	uint64_t base;    // device view of packets read in place (registered memory); 0: in the block
+	uint32_t d_off;   // descriptors: offset in the block
+	uint32_t p_off;   // packet bytes (base == 0): offset in the block
+	uint32_t pad[8];
+};
+static_assert(sizeof(BurstReq) == 64, "one header line");
+constexpr uint32_t kBurstFirst = 8192;
+
+hipError_t launch_burst_server(BurstBox *box, const uint8_t *req, uint8_t *scratch, uint32_t *out, uint8_t *verdict,
+			       const void *zero, hipStream_t st);
 
 // Kernel selection flags (see cgck_dispatch.cpp) and the measured defaults
 // (tools/sweep.py; profiles/r01).  The group kernel streams whole lines per

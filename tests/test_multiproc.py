@@ -94,10 +94,27 @@ def test_device_for_refuses_oversubscription():
 def test_burst_summary_is_compact():
     rows = [{"mode": m, "pkt_len": ln, "burst": b, "us_median": 1.0}
             for m in ("rx_window_registered", "rx_verify_registered", "tx_fill_registered", "rx_verify")
-            for ln in (64, 1500) for b in (32, 256, 2048)]
-    cpu = {"rows": [{"pkt_len": ln, "burst": b, "us_per_burst": 2.0} for ln in (64, 1500) for b in (32, 256, 2048)]}
+            for ln in bench.BURST_LENS for b in bench.BURSTS]
+    cpu = {"rows": [{"pkt_len": ln, "burst": b, "us_per_burst": 2.0} for ln in bench.BURST_LENS for b in bench.BURSTS]}
     s = bench.burst_summary(rows, cpu)
     assert len(s) <= 10 and all(len(r) == len(bench.BURST_COLS) and r[-1] == 2.0 and r[2] == 1.0 for r in s)
+
+
+def test_burst_crossover():
+    """The crossover is the first burst of the final winning run: a GPU win at
+    a small burst followed by a loss does not count."""
+    B = bench.BURSTS
+    gpu = {64: [9.0] * len(B), 576: [1.0] + [9.0] * (len(B) - 3) + [1.0, 1.0], 1500: [1.0] * len(B)}
+    rows = [{"mode": "rx_window_registered", "pkt_len": ln, "burst": b, "us_median": gpu[ln][i]}
+            for ln in gpu for i, b in enumerate(B)]
+    rows += [{"mode": "rx_window_registered_server", "pkt_len": 64, "burst": B[-1], "us_median": 1.0}]
+    cpu = {"rows": [{"pkt_len": ln, "burst": b, "us_per_burst": 2.0} for ln in gpu for b in B]}
+    x = bench.burst_crossover(rows, cpu)
+    assert x["64"]["rx_window"] == B[-1]     # the server row wins at the largest burst only
+    assert x["576"]["rx_window"] == B[-2]
+    assert x["1500"]["rx_window"] == B[0]
+    assert x["1500"]["tx_window"] is None    # no TX rows measured
+    assert bench.burst_crossover({"error": "x"}, cpu) is None
 
 
 def test_single_rank_is_noop():
@@ -114,5 +131,5 @@ def test_cpu_burst_leg_runs():
     pinned core) produces a row per packet length and burst size."""
     r = bench.cpu_burst()
     assert r["cores"] == 1 and r["kind"] in ("reference", "port")
-    assert {(x["pkt_len"], x["burst"]) for x in r["rows"]} == {(ln, b) for ln in (1500, 64) for b in bench.BURSTS}
+    assert {(x["pkt_len"], x["burst"]) for x in r["rows"]} == {(ln, b) for ln in bench.BURST_LENS for b in bench.BURSTS}
     assert all(x["us_per_burst"] > 0 for x in r["rows"])

@@ -79,20 +79,25 @@ static double median(double *t, int n)
 int main(int argc, char **argv)
 {
 	const double budget = argc > 1 ? atof(argv[1]) : 0.4;
-	const int bursts[] = {32, 256, 2048};
-	const int lens[] = {1500, 64};
+	const int bursts[] = {32, 64, 128, 256, 512, 1024, 2048};
+	const int nb = (int)(sizeof(bursts) / sizeof(bursts[0]));
+	/* 1500 B MTU frames, 576 B (con-gen's MTU 522 + headers, con-gen.c:741,
+	 * rounded up to the IMIX class) and 64 B minimum frames */
+	const int lens[] = {1500, 576, 64};
+	const int nl = (int)(sizeof(lens) / sizeof(lens[0]));
 	const int maxb = 2048, maxit = 100000;
 	uint8_t *ring = aligned_alloc(4096, (size_t)maxb * SLOT);
 	cgck_desc_t *desc = malloc(sizeof(cgck_desc_t) * maxb);
 	uint32_t *out = malloc(4 * maxb);
 	uint8_t *ver = malloc(maxb);
 	double *t = malloc(sizeof(double) * maxit);
+	double *tc = malloc(sizeof(double) * maxit); /* RX window: the per-packet calls + rx_end only */
 	cgck_ctx_t *ctx;
-	if (!ring || !desc || !out || !ver || !t || cgck_ctx_create(0, &ctx)) {
+	if (!ring || !desc || !out || !ver || !t || !tc || cgck_ctx_create(0, &ctx)) {
 		fprintf(stderr, "txburst: setup failed: %s\n", cgck_last_error());
 		return 1;
 	}
-	for (int li = 0; li < 2; li++) {
+	for (int li = 0; li < nl; li++) {
 		const int len = lens[li];
 		uint64_t s = 0x9E3779B97F4A7C15ull;
 		for (int i = 0; i < maxb; i++) {
@@ -129,7 +134,7 @@ int main(int argc, char **argv)
 				fprintf(stderr, "txburst: burst_open failed: %s\n", cgck_last_error());
 				return 1;
 			}
-			for (int bi = 0; bi < 3; bi++) {
+			for (int bi = 0; bi < nb; bi++) {
 				const int R = bursts[bi];
 				const uint32_t vf = CGCK_IP | CGCK_L4 | CGCK_VERIFY | CGCK_V_IP_ZERO_IS_FFFF |
 						    CGCK_V_UDP_ZERO_SKIP;
@@ -156,7 +161,7 @@ int main(int argc, char **argv)
 				       rx_name[pass], len, R, it, us, R / us, bad_ip, bad_l4, (R + 63) / 64);
 				fflush(stdout);
 			}
-			for (int bi = 0; bi < 3; bi++) {
+			for (int bi = 0; bi < nb; bi++) {
 				const int R = bursts[bi];
 				int it = 0, w = 0, bad_ip = 0, bad_l4 = 0;
 				double t0 = now();
@@ -167,6 +172,7 @@ int main(int argc, char **argv)
 						fprintf(stderr, "txburst: rx_begin failed: %s\n", cgck_last_error());
 						return 1;
 					}
+					const double a1 = now();
 					for (int i = 0; i < R; i++) {
 						uint8_t *ip = ring + (size_t)i * SLOT + L3;
 						uint16_t saved, v;
@@ -187,17 +193,19 @@ int main(int argc, char **argv)
 					}
 					bad_ip = bi_;
 					bad_l4 = bl_;
-					if (w++ >= 20)
+					if (w++ >= 20) {
+						tc[it] = now() - a1;
 						t[it++] = now() - a;
+					}
 				}
-				const double us = median(t, it) * 1e6;
+				const double us = median(t, it) * 1e6, us_calls = median(tc, it) * 1e6;
 				printf("{\"mode\": \"%s\", \"pkt_len\": %d, \"burst\": %d, \"iters\": %d, "
-				       "\"us_median\": %.2f, \"mpkt_s\": %.3f, \"bad_ip\": %d, \"bad_l4\": %d, "
-				       "\"bad_l4_expected\": %d}\n",
-				       win_name[pass], len, R, it, us, R / us, bad_ip, bad_l4, (R + 63) / 64);
+				       "\"us_median\": %.2f, \"us_calls\": %.2f, \"mpkt_s\": %.3f, \"bad_ip\": %d, "
+				       "\"bad_l4\": %d, \"bad_l4_expected\": %d}\n",
+				       win_name[pass], len, R, it, us, us_calls, R / us, bad_ip, bad_l4, (R + 63) / 64);
 				fflush(stdout);
 			}
-			for (int bi = 0; bi < 3 && pass == 1; bi++) { /* TX: registered ring, launch path */
+			for (int bi = 0; bi < nb && pass == 1; bi++) { /* TX: registered ring, launch path */
 				const int R = bursts[bi];
 				int it = 0, w = 0;
 				double t0 = now();
