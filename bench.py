@@ -467,16 +467,20 @@ TRAFFIC_SOURCE = ("profiles/pmc_latest.json: FETCH_SIZE x 2 + WRITE_SIZE per lau
                   "rocprofv3 --pmc passes of this bench (tools/gpu_prof.sh), not measured in this run")
 
 
-def load_traffic(key="1500"):
+def load_traffic(key="1500", kernel=None):
     """Per-launch HBM bytes of a workload's kernel from the committed PMC
     summary (profiles/pmc_latest.json, written by tools/pmc_traffic.py from
-    separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench)."""
+    separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench);
+    None when the summary was taken on another kernel than this run's."""
     p = os.path.join(ROOT, "profiles", "pmc_latest.json")
     try:
         with open(p) as f:
-            return json.load(f).get(f"bytes_per_launch_{key}")
+            d = json.load(f)
     except (OSError, ValueError):
         return None
+    if kernel and d.get("kernels", {}).get(key) not in (None, kernel):
+        return None
+    return d.get(f"bytes_per_launch_{key}")
 
 
 def roofline(n, size, ev_ms, kernel, traffic_key, extra_bytes=0):
@@ -485,7 +489,7 @@ def roofline(n, size, ev_ms, kernel, traffic_key, extra_bytes=0):
     algo = n * (size + 4) + extra_bytes
     ach = algo / (ev_ms * 1e-3)
     return {"bound": "hbm", "achieved": ach / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-            "frac": ach / HBM_PEAK, "traffic": load_traffic(traffic_key), "kernel": kernel,
+            "frac": ach / HBM_PEAK, "traffic": load_traffic(traffic_key, kernel), "kernel": kernel,
             "algorithmic_bytes_per_launch": algo, "kernel_ms_hip_events": ev_ms}
 
 

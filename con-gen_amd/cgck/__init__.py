@@ -447,18 +447,20 @@ class Engine:
         return ms.value
 
     # -- numpy conveniences (tests) --
-    def run_host_strided(self, buf, n, stride, l3_off, ip_len, flags, want_verdict=False):
+    def run_host_strided(self, buf, n, stride, l3_off, ip_len, flags, want_verdict=True):
         """Copy a host batch to the device, run cgck_strided, copy results (and,
-        with STORE, the bytes) back.  Returns (out, verdict)."""
+        with STORE, the bytes) back.  Returns (out, verdict); verdict is None
+        when want_verdict is False (no verdict array passed to the library)."""
         d = DeviceBuffer(max(buf.nbytes, 1))
         o = DeviceBuffer(4 * max(n, 1))
         v = DeviceBuffer(max(n, 1))
         d.upload(buf, stream=self.stream)
-        self.strided(d.ptr, n, stride, l3_off, ip_len, flags, o.ptr, v.ptr, None)
+        self.strided(d.ptr, n, stride, l3_off, ip_len, flags, o.ptr, v.ptr if want_verdict else None, None)
         out = np.zeros(n, np.uint32)
-        ver = np.zeros(n, np.uint8)
+        ver = np.zeros(n, np.uint8) if want_verdict else None
         o.download(out, stream=self.stream)
-        v.download(ver, stream=self.stream)
+        if want_verdict:
+            v.download(ver, stream=self.stream)
         if flags & STORE:
             d.download(buf, stream=self.stream)
         self.sync()

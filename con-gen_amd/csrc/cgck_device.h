@@ -150,6 +150,20 @@ __device__ __forceinline__ CGCK_GLOBAL T *gbl_at(uint64_t a)
 }
 
 // Streaming chunk load; NT = nontemporal (read-once data, no cache retention).
+// 16 bytes per lane from global memory into LDS by DMA (global_load_lds_dwordx4,
+// nontemporal): lane l's bytes land at lds_dst + 16 l (lds_dst wave-uniform, in
+// M0).  Inline asm, so the compiler counts none of it in vmcnt: every wait on
+// it is explicit in the caller.
+__device__ __forceinline__ void glds16_nt(const void *gsrc, uint32_t lds_dst)
+{
+	uint32_t keep;
+	asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\t"
+		     "s_mov_b32 m0, %0"
+		     : "=&s"(keep)
+		     : "v"(gsrc), "s"(lds_dst)
+		     : "memory");
+}
+
 template <bool NT>
 __device__ __forceinline__ uint4 ld(const uint4 *p)
 {

@@ -2,7 +2,7 @@
 //
 // The product library (libcgck.so) carries only the families the dispatcher
 // picks by itself: group (>= 1 KiB typical length, drop-in and window calls),
-// lpa (aligned fixed-length 20..64-byte strided batches), lpp (small
+// lpd / lpa (aligned fixed-length 20..64-byte strided batches), lpp (small
 // unaligned or descriptor packets) and slot2 (mid-size / mixed lengths).  The
 // A/B-only variants measured against them (slot, lppp, the other lpp shapes,
 // the LDS-DMA stream kernels, the probe kernels) are compiled only into
@@ -39,6 +39,8 @@ hipError_t launch_group(const KParams &p, uint32_t max_len, int num_cus, bool nt
 hipError_t launch_lpp(const KParams &p, int num_cus, bool nt, int shape, hipStream_t st);
 hipError_t launch_slot2(const KParams &p, int num_cus, bool nt, hipStream_t st);
 hipError_t launch_lpa(const KParams &p, int num_cus, bool nt, hipStream_t st);
+hipError_t launch_lpd(const KParams &p, int num_cus, hipStream_t st);
+bool lpd_ok(const KParams &p);
 #if CGCK_LAB
 hipError_t launch_span(const KParams &p, int num_cus, bool nt, hipStream_t st);
 bool span_ok(const KParams &p);
@@ -53,14 +55,16 @@ bool stream_ok(const KParams &p);
 //   variant (bits 0-3): 0 auto, 1 group (G lanes per packet), 2 lane per
 //     packet (lpp), 9 lane per 128-byte slot pipelined two deep (slot2, the
 //     default for mid-size packets), 10 lane per packet for aligned
-//     fixed-length strided 20..64-byte packets, A/B pipelined (lpa, the
-//     default there).  libcgck_lab.so only: 3 lane per 128-byte slot, 4
-//     software-pipelined lane per packet, 5..8 lpp shapes 1..3, 0, 11 the
-//     lane-group kernel fed by LDS-DMA, 12 the packed span (descriptor
-//     batches whose frames lie back to back: coalesced stream + prefix sums,
-//     cgck_span.hip; picked under the lab's packed layout hint).  A variant this build lacks falls
-//     back to the automatic choice; one whose preconditions a batch fails
-//     falls back to lpp or group;
+//     fixed-length strided 20..64-byte packets, A/B pipelined (lpa), 13 the
+//     same fed by LDS-DMA with staged output runs (lpd, the default there when
+//     the batch has no verdicts, counters or stores and stride <= 64).
+//     libcgck_lab.so only: 3 lane per 128-byte slot, 4 software-pipelined
+//     lane per packet, 5..8 lpp shapes 1..3, 0, 11 the lane-group kernel fed
+//     by LDS-DMA, 12 the packed span (descriptor batches whose frames lie back
+//     to back: coalesced stream + prefix sums, cgck_span.hip; picked under the
+//     lab's packed layout hint).  A variant this build lacks falls back to the
+//     automatic choice; one whose preconditions a batch fails falls back to
+//     lpa, lpp or group;
 //   kNT (bit 4) nontemporal loads, kContig (bit 5) contiguous block ranges,
 //   kExplicit (bit 6) take bits 4-5 as given instead of the measured defaults,
 //   kPacked (bit 7) the context's (lab-only) layout hint says packed.
@@ -76,19 +80,21 @@ hipError_t launch_cksum(const KParams &p0, uint32_t len_hint, int num_cus, int k
 	const bool lpa_ok = lane_ok && !p.desc && p.ip_len >= 20 && p.ip_len <= 64 &&
 			    ((reinterpret_cast<uintptr_t>(p.base) | p.stride | p.l3_off) & 15) == 0;
 #if CGCK_LAB
-	const bool known = variant <= 12;
+	const bool known = variant <= 13;
 	const bool packed = (kernel & kPacked) && span_ok(p);
 #else
-	const bool known = variant == 1 || variant == 2 || variant == 9 || variant == 10;
+	const bool known = variant == 1 || variant == 2 || variant == 9 || variant == 10 || variant == 13;
 	const bool packed = false;
 #endif
 	if (variant == 0 || !known)
-		variant = !lane_ok ? 1 : lpa_ok ? 10 : packed ? 12 : len_hint >= kGroupFromLen ? 1
+		variant = !lane_ok ? 1 : lpa_ok ? (lpd_ok(p) ? 13 : 10) : packed ? 12 : len_hint >= kGroupFromLen ? 1
 			: len_hint <= kLppUpToLen ? 2 : 9;
 	if (variant >= 2 && !lane_ok)
 		variant = 1;
 	if (variant == 10 && !lpa_ok)
 		variant = 2;
+	if (variant == 13 && !(lpa_ok && lpd_ok(p)))
+		variant = lpa_ok ? 10 : 2;
 #if CGCK_LAB
 	if (variant == 12 && !span_ok(p))
 		variant = 1;
@@ -114,6 +120,8 @@ hipError_t launch_cksum(const KParams &p0, uint32_t len_hint, int num_cus, int k
 		return launch_slot2(p, num_cus, nt, st);
 	case 10:
 		return launch_lpa(p, num_cus, nt, st);
+	case 13:
+		return launch_lpd(p, num_cus, st);
 #if CGCK_LAB
 	case 12:
 		return launch_span(p, num_cus, nt, st);

@@ -224,8 +224,9 @@ __device__ __forceinline__ void lpa_load(const KParams &p, uint64_t k, bool live
 // the group, slot and hash kernels' stores lost up to 13 points).  (A staged
 // form — four results per lane leaving as one 16-byte store after an LDS
 // transpose — measured 66.7 % vs 69.5 % of HBM peak on one box.)
-template <bool NT>
-__device__ __forceinline__ void lpa_reduce(const KParams &p, uint64_t k, int len, int nch, const Quad &q)
+template <bool NT, bool STAGE = false>
+__device__ __forceinline__ void lpa_reduce(const KParams &p, uint64_t k, int len, int nch, const Quad &q,
+					   uint32_t *so = nullptr)
 {
 	const bool ok = k < p.n;
 	// Fast path (wave-uniform): ip_cksum + tcp_cksum only, whole chunks, and
@@ -245,7 +246,9 @@ __device__ __forceinline__ void lpa_reduce(const KParams &p, uint64_t k, int len
 		L = fold16(L + PS + (proto << 8) + bswap16((uint32_t)(len - 20)));
 		if (ok) {
 			const uint32_t out = finish(IPs) | (finish(L) << 16);
-			if (p.out) {
+			if (STAGE) {
+				*so = out;
+			} else if (p.out) {
 				uint32_t *o = p.out + k;
 				asm volatile("global_store_dword %0, %1, off nt" ::"v"(o), "v"(out) : "memory");
 			}
@@ -282,8 +285,12 @@ __device__ __forceinline__ void lpa_reduce(const KParams &p, uint64_t k, int len
 			// allocate onto this store's data VGPR) behind a vmcnt(0) for the
 			// store.  Every vmcnt the compiler computes stays conservative: the
 			// hidden store only makes in-order waits include it.
-			uint32_t *o = p.out + k;
-			asm volatile("global_store_dword %0, %1, off nt" ::"v"(o), "v"(r.out) : "memory");
+			if (STAGE) {
+				*so = r.out;
+			} else {
+				uint32_t *o = p.out + k;
+				asm volatile("global_store_dword %0, %1, off nt" ::"v"(o), "v"(r.out) : "memory");
+			}
 		}
 		if (p.verdict)
 			gbl(p.verdict)[k] = (uint8_t)r.verdict;
@@ -317,6 +324,313 @@ __global__ __launch_bounds__(256) void lpa_kernel(KParams p)
 		}
 		it += (uint64_t)DEPTH * S;
 	}
+}
+
+// --------------------------------------------------------------------------
+// Lane per packet fed by LDS-DMA (lpd: the 64 B config's default)
+// --------------------------------------------------------------------------
+//
+// lpa's per-lane loads touch 64 lines per instruction.  Here each step of 64
+// packets (63 * stride + len <= 4 KiB) moves as four contiguous 1 KiB
+// global_load_lds_dwordx4 instructions into a ring of D LDS slots of its
+// wave, and lane L reads packet L's chunks from LDS and reduces them with
+// lpa_reduce (the same arithmetic).  Steps come in chunks of C, and chunks
+// are grid-interleaved (wave b takes chunks b, b + G, ...), so the grid sweeps
+// one window of the batch: the DMA sweep alone then reads 89-99 % of 8 TB/s
+// (a contiguous range per wave: 78-89 %).  The output stores were the cost
+// left (92 % with the reduce but no stores, 74 % with a u32 store per packet),
+// so a chunk's outputs are staged in LDS and leave as one contiguous
+// C * 256-byte run of 16-byte stores (sc1 policy).  In one process on one
+// buffer (tools/sweep.py, profiles/r02/lpd/): C = 32, D = 2, 8 waves per CU,
+// sc1 stores 80.6 % against lpa's 71.8 %; C = 16 75.2 %, nt stores 78.8 %,
+// default-policy stores 73.1 %, D = 3 or 10 waves per CU lose (LDS occupancy
+// below the grid: a tail of non-resident waves).
+//
+// Counted vmcnt: per step 4 DMA; a chunk flush adds C / 4 stores, so the wait
+// for step j leaves the D - 1 later steps' DMA and, right after a flush, the
+// flush's stores in flight.
+template <int D, int C, int SP>
+__global__ __launch_bounds__(64) void lpd_kernel(KParams p)
+{
+	extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+	const int lane = threadIdx.x;
+	const int len = (int)p.ip_len, nch = (len + 15) >> 4;
+	const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)smem);
+	uint32_t *so = reinterpret_cast<uint32_t *>(smem + D * 4096); // C > 1: a chunk's outputs
+	const uint8_t *zero = (const uint8_t *)p.zero + (blockIdx.x & 63) * 64;
+	const uint64_t base = reinterpret_cast<uint64_t>(p.base) + p.l3_off;
+	const uint64_t last_chunk = (base + (p.n - 1) * p.stride + len - 1) & ~(uint64_t)15;
+	// Chunks of C steps of 64 packets, grid-interleaved (wave b takes chunks
+	// b, b + G, ...): the grid sweeps one window of the batch, so reads and
+	// output writes stay within few DRAM pages chip-wide.  C > 1: a chunk's
+	// outputs are staged in LDS and leave as one contiguous C * 256-byte run.
+	const uint64_t NS = (p.n + 63) / 64, NC = (NS + C - 1) / C, G = gridDim.x, b = blockIdx.x;
+	if (b >= NC)
+		return;
+	const uint64_t nsteps = (NC - b + G - 1) / G * C;
+	auto gstep = [&](uint64_t j) { return (b + (j / C) * G) * C + j % C; };
+	// bytes a step covers: lanes past them (stride < 64) read the zero line
+	const uint32_t span = (uint32_t)(63 * p.stride) + (uint32_t)len;
+	auto issue = [&](uint64_t j) { // step j of this wave into slot j % D
+		const uint64_t gs = gstep(j);
+		const uint64_t a = base + gs * 64 * p.stride;
+		const uint32_t slot = lds0 + (uint32_t)(j % D) * 4096;
+#pragma unroll
+		for (int i = 0; i < 4; ++i) {
+			const uint32_t at = 1024 * i + 16 * lane;
+			const uint64_t src = a + at;
+			glds16_nt(j < nsteps && gs < NS && at < span && src <= last_chunk ? reinterpret_cast<const void *>(src)
+											  : zero,
+				  slot + 1024 * i);
+		}
+	};
+#pragma unroll
+	for (int d = 0; d < D - 1; ++d)
+		issue(d);
+	const int o = lane * (int)p.stride; // packet L's byte offset in a slot
+	const bool stage = C > 1 && p.out;
+	for (uint64_t j = 0; j < nsteps; ++j) {
+		issue(j + D - 1);
+		// Wait for step j's DMA.  Issued after it: the DMA of the D - 1 later
+		// steps, plus the output stores of the steps since (C == 1: one per
+		// step once the ring is full; C > 1: C / 4 of the last chunk flush,
+		// when that flush came after step j's DMA).
+		if (C == 1) {
+			if (j + 1 < (uint64_t)D || !p.out)
+				asm volatile("s_waitcnt vmcnt(%0)" ::"i"(4 * (D - 1)) : "memory");
+			else
+				asm volatile("s_waitcnt vmcnt(%0)" ::"i"(5 * (D - 1)) : "memory");
+		} else {
+			if (stage && j >= (uint64_t)C && (j % C) <= (uint64_t)(D - 2))
+				asm volatile("s_waitcnt vmcnt(%0)" ::"i"(4 * (D - 1) + C / 4) : "memory");
+			else
+				asm volatile("s_waitcnt vmcnt(%0)" ::"i"(4 * (D - 1)) : "memory");
+		}
+		__builtin_amdgcn_s_barrier();
+		const uint8_t *sl = smem + (uint32_t)(j % D) * 4096;
+		Quad q;
+#pragma unroll
+		for (int i = 0; i < 4; ++i)
+			q.c[i] = *reinterpret_cast<const uint4 *>(sl + o + 16 * (i < nch ? i : nch - 1));
+		asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // the slot is refilled next step
+		const uint64_t k = gstep(j) * 64 + lane;
+		if (stage)
+			lpa_reduce<false, true>(p, k, len, nch, q, so + (j % C) * 64 + lane);
+		else
+			lpa_reduce<false>(p, k, len, nch, q);
+		if (stage && (j + 1) % C == 0 && p.contig != 2) { // contig 2: lab $CGCK_LPD_SINK, no flush
+			// flush the chunk: C / 4 coalesced 16-byte stores per lane
+			const uint64_t first = (b + (j / C) * G) * C * 64;
+			asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+			if (first + C * 64 <= p.n) {
+				const uint4 *s4 = reinterpret_cast<const uint4 *>(so);
+#pragma unroll
+				for (int i = 0; i < C / 4; ++i) {
+					typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+					const uint4 w = s4[i * 64 + lane];
+					const u32x4 v = {w.x, w.y, w.z, w.w};
+					uint4 *dst = reinterpret_cast<uint4 *>(p.out + first) + i * 64 + lane;
+					if (SP == 0)
+						asm volatile("s_waitcnt lgkmcnt(0)\n\tglobal_store_dwordx4 %0, %1, off nt"
+							     ::"v"(dst), "v"(v) : "memory");
+					else if (SP == 1)
+						asm volatile("s_waitcnt lgkmcnt(0)\n\tglobal_store_dwordx4 %0, %1, off"
+							     ::"v"(dst), "v"(v) : "memory");
+					else
+						asm volatile("s_waitcnt lgkmcnt(0)\n\tglobal_store_dwordx4 %0, %1, off sc1"
+							     ::"v"(dst), "v"(v) : "memory");
+				}
+			} else {
+				// the batch's last, partial chunk: per-packet stores, then drain
+				for (int i = lane; i < C * 64; i += 64)
+					if (first + i < p.n)
+						gbl(p.out)[first + i] = so[i];
+				asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+			}
+		}
+	}
+	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+#if CGCK_LAB
+// Loader/consumer form (A/B; lost: 62-72 %): the output store sits in the
+// consumers' vmcnt only.
+// Wave 0 of a 256-thread workgroup only moves bytes (a phase = 3 steps of 64
+// packets, 12 KiB, into a ring of P phases); waves 1..3 each reduce one step
+// per phase from LDS and store its outputs.  Per phase: the loader waits
+// (counted vmcnt) for phase ph, all four waves pass barrier ph, the loader
+// refills the slots of phase ph - 1 (which the consumers finished,
+// lgkmcnt(0), before that barrier) with phase ph + P - 1.
+template <int P>
+__global__ __launch_bounds__(256) void lpd_lc_kernel(KParams p)
+{
+	extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+	const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+	const int lane = threadIdx.x & 63;
+	const int len = (int)p.ip_len, nch = (len + 15) >> 4;
+	const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)smem);
+	const uint8_t *zero = (const uint8_t *)p.zero + (blockIdx.x & 63) * 64;
+	const uint64_t base = reinterpret_cast<uint64_t>(p.base) + p.l3_off;
+	const uint64_t last_chunk = (base + (p.n - 1) * p.stride + len - 1) & ~(uint64_t)15;
+	// phases of 192 packets, grid-interleaved (workgroup b takes phases b,
+	// b + G, ...), as in the per-wave form
+	const uint64_t NP = (p.n + 191) / 192, G = gridDim.x, b = blockIdx.x;
+	if (b >= NP)
+		return; // uniform across the workgroup
+	const uint64_t nph = (NP - b + G - 1) / G;
+	if (wave == 0) {
+		auto issue = [&](uint64_t ph) {
+			const uint32_t grp = lds0 + (uint32_t)(ph % P) * 3 * 4096;
+#pragma unroll
+			for (int c = 0; c < 3; ++c) {
+				const uint64_t first = (b + ph * G) * 192 + 64 * c;
+				const uint64_t a = base + first * p.stride;
+#pragma unroll
+				for (int i = 0; i < 4; ++i) {
+					const uint64_t src = a + 1024 * i + 16 * lane;
+					glds16_nt(ph < nph && first < p.n && src <= last_chunk ? reinterpret_cast<const void *>(src) : zero,
+						  grp + c * 4096 + 1024 * i);
+				}
+			}
+		};
+#pragma unroll
+		for (int d = 0; d < P - 1; ++d)
+			issue(d);
+		for (uint64_t ph = 0; ph < nph; ++ph) {
+			// phase ph landed: phases ph + 1 .. ph + P - 2 may stay in flight
+			asm volatile("s_waitcnt vmcnt(%0)" ::"i"((P - 2) * 12) : "memory");
+			__builtin_amdgcn_s_barrier();
+			issue(ph + P - 1);
+		}
+		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+	} else {
+		const int c = wave - 1;
+		const int o = lane * (int)p.stride;
+		for (uint64_t ph = 0; ph < nph; ++ph) {
+			__builtin_amdgcn_s_barrier();
+			const uint64_t first = (b + ph * G) * 192 + 64 * c;
+			if (first < p.n) {
+				const uint8_t *sl = smem + ((uint32_t)(ph % P) * 3 + c) * 4096;
+				Quad q;
+#pragma unroll
+				for (int i = 0; i < 4; ++i)
+					q.c[i] = *reinterpret_cast<const uint4 *>(sl + o + 16 * (i < nch ? i : nch - 1));
+				asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+				lpa_reduce<false>(p, first + lane, len, nch, q);
+			}
+			// this phase's slots are refilled after the next barrier
+			asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+		}
+	}
+}
+
+#endif // CGCK_LAB
+
+bool lpd_ok(const KParams &p)
+{
+	return !p.desc && !p.verdict && !p.bad && !(p.flags & CGCK_STORE) && p.ip_len >= 20 && p.ip_len <= 64 &&
+	       p.stride <= 64 && p.stride * 63 + p.ip_len <= 4096 &&
+	       ((reinterpret_cast<uintptr_t>(p.base) | p.stride | p.l3_off) & 15) == 0;
+}
+
+hipError_t launch_lpd(const KParams &p, int num_cus, hipStream_t st)
+{
+	static const int wpc = [] { // $CGCK_LPD_WPC: waves per CU
+		const char *e = getenv("CGCK_LPD_WPC");
+		return e && atoi(e) > 0 ? atoi(e) : 8;
+	}();
+	const uint64_t want = (p.n + 64 * 16 - 1) / (64 * 16); // >= 16 steps per wave
+	const uint64_t cap = (uint64_t)num_cus * wpc;
+	const dim3 g((unsigned)(want < cap ? (want ? want : 1) : cap));
+#if CGCK_LAB
+	static const int depth = [] { // $CGCK_LPD_D: ring slots 2..4
+		const char *e = getenv("CGCK_LPD_D");
+		const int d = e ? atoi(e) : 0;
+		return d >= 2 && d <= 4 ? d : 2;
+	}();
+	static const int lc = [] { // $CGCK_LPD_LC: ring phases of the loader/consumer form (0: per-wave form)
+		const char *e = getenv("CGCK_LPD_LC");
+		const int v = e ? atoi(e) : 0;
+		return v >= 2 && v <= 5 ? v : 0;
+	}();
+	if (lc) {
+		static const int wgpc = [] { // $CGCK_LPD_WGPC: workgroups per CU
+			const char *e = getenv("CGCK_LPD_WGPC");
+			return e && atoi(e) > 0 ? atoi(e) : 3;
+		}();
+		const uint64_t want_lc = (p.n + 192 * 16 - 1) / (192 * 16); // >= 16 phases per workgroup
+		const uint64_t cap_lc = (uint64_t)num_cus * wgpc;
+		const dim3 glc((unsigned)(want_lc < cap_lc ? (want_lc ? want_lc : 1) : cap_lc));
+#define CGCK_LPDLC(PP)                                                                           \
+	do {                                                                                     \
+		CGCK_NOTE_KERNEL("lpd_lc_kernel<%d>", PP);                                       \
+		hipLaunchKernelGGL((lpd_lc_kernel<PP>), glc, dim3(256), (PP) * 3 * 4096, st, p); \
+	} while (0)
+		switch (lc) {
+		case 2: CGCK_LPDLC(2); break;
+		case 4: CGCK_LPDLC(4); break;
+		case 5: CGCK_LPDLC(5); break;
+		default: CGCK_LPDLC(3); break;
+		}
+#undef CGCK_LPDLC
+		return hipGetLastError();
+	}
+	static const bool sink = getenv("CGCK_LPD_SINK") != nullptr; // measure without output stores
+	KParams q = p;
+	if (sink)
+		q.contig = 2;
+	static const int chunk = [] { // $CGCK_LPD_C: steps per output chunk (1, 4, 8, 16, 32, 64)
+		const char *e = getenv("CGCK_LPD_C");
+		const int c = e ? atoi(e) : 32;
+		return c == 1 || c == 4 || c == 8 || c == 16 || c == 64 ? c : 32;
+	}();
+	static const int sp = [] { // $CGCK_LPD_SP: flush store policy 0 nt, 1 default, 2 sc1
+		const char *e = getenv("CGCK_LPD_SP");
+		const int v = e ? atoi(e) : 2;
+		return v >= 0 && v <= 2 ? v : 2;
+	}();
+#define CGCK_LPD_S(DD, CC, SS)                                                                   \
+	do {                                                                                     \
+		CGCK_NOTE_KERNEL("lpd_kernel<%d, %d, %d>", DD, CC, SS);                          \
+		hipLaunchKernelGGL((lpd_kernel<DD, CC, SS>), g, dim3(64), (DD) * 4096 + (CC) * 256, st, q); \
+	} while (0)
+#define CGCK_LPD(DD, CC)                                                                         \
+	do {                                                                                     \
+		if (sp == 1)                                                                     \
+			CGCK_LPD_S(DD, CC, 1);                                                   \
+		else if (sp == 0)                                                                \
+			CGCK_LPD_S(DD, CC, 0);                                                   \
+		else                                                                             \
+			CGCK_LPD_S(DD, CC, 2);                                                   \
+	} while (0)
+#define CGCK_LPD_D(DD)                                                                           \
+	do {                                                                                     \
+		if (chunk == 1)                                                                  \
+			CGCK_LPD(DD, 1);                                                         \
+		else if (chunk == 4)                                                             \
+			CGCK_LPD(DD, 4);                                                         \
+		else if (chunk == 8)                                                             \
+			CGCK_LPD(DD, 8);                                                         \
+		else if (chunk == 16)                                                            \
+			CGCK_LPD(DD, 16);                                                        \
+		else if (chunk == 64)                                                            \
+			CGCK_LPD(DD, 64);                                                        \
+		else                                                                             \
+			CGCK_LPD(DD, 32);                                                        \
+	} while (0)
+	switch (depth) {
+	case 3: CGCK_LPD_D(3); break;
+	case 4: CGCK_LPD_D(4); break;
+	default: CGCK_LPD_D(2); break;
+	}
+#undef CGCK_LPD_D
+#undef CGCK_LPD
+#undef CGCK_LPD_S
+#else
+	CGCK_NOTE_KERNEL("lpd_kernel<2, 32, 2>");
+	hipLaunchKernelGGL((lpd_kernel<2, 32, 2>), g, dim3(64), 2 * 4096 + 32 * 256, st, p);
+#endif
+	return hipGetLastError();
 }
 
 hipError_t launch_lpa(const KParams &p, int num_cus, bool nt, hipStream_t st)

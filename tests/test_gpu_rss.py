@@ -87,6 +87,21 @@ def test_batch_shapes(engine, port, n, stride, cnt, off, ks):
     assert np.array_equal(out, exp)
 
 
+@pytest.mark.parametrize("mask", [0xFFFFFFFF, 0x7F])
+def test_batch_dense_ring_wrap(engine, port, mask):
+    """The default dense-tuple kernel (toeplitz12x4_ab_kernel<12>, one block per
+    CU) over more 256-group chunks than its register ring holds per block, a
+    partial last chunk and an n % 4 tail handed to the per-record kernel:
+    n = 4*256*CUs*13 + 4*37 + 3 with CUs = 256 (MI355X), compared in full."""
+    n = 4 * 256 * 256 * 13 + 4 * 37 + 3
+    rng = np.random.default_rng(1213)
+    host = rng.integers(0, 256, 12 * n, dtype=np.uint8)
+    key = rng.integers(0, 256, 40, dtype=np.uint8)
+    out = run_batch(engine, host, n, 12, 12, key, mask=mask)
+    exp = port.toeplitz_batch(host, n, 12, 12, key, mask=mask)
+    assert np.array_equal(out, exp)
+
+
 def test_batch_empty(engine, g):
     key = hexa(g["freebsd_rss_key"])
     engine.toeplitz(None, 0, 12, 12, key, None)

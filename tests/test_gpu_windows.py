@@ -242,5 +242,9 @@ def test_last_kernel_names(engine):
     engine.strided(buf.ptr, n, 1500, 0, 1500, cgck.GEN_BOTH, out.ptr)
     assert engine.last_kernel == "cksum_kernel<16, 6, 1, false, true>"
     engine.strided(buf.ptr, n, 64, 0, 64, cgck.GEN_BOTH, out.ptr)
+    assert engine.last_kernel == "lpd_kernel<2, 32, 2>"
+    ver = cgck.DeviceBuffer(n)
+    engine.strided(buf.ptr, n, 64, 0, 64, cgck.GEN_BOTH, out.ptr, ver.ptr)   # verdicts: lpa
     assert engine.last_kernel.startswith("lpa_kernel<false, ")
     engine.sync()
+    ver.free()
