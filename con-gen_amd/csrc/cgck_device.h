@@ -164,6 +164,43 @@ __device__ __forceinline__ void glds16_nt(const void *gsrc, uint32_t lds_dst)
 		     : "memory");
 }
 
+// Write count u32 outputs staged in LDS (src) to global dst, threads t of nt
+// cooperating.  CGCK_FLUSH_POLICY (A/B builds): 0 nontemporal u32 stores, 1 u32
+// with sc1, 2 16-byte stores with sc1 (dst aligned up by a u32 head, u32
+// tail), 3 16-byte nontemporal stores.  Stores through inline asm are
+// invisible to the compiler's vmcnt accounting; since the counter retires in
+// order, an extra store only makes its waits stricter.
+#ifndef CGCK_FLUSH_POLICY
+#define CGCK_FLUSH_POLICY 0
+#endif
+__device__ __forceinline__ void flush_u32(const uint32_t *src, uint32_t *dst, int count, int t, int nt)
+{
+#if CGCK_FLUSH_POLICY == 0
+	for (int i = t; i < count; i += nt)
+		__builtin_nontemporal_store(src[i], (CGCK_GLOBAL uint32_t *)dst + i);
+#elif CGCK_FLUSH_POLICY == 1
+	for (int i = t; i < count; i += nt)
+		asm volatile("global_store_dword %0, %1, off sc1" ::"v"(dst + i), "v"(src[i]) : "memory");
+#else
+	int head = (int)(((16 - ((uintptr_t)dst & 15)) & 15) >> 2);
+	head = head < count ? head : count;
+	if (t < head)
+		asm volatile("global_store_dword %0, %1, off sc1" ::"v"(dst + t), "v"(src[t]) : "memory");
+	const int body = (count - head) >> 2;
+	for (int i = t; i < body; i += nt) {
+		const uint32_t *s4 = src + head + 4 * i;
+		const u32x4_t v = {s4[0], s4[1], s4[2], s4[3]};
+#if CGCK_FLUSH_POLICY == 3
+		asm volatile("global_store_dwordx4 %0, %1, off nt" ::"v"(dst + head + 4 * i), "v"(v) : "memory");
+#else
+		asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(dst + head + 4 * i), "v"(v) : "memory");
+#endif
+	}
+	for (int i = head + 4 * body + t; i < count; i += nt)
+		asm volatile("global_store_dword %0, %1, off sc1" ::"v"(dst + i), "v"(src[i]) : "memory");
+#endif
+}
+
 template <bool NT>
 __device__ __forceinline__ uint4 ld(const uint4 *p)
 {

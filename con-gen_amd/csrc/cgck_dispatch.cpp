@@ -48,6 +48,7 @@ hipError_t launch_slot(const KParams &p, int num_cus, bool nt, hipStream_t st);
 hipError_t launch_lppp(const KParams &p, int num_cus, bool nt, hipStream_t st);
 hipError_t launch_stream(const KParams &p, int num_cus, hipStream_t st);
 bool stream_ok(const KParams &p);
+hipError_t launch_slotd(const KParams &p, int num_cus, hipStream_t st);
 #endif
 
 // `kernel` = variant | flags (include/cgck.h is agnostic of this; $CGCK_KERNEL
@@ -62,7 +63,8 @@ bool stream_ok(const KParams &p);
 //     lane per packet, 5..8 lpp shapes 1..3, 0, 11 the lane-group kernel fed
 //     by LDS-DMA, 12 the packed span (descriptor batches whose frames lie back
 //     to back: coalesced stream + prefix sums, cgck_span.hip; picked under the
-//     lab's packed layout hint).  A variant this build lacks falls back to the
+//     lab's packed layout hint), 14 lane per slot fed by LDS-DMA (slotd).  A
+//     variant this build lacks falls back to the
 //     automatic choice; one whose preconditions a batch fails falls back to
 //     lpa, lpp or group;
 //   kNT (bit 4) nontemporal loads, kContig (bit 5) contiguous block ranges,
@@ -80,7 +82,7 @@ hipError_t launch_cksum(const KParams &p0, uint32_t len_hint, int num_cus, int k
 	const bool lpa_ok = lane_ok && !p.desc && p.ip_len >= 20 && p.ip_len <= 64 &&
 			    ((reinterpret_cast<uintptr_t>(p.base) | p.stride | p.l3_off) & 15) == 0;
 #if CGCK_LAB
-	const bool known = variant <= 13;
+	const bool known = variant <= 14;
 	const bool packed = (kernel & kPacked) && span_ok(p);
 #else
 	const bool known = variant == 1 || variant == 2 || variant == 9 || variant == 10 || variant == 13;
@@ -139,6 +141,8 @@ hipError_t launch_cksum(const KParams &p0, uint32_t len_hint, int num_cus, int k
 		return launch_lpp(p, num_cus, nt, 0, st);
 	case 11:
 		return launch_stream(p, num_cus, st);
+	case 14:
+		return launch_slotd(p, num_cus, st);
 #endif
 	default:
 		return launch_group(p, len_hint, num_cus, nt, st);

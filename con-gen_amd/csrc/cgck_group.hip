@@ -44,8 +44,8 @@ __device__ __forceinline__ void cksum_body(const KParams &p)
 	auto flush = [&](uint64_t e) {        // block-uniform call
 		__syncthreads();
 		const uint64_t end = e < p.n ? e : p.n;
-		for (uint64_t i = threadIdx.x; wb + i < end; i += 256)
-			__builtin_nontemporal_store(so[i], gbl(p.out) + wb + i);
+		if (end > wb)
+			flush_u32(so, p.out + wb, (int)(end - wb), threadIdx.x, 256);
 		__syncthreads();
 		wb = e;
 	};

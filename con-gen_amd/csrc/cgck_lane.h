@@ -289,12 +289,11 @@ __device__ __forceinline__ void wave_stage_flush(const KParams &p, WaveStage &s,
 	__builtin_amdgcn_wave_barrier();
 	asm volatile("" ::: "memory");
 	const int c = (int)(e - s.sb);
-	for (int i = l; i < c; i += 64) {
-		if (p.out)
-			__builtin_nontemporal_store(s.so[i], gbl(p.out) + s.sb + i);
-		if (p.verdict)
+	if (p.out)
+		flush_u32(s.so, p.out + s.sb, c, l, 64);
+	if (p.verdict)
+		for (int i = l; i < c; i += 64)
 			gbl(p.verdict)[s.sb + i] = s.sv[i];
-	}
 	__builtin_amdgcn_wave_barrier();
 	asm volatile("" ::: "memory");
 	s.sb = e;

@@ -1005,6 +1005,9 @@ __device__ __forceinline__ void slot_reduce(const KParams &p, uint64_t cur, cons
 		wave_stage_put(ws, cur + M.owner, result(p, a0, len, fold16(r), h));
 }
 
+#ifndef CGCK_SLOT2_CHUNK
+#define CGCK_SLOT2_CHUNK 0
+#endif
 template <bool DESC, bool NT>
 __global__ __launch_bounds__(256) void slot2_kernel(KParams p)
 {
@@ -1014,11 +1017,18 @@ __global__ __launch_bounds__(256) void slot2_kernel(KParams p)
 	const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63; // wave-uniform (SGPR)
 	const uint64_t nwaves = (uint64_t)gridDim.x * 4;
 	const uint64_t wid = (uint64_t)blockIdx.x * 4 + wv;
+#if CGCK_SLOT2_CHUNK
+	// chunks of CGCK_SLOT2_CHUNK packets, grid-interleaved (A/B builds)
+	for (uint64_t ck = wid; ck * CGCK_SLOT2_CHUNK < p.n; ck += nwaves) {
+	const uint64_t r0 = ck * CGCK_SLOT2_CHUNK;
+	const uint64_t r1 = r0 + CGCK_SLOT2_CHUNK < p.n ? r0 + CGCK_SLOT2_CHUNK : p.n;
+#else
 	const uint64_t per = (p.n + nwaves - 1) / nwaves;
 	const uint64_t r0 = wid * per;
 	const uint64_t r1 = r0 + per < p.n ? r0 + per : p.n;
 	if (r0 >= r1)
 		return;
+#endif
 	WaveStage ws{so[wv], sv[wv], r0};
 
 	// prologue: map A, desc of B, chunks of A
@@ -1050,7 +1060,117 @@ __global__ __launch_bounds__(256) void slot2_kernel(KParams p)
 		curB = curD;
 	}
 	wave_stage_flush(p, ws, r1);
+#if CGCK_SLOT2_CHUNK
+	}
+#endif
 }
+
+#if CGCK_LAB
+// --------------------------------------------------------------------------
+// Lane per 128-byte slot fed by LDS-DMA (slotd: IMIX, A/B against slot2)
+// --------------------------------------------------------------------------
+//
+// slot2's register loads sit at the register-load read ceiling (the probe on
+// the same buffer: 71.6-73.1 %), while grid-interleaved LDS-DMA reads run near
+// the HBM peak (lpd_kernel).  Same slot map as slot2 (smap); each step's slots
+// are moved by 8 DMA instructions into an 8 KiB LDS slot of a 2-deep ring:
+// instruction i, lane l moves chunk (l & 7) of slot 8 i + (l >> 3), so an
+// instruction reads up to 1 KiB contiguous of one packet and slot s lands at
+// +128 s.  Lane s then reads its 8 chunks back from LDS and reduces them with
+// slot_reduce.  One wave per workgroup; chunks of kSlotdChunk descriptors are
+// grid-interleaved.  Descriptor loads are the compiler's (its vmcnt waits for
+// them also cover the DMA issued before, which only makes them stricter); the
+// wait for a step's DMA is explicit: only the next step's 8 DMA stay in flight.
+constexpr int kSlotdChunk = 2048;
+
+template <bool NT>
+__device__ __forceinline__ void slotd_issue(const KParams &p, const SMap &M, bool live, uint32_t lds_slot,
+					    const uint8_t *zero)
+{
+	const int l = threadIdx.x & 63;
+	// per slot (lane sigma of M): its first chunk and the chunks it holds
+	const uint64_t cb = (M.a0 & ~(uint64_t)15) + 128 * (uint64_t)M.s;
+	int rem = M.nch - 8 * M.s;
+	rem = !live || !M.act || M.m == 0 ? 0 : rem < 0 ? 0 : rem > 8 ? 8 : rem;
+	const uint32_t cb_lo = (uint32_t)cb, cb_hi = (uint32_t)(cb >> 32);
+	const int c = l & 7;
+#pragma unroll
+	for (int i = 0; i < 8; ++i) {
+		const int sg = 8 * i + (l >> 3);
+		const uint32_t lo = __shfl(cb_lo, sg, 64), hi = __shfl(cb_hi, sg, 64);
+		const int r = __shfl(rem, sg, 64);
+		const uint64_t src = ((uint64_t)hi << 32 | lo) + 16 * (uint64_t)(c < r ? c : r - 1);
+		glds16_nt(r > 0 ? reinterpret_cast<const void *>(src) : zero, lds_slot + 1024 * i);
+	}
+}
+
+template <bool DESC>
+__global__ __launch_bounds__(64) void slotd_kernel(KParams p)
+{
+	extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+	uint32_t *mark = reinterpret_cast<uint32_t *>(smem + 2 * 8192);
+	uint32_t *so = mark + 64;
+	uint8_t *sv = reinterpret_cast<uint8_t *>(so + kWaveStage);
+	const int l = threadIdx.x & 63;
+	const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)smem);
+	const uint8_t *zero = (const uint8_t *)p.zero + (blockIdx.x & 63) * 64;
+	for (uint64_t ck = blockIdx.x; ck * kSlotdChunk < p.n; ck += gridDim.x) {
+		const uint64_t r0 = ck * kSlotdChunk;
+		const uint64_t r1 = r0 + kSlotdChunk < p.n ? r0 + kSlotdChunk : p.n;
+		WaveStage ws{so, sv, r0};
+		uint64_t cur = r0;
+		SMap M = smap<DESC>(p, cur, r1, load_desc<DESC>(p, cur + l, r1), *reinterpret_cast<uint32_t(*)[64]>(mark));
+		slotd_issue<false>(p, M, true, lds0, zero);
+		uint64_t curN = cur + (M.m ? M.m : 1);
+		DescW dN = load_desc<DESC>(p, curN + l, r1);
+		for (uint32_t j = 0;; ++j) {
+			const SMap MN = smap<DESC>(p, curN, r1, dN, *reinterpret_cast<uint32_t(*)[64]>(mark));
+			const uint64_t curNN = curN + (MN.m ? MN.m : 1);
+			const DescW dNN = load_desc<DESC>(p, curNN + l, r1);
+			slotd_issue<false>(p, MN, curN < r1, lds0 + ((j + 1) & 1) * 8192, zero);
+			// step j's DMA (and everything before it) has landed: only the
+			// next step's 8 DMA may stay in flight
+			asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+			__builtin_amdgcn_s_barrier();
+			const uint4 *sl = reinterpret_cast<const uint4 *>(smem + (j & 1) * 8192) + 8 * l;
+			uint4 w[8];
+#pragma unroll
+			for (int i = 0; i < 8; ++i)
+				w[i] = sl[i];
+			asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // the slot is refilled next step
+			slot_reduce<false>(p, cur, M, w, ws);
+			if (curN >= r1)
+				break;
+			cur = curN;
+			M = MN;
+			curN = curNN;
+			dN = dNN;
+		}
+		wave_stage_flush(p, ws, r1);
+		asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // the last (zero) DMA landed before the ring is reused
+	}
+}
+
+hipError_t launch_slotd(const KParams &p, int num_cus, hipStream_t st)
+{
+	static const int wpc = [] { // $CGCK_SLOTD_WPC: waves per CU
+		const char *e = getenv("CGCK_SLOTD_WPC");
+		return e && atoi(e) > 0 ? atoi(e) : 6;
+	}();
+	const uint64_t want = (p.n + kSlotdChunk - 1) / kSlotdChunk;
+	const uint64_t cap = (uint64_t)num_cus * wpc;
+	const dim3 g((unsigned)(want < cap ? (want ? want : 1) : cap));
+	const size_t lds = 2 * 8192 + 64 * 4 + kWaveStage * 4 + kWaveStage;
+	if (p.desc) {
+		CGCK_NOTE_KERNEL("slotd_kernel<true>");
+		hipLaunchKernelGGL((slotd_kernel<true>), g, dim3(64), lds, st, p);
+	} else {
+		CGCK_NOTE_KERNEL("slotd_kernel<false>");
+		hipLaunchKernelGGL((slotd_kernel<false>), g, dim3(64), lds, st, p);
+	}
+	return hipGetLastError();
+}
+#endif // CGCK_LAB
 
 // --------------------------------------------------------------------------
 // Launchers

@@ -46,7 +46,10 @@
 namespace cgck {
 
 constexpr int kStrS = 6;                    // DMA instructions (KiB) per step
-constexpr int kStrWin = 64;                 // steps per output window
+#ifndef CGCK_STR_WIN
+#define CGCK_STR_WIN 64
+#endif
+constexpr int kStrWin = CGCK_STR_WIN;       // steps per output window
 constexpr uint32_t kStrSlot = kStrS * 1024; // bytes per slot
 
 // DMA of the region of the step starting at packet `first` into a slot.
@@ -101,6 +104,8 @@ __global__ __launch_bounds__(64) void stream_kernel(KParams p)
 				  lds0 + (uint32_t)((j + kStrD - 1) % kStrD) * kStrSlot);
 			asm volatile("s_waitcnt vmcnt(%0)" ::"i"((kStrD - 1) * kStrS) : "memory");
 			__builtin_amdgcn_s_barrier();
+			if (p.contig == 3) // $CGCK_STR_NOCONS: the DMA pipeline alone (A/B)
+				continue;
 
 			const uint64_t first = r0 + 4 * (w0 + j);
 			const uint64_t a_reg = (base + first * p.stride) & ~(uint64_t)15;
@@ -353,16 +358,20 @@ hipError_t launch_stream(const KParams &p, int num_cus, hipStream_t st)
 		const char *e = getenv("CGCK_STR_RING");
 		return e && atoi(e) >= 2 && atoi(e) <= 4 ? atoi(e) : 3;
 	}();
+	static const bool nocons = getenv("CGCK_STR_NOCONS") != nullptr;
+	KParams q = p;
+	if (nocons)
+		q.contig = 3;
 	const uint64_t waves = (uint64_t)num_cus * wpc;
 	const uint64_t want = (p.n + 63) / 64; // at least 16 steps per wave
 	const dim3 g((unsigned)(want < waves ? (want ? want : 1) : waves));
 	const size_t lds = ring * kStrSlot + 4 * kStrWin * 4 + 4 * kStrWin;
 	if (ring == 2)
-		hipLaunchKernelGGL(stream_kernel<2>, g, dim3(64), lds, st, p);
+		hipLaunchKernelGGL(stream_kernel<2>, g, dim3(64), lds, st, q);
 	else if (ring == 4)
-		hipLaunchKernelGGL(stream_kernel<4>, g, dim3(64), lds, st, p);
+		hipLaunchKernelGGL(stream_kernel<4>, g, dim3(64), lds, st, q);
 	else
-		hipLaunchKernelGGL(stream_kernel<3>, g, dim3(64), lds, st, p);
+		hipLaunchKernelGGL(stream_kernel<3>, g, dim3(64), lds, st, q);
 	return hipGetLastError();
 }
 

@@ -3,6 +3,7 @@
 # runs into con-gen_amd/<name>.so (git-ignored).  Host side only.
 #   tools/build_variant.sh NAME FILE 'SED-EXPR'   working tree + one sed edit
 #   tools/build_variant.sh NAME --rev REV         the sources of git revision REV
+#   tools/build_variant.sh NAME --tree            the working tree as it is (with $VARIANT_FLAGS)
 set -eu
 NAME=$1
 R=$(cd "$(dirname "$0")/.." && pwd)
@@ -10,6 +11,9 @@ T=$(mktemp -d /tmp/cgck_variant.XXXXXX)
 mkdir -p "$T/con-gen_amd"
 if [ "$2" = "--rev" ]; then
 	(cd "$R" && git archive "$3" con-gen_amd/csrc include) | tar -x -C "$T"
+elif [ "$2" = "--tree" ]; then
+	cp -r "$R/con-gen_amd/csrc" "$T/con-gen_amd/csrc"
+	ln -s "$R/include" "$T/include"
 else
 	FILE=$2; EXPR=$3
 	cp -r "$R/con-gen_amd/csrc" "$T/con-gen_amd/csrc"

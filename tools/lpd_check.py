@@ -37,6 +37,32 @@ def main():
     if preset == "mtu":
         shapes = [(16 << 20, 1500, 1500), (1000003, 1500, 1500), (777, 1500, 1500), (5, 1500, 1500),
                   (300001, 1504, 1499), (100000, 1024, 1000), (4097, 1516, 1516), (123457, 576, 576)]
+    if preset == "imix":   # descriptor batches: the synthetic IMIX set (BASELINE configs[3])
+        for n in (16 << 20, 100003, 4097, 65, 1):
+            nbytes = cgck.load().cgck_imix_bytes(n)
+            buf, desc = cgck.DeviceBuffer(nbytes), cgck.DeviceBuffer(12 * n)
+            e0.synth_imix(buf.ptr, desc.ptr, n, 0xC0C0 + n)
+            outs = {v: cgck.DeviceBuffer(4 * n) for v in engines}
+            for name, fl in (("GEN_BOTH", cgck.GEN_BOTH), ("RAW", cgck.RAW), ("VERIFY_BSD", cgck.VERIFY_BSD)):
+                got = {}
+                for v, e in engines.items():
+                    e.set_desc_len_hint(nbytes // n)
+                    e.desc(buf.ptr, desc.ptr, n, fl, outs[v].ptr)
+                    got[v] = np.zeros(n, np.uint32)
+                    outs[v].download(got[v], stream=e.stream)
+                    e.sync()
+                    kern = e.last_kernel
+                diff = int(np.count_nonzero(got[ref] != got[cand]))
+                chk = ""
+                if name == "GEN_BOTH":
+                    bad, cnt = P.check_synth_imix(n, 0xC0C0 + n, cgck.GEN_BOTH, got[cand], 7)
+                    chk = f" oracle {bad}/{cnt}"
+                    diff += bad
+                bad_total += diff
+                print(f"imix n={n} {name}: {cand} vs {ref} mismatches {diff}{chk} ({kern})", flush=True)
+            for b in list(outs.values()) + [buf, desc]:
+                b.free()
+        shapes = []
     flag_sets = [("GEN_BOTH", cgck.GEN_BOTH), ("RAW", cgck.RAW), ("IP", cgck.IP),
                  ("L4", cgck.L4), ("GEN_NOPSEUDO", cgck.IP | cgck.L4 | cgck.L4_NOPSEUDO)]
     for n, stride, ln in shapes:
