@@ -49,6 +49,8 @@ hipError_t launch_lppp(const KParams &p, int num_cus, bool nt, hipStream_t st);
 hipError_t launch_stream(const KParams &p, int num_cus, hipStream_t st);
 bool stream_ok(const KParams &p);
 hipError_t launch_slotd(const KParams &p, int num_cus, hipStream_t st);
+hipError_t launch_lpw(const KParams &p, int num_cus, hipStream_t st);
+bool lpw_ok(const KParams &p);
 #endif
 
 // `kernel` = variant | flags (include/cgck.h is agnostic of this; $CGCK_KERNEL
@@ -63,7 +65,8 @@ hipError_t launch_slotd(const KParams &p, int num_cus, hipStream_t st);
 //     lane per packet, 5..8 lpp shapes 1..3, 0, 11 the lane-group kernel fed
 //     by LDS-DMA, 12 the packed span (descriptor batches whose frames lie back
 //     to back: coalesced stream + prefix sums, cgck_span.hip; picked under the
-//     lab's packed layout hint), 14 lane per slot fed by LDS-DMA (slotd).  A
+//     lab's packed layout hint), 14 lane per slot fed by LDS-DMA (slotd), 15 lane per
+//     packet over DMA'd windows of the step's span (lpw).  A
 //     variant this build lacks falls back to the
 //     automatic choice; one whose preconditions a batch fails falls back to
 //     lpa, lpp or group;
@@ -82,7 +85,7 @@ hipError_t launch_cksum(const KParams &p0, uint32_t len_hint, int num_cus, int k
 	const bool lpa_ok = lane_ok && !p.desc && p.ip_len >= 20 && p.ip_len <= 64 &&
 			    ((reinterpret_cast<uintptr_t>(p.base) | p.stride | p.l3_off) & 15) == 0;
 #if CGCK_LAB
-	const bool known = variant <= 14;
+	const bool known = variant <= 15;
 	const bool packed = (kernel & kPacked) && span_ok(p);
 #else
 	const bool known = variant == 1 || variant == 2 || variant == 9 || variant == 10 || variant == 13;
@@ -101,6 +104,8 @@ hipError_t launch_cksum(const KParams &p0, uint32_t len_hint, int num_cus, int k
 	if (variant == 12 && !span_ok(p))
 		variant = 1;
 	if (variant == 11 && !stream_ok(p))
+		variant = 1;
+	if (variant == 15 && !lpw_ok(p))
 		variant = 1;
 #endif
 	bool nt, contig;
@@ -143,6 +148,8 @@ hipError_t launch_cksum(const KParams &p0, uint32_t len_hint, int num_cus, int k
 		return launch_stream(p, num_cus, st);
 	case 14:
 		return launch_slotd(p, num_cus, st);
+	case 15:
+		return launch_lpw(p, num_cus, st);
 #endif
 	default:
 		return launch_group(p, len_hint, num_cus, nt, st);

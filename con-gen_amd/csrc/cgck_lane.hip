@@ -1151,6 +1151,280 @@ __global__ __launch_bounds__(64) void slotd_kernel(KParams p)
 	}
 }
 
+// --------------------------------------------------------------------------
+// Lane per packet over DMA'd windows of the batch's own span (lpw: IMIX)
+// --------------------------------------------------------------------------
+//
+// A step is 64 consecutive descriptors, one per lane.  When their chunk
+// ranges chain (each packet starts at or before the furthest end so far, in
+// address order: a packed batch such as the IMIX set), every chunk of the
+// step's span [S, E) belongs to one of them, so the span is streamed with
+// contiguous DMA in windows of kLpwWin chunks (+64 chunks of overlap so a
+// header that starts near a window's end is complete) through a 2-deep LDS
+// ring, and lane L sums the chunks of its own packet that fall in each
+// window.  No slot map: a step's descriptors do not depend on the previous
+// step, and they travel by DMA with the data (768 B, one instruction, into
+// a 2-deep descriptor ring), two steps ahead, so no wait in the loop is on a
+// compiler-tracked load.  Every round issues kLpwDma + 1 DMA instructions
+// (zero lines where there is nothing to move), so the waits are counted.
+// Steps that do not chain are computed from global memory by the same lanes.
+constexpr int kLpwDma = 8;                       // data DMA instructions per window
+constexpr int kLpwWin = kLpwDma * 64 - 64;       // chunks a window owns (448)
+constexpr int kLpwSlot = kLpwDma * 1024;         // bytes per ring slot
+
+struct LpwStep {
+	uint64_t a0;
+	int len, q, nch, e;
+	bool ok;
+	uint64_t cs, ce; // absolute chunk range of the lane's packet
+	uint64_t S, E;   // wave: span
+	uint32_t nwin;   // wave: windows (0: not chained, computed from global memory)
+};
+
+template <bool DESC>
+__device__ __forceinline__ LpwStep lpw_step(const KParams &p, uint64_t first, const DescW &d)
+{
+	const int l = threadIdx.x & 63;
+	const Pkt pk = decode<DESC>(p, first + l, p.n, d);
+	LpwStep s;
+	s.a0 = pk.a0;
+	s.len = (int)pk.len;
+	s.ok = pk.ok;
+	s.q = (int)(pk.a0 & 15);
+	s.nch = nchunks(pk.a0, pk.len);
+	s.e = s.q + s.len - 16 * (s.nch - 1);
+	s.cs = pk.a0 >> 4;
+	s.ce = s.cs + (uint64_t)s.nch;
+	// Over the non-empty packets in lane order: running maxima of the starts
+	// and of the ends (inclusive scans, then shifted by one lane).  The step
+	// chains when every start is >= the starts before it and <= the furthest
+	// end before it: then [S, E) is exactly the union of the packets' chunks.
+	const bool ne = s.ok && s.nch > 0;
+	uint64_t mE = ne ? s.ce : 0, mS = ne ? s.cs : 0;
+#pragma unroll
+	for (int d2 = 1; d2 < 64; d2 <<= 1) {
+		const uint64_t yE = shfl64(mE, l >= d2 ? l - d2 : l), yS = shfl64(mS, l >= d2 ? l - d2 : l);
+		if (l >= d2) {
+			mE = yE > mE ? yE : mE;
+			mS = yS > mS ? yS : mS;
+		}
+	}
+	const uint64_t prev_e = shfl64(mE, l > 0 ? l - 1 : 0), prev_s = shfl64(mS, l > 0 ? l - 1 : 0);
+	const uint64_t nonempty = __ballot(ne);
+	const int f = nonempty ? __ffsll((long long)nonempty) - 1 : 0; // first non-empty lane
+	const bool brk = ne && l > f && (s.cs < prev_s || s.cs > prev_e);
+	s.S = nonempty ? shfl64(s.cs, f) : 0;
+	s.E = nonempty ? shfl64(mE, 63) : 0;
+	const uint64_t span = s.E - s.S;
+	s.nwin = __any(brk) || span > 16 * kLpwWin ? 0u : (uint32_t)((span + kLpwWin - 1) / kLpwWin);
+	if (!__any(brk) && span == 0)
+		s.nwin = 1; // a step of empty packets: one window, nothing moved
+	return s;
+}
+
+// One round: window t of step s (live) or zero lines, plus the descriptors
+// of step dstep (when dlive) into the descriptor slot.
+template <bool DESC>
+__device__ __forceinline__ void lpw_issue(const KParams &p, uint64_t wb, uint64_t E, bool live, uint32_t lds_slot,
+					  uint64_t dfirst, bool dlive, uint32_t lds_dslot, const uint8_t *zero)
+{
+	// window [wb, wb + 512) of a span ending at E (values, not a step
+	// reference: selecting between two steps' structs put them in scratch)
+	const int l = threadIdx.x & 63;
+	const uint32_t base = __builtin_amdgcn_readfirstlane(lds_slot); // wave-uniform: M0
+#pragma unroll
+	for (int i = 0; i < kLpwDma; ++i) {
+		const uint64_t c = wb + 64 * i + l;
+		glds16_nt(live && c < E ? reinterpret_cast<const void *>(c << 4) : zero, base + 1024 * i);
+	}
+	const uint64_t doff = 12 * dfirst + 16 * (uint64_t)l;
+	const bool dok = DESC && dlive && l < 48 && doff < 12 * p.n;
+	glds16_nt(dok ? reinterpret_cast<const void *>(reinterpret_cast<const uint8_t *>(p.desc) + doff) : zero,
+		  __builtin_amdgcn_readfirstlane(lds_dslot));
+}
+
+template <bool DESC>
+__device__ __forceinline__ DescW lpw_desc_lds(const uint8_t *dslot)
+{
+	DescW d{0, 0, 0};
+	if (DESC) {
+		const uint32_t *q = reinterpret_cast<const uint32_t *>(dslot) + 3 * (threadIdx.x & 63);
+		d.lo = q[0];
+		d.hi = q[1];
+		d.w2 = q[2];
+	}
+	return d;
+}
+
+template <bool DESC, int C>
+__global__ __launch_bounds__(64) void lpw_kernel(KParams p)
+{
+	extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+	uint8_t *dring = smem + 2 * kLpwSlot; // 2 x 1 KiB descriptor slots (64 lanes x 16 B; 768 B used)
+	uint32_t *so = reinterpret_cast<uint32_t *>(dring + 2 * 1024);
+	uint8_t *sv = reinterpret_cast<uint8_t *>(so + C * 64);
+	const int l = threadIdx.x & 63;
+	const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)smem);
+	const uint32_t ldsd = lds0 + 2 * kLpwSlot;
+	const uint8_t *zero = (const uint8_t *)p.zero + (blockIdx.x & 63) * 64;
+	const uint64_t NS = (p.n + 63) / 64, NC = (NS + C - 1) / C, G = gridDim.x, b = blockIdx.x;
+	if (b >= NC)
+		return;
+	const uint64_t nsteps = (NC - b + G - 1) / G * C;
+	auto gstep = [&](uint64_t j) { return (b + (j / C) * G) * C + j % C; };
+	auto first_of = [&](uint64_t j) { return j < nsteps ? gstep(j) * 64 : p.n; };
+
+	LpwStep cur = lpw_step<DESC>(p, first_of(0), load_desc<DESC>(p, first_of(0) + l, p.n));
+	LpwStep nxt = lpw_step<DESC>(p, first_of(1), load_desc<DESC>(p, first_of(1) + l, p.n));
+	LpwStep nn = nxt;
+	uint32_t kiss = 0;      // rounds issued (round k uses data slot k & 1)
+	bool pre = false;       // cur's window 0 (with step j + 2's descriptors) already issued
+	for (uint64_t j = 0; j < nsteps; ++j) {
+		const uint64_t first = first_of(j);
+		uint32_t acc = 0, corr = 0;
+		Hdr h{};
+		if (first < p.n && cur.nwin > 0) {
+			if (!pre) {
+				lpw_issue<DESC>(p, cur.S, cur.E, true, lds0 + (kiss & 1) * kLpwSlot, first_of(j + 2), first_of(j + 2) < p.n,
+						ldsd + (uint32_t)((j + 2) & 1) * 1024, zero);
+				++kiss;
+			}
+			for (uint32_t t = 0; t < cur.nwin; ++t) {
+				// the next round: this step's next window, or the next step's first
+				// (carrying the descriptors of step j + 3)
+				const bool more = t + 1 < cur.nwin;
+				const bool nx = !more && first_of(j + 1) < p.n && nxt.nwin > 0;
+				const uint64_t iwb = more ? cur.S + (uint64_t)(t + 1) * kLpwWin : nxt.S;
+				const uint64_t iE = more ? cur.E : nxt.E;
+				lpw_issue<DESC>(p, iwb, iE, more || nx, lds0 + (kiss & 1) * kLpwSlot,
+						first_of(j + 3), !more && first_of(j + 3) < p.n,
+						ldsd + (uint32_t)((j + 3) & 1) * 1024, zero);
+				++kiss;
+				pre = nx;
+				asm volatile("s_waitcnt vmcnt(%0)" ::"i"(kLpwDma + 1) : "memory");
+				__builtin_amdgcn_s_barrier();
+				if (t == 0) // step j + 2's descriptors came with window 0 of this step
+					nn = lpw_step<DESC>(p, first_of(j + 2), lpw_desc_lds<DESC>(dring + ((j + 2) & 1) * 1024));
+				const uint4 *win = reinterpret_cast<const uint4 *>(smem + (kiss & 1) * kLpwSlot); // round kiss - 2
+				const uint64_t wb = cur.S + (uint64_t)t * kLpwWin;
+				const uint64_t we = wb + kLpwWin;
+				const uint64_t lo = cur.cs > wb ? cur.cs : wb;
+				const uint64_t hi = cur.ce < we ? cur.ce : we;
+				const int cnt = cur.ok && hi > lo ? (int)(hi - lo) : 0;
+				const int o = (int)(lo - wb);
+				int i = 0;
+				for (; __any(i + 4 <= cnt); i += 4) {
+					uint4 v[4];
+#pragma unroll
+					for (int u = 0; u < 4; ++u)
+						v[u] = win[o + (i + u < cnt ? i + u : 0)];
+#pragma unroll
+					for (int u = 0; u < 4; ++u)
+						acc = i + u < cnt ? sum4(v[u], acc) : acc;
+				}
+				for (; __any(i < cnt); ++i) {
+					const uint4 v = win[o + (i < cnt ? i : 0)];
+					acc = i < cnt ? sum4(v, acc) : acc;
+				}
+				const bool head = cur.ok && cur.nch > 0 && cur.cs >= wb && cur.cs < we;
+				const bool tail = cur.ok && cur.nch > 0 && cur.ce - 1 >= wb && cur.ce - 1 < we;
+				const bool dw = !__any(cur.ok && ((cur.q | cur.len) & 3) != 0);
+				if (__any(head && cur.q != 0))
+					corr += head && cur.q != 0 ? lead_sum(win[(int)(cur.cs - wb)], cur.q, dw) : 0u;
+				if (__any(tail && cur.e != 16))
+					corr += tail && cur.e != 16 ? trail_sum(win[(int)(cur.ce - 1 - wb)], cur.e, dw) : 0u;
+				// the header's chunks: in this window and its overlap
+				const bool hstart = cur.ok && cur.cs >= wb && cur.cs < we;
+				if (!(p.flags & CGCK_RAW) && __any(hstart)) {
+					uint4 w8[8];
+					const int ho = hstart ? (int)(cur.cs - wb) : 0;
+#pragma unroll
+					for (int u = 0; u < 8; ++u)
+						w8[u] = win[ho + u];
+					const Hdr hh = header<8, false>(w8, reinterpret_cast<const uint4 *>(cur.a0 & ~(uint64_t)15),
+								    cur.nch, cur.q, cur.len, p.flags, hstart);
+					if (hstart)
+						h = hh;
+				}
+				asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // the slots are refilled next round
+			}
+			if (!pre) // the last round was a zero round: drained before the next issue or a fallback
+				asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+		} else if (first < p.n) {
+			// not chained: the lane's packet straight from global memory
+			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+			pre = false;
+			nn = lpw_step<DESC>(p, first_of(j + 2), load_desc<DESC>(p, first_of(j + 2) + l, p.n));
+			const uint4 *c0 = reinterpret_cast<const uint4 *>(cur.a0 & ~(uint64_t)15);
+			const int cnt = cur.ok ? cur.nch : 0;
+			for (int i = 0; __any(i < cnt); ++i) {
+				const uint4 v = ldc<false>(c0, i, cnt, p.zero);
+				acc = i < cnt ? sum4(v, acc) : acc;
+				if (i == 0 && cnt > 0 && cur.q != 0)
+					corr += lead_sum(v, cur.q, false);
+				if (i == cnt - 1 && cur.e != 16)
+					corr += trail_sum(v, cur.e, false);
+			}
+			if (!(p.flags & CGCK_RAW)) {
+				uint4 w8[8];
+#pragma unroll
+				for (int u = 0; u < 8; ++u)
+					w8[u] = ldc<false>(c0, u, cnt, p.zero);
+				h = header<8, false>(w8, c0, cur.nch, cur.q, cur.len, p.flags, cur.ok);
+			}
+		}
+		if (first < p.n) {
+			const uint32_t r = fold16(acc) + (0xffffu - fold16(corr));
+			const Res res = result(p, cur.a0, cur.len, fold16(r), h);
+			const int slot = (int)(j % C) * 64 + l;
+			so[slot] = res.out;
+			sv[slot] = (uint8_t)res.verdict;
+		}
+		if ((j + 1) % C == 0 || j + 1 == nsteps) {
+			// flush the chunk's outputs (packets [f0, f0 + 64 C) of the batch)
+			const uint64_t f0 = gstep(j - j % C) * 64;
+			asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+			const uint64_t cntp = f0 < p.n ? (p.n - f0 < (uint64_t)C * 64 ? p.n - f0 : (uint64_t)C * 64) : 0;
+			for (uint64_t i = l; i < cntp; i += 64) {
+				if (p.out)
+					gbl(p.out)[f0 + i] = so[i];
+				if (p.verdict)
+					gbl(p.verdict)[f0 + i] = sv[i];
+			}
+		}
+		cur = nxt;
+		nxt = nn;
+	}
+	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+bool lpw_ok(const KParams &p)
+{
+	return !p.bad && !(p.flags & (CGCK_STORE | kFlagNoLenCheck | kFlagL4Auto)) &&
+	       (reinterpret_cast<uintptr_t>(p.desc) & 15) == 0;
+}
+
+hipError_t launch_lpw(const KParams &p, int num_cus, hipStream_t st)
+{
+	static const int wpc = [] { // $CGCK_LPW_WPC: waves per CU
+		const char *e = getenv("CGCK_LPW_WPC");
+		return e && atoi(e) > 0 ? atoi(e) : 8;
+	}();
+	constexpr int C = 4; // 20.5 KiB of LDS per wave: 8 waves per CU
+	const uint64_t want = (p.n + 64 * C - 1) / (64 * C);
+	const uint64_t cap = (uint64_t)num_cus * wpc;
+	const dim3 g((unsigned)(want < cap ? (want ? want : 1) : cap));
+	const size_t lds = 2 * kLpwSlot + 2 * 1024 + C * 64 * 5;
+	if (p.desc) {
+		CGCK_NOTE_KERNEL("lpw_kernel<true, %d>", C);
+		hipLaunchKernelGGL((lpw_kernel<true, C>), g, dim3(64), lds, st, p);
+	} else {
+		CGCK_NOTE_KERNEL("lpw_kernel<false, %d>", C);
+		hipLaunchKernelGGL((lpw_kernel<false, C>), g, dim3(64), lds, st, p);
+	}
+	return hipGetLastError();
+}
+
 hipError_t launch_slotd(const KParams &p, int num_cus, hipStream_t st)
 {
 	static const int wpc = [] { // $CGCK_SLOTD_WPC: waves per CU
