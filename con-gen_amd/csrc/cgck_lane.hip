@@ -1305,6 +1305,8 @@ __global__ __launch_bounds__(64) void lpw_kernel(KParams p)
 				__builtin_amdgcn_s_barrier();
 				if (t == 0) // step j + 2's descriptors came with window 0 of this step
 					nn = lpw_step<DESC>(p, first_of(j + 2), lpw_desc_lds<DESC>(dring + ((j + 2) & 1) * 1024));
+				if (p.contig == 4) // $CGCK_LPW_NOCONS: rounds without the per-window work (A/B)
+					continue;
 				const uint4 *win = reinterpret_cast<const uint4 *>(smem + (kiss & 1) * kLpwSlot); // round kiss - 2
 				const uint64_t wb = cur.S + (uint64_t)t * kLpwWin;
 				const uint64_t we = wb + kLpwWin;
@@ -1410,6 +1412,10 @@ hipError_t launch_lpw(const KParams &p, int num_cus, hipStream_t st)
 		const char *e = getenv("CGCK_LPW_WPC");
 		return e && atoi(e) > 0 ? atoi(e) : 8;
 	}();
+	static const bool nocons = getenv("CGCK_LPW_NOCONS") != nullptr;
+	KParams q = p;
+	if (nocons)
+		q.contig = 4;
 	constexpr int C = 4; // 20.5 KiB of LDS per wave: 8 waves per CU
 	const uint64_t want = (p.n + 64 * C - 1) / (64 * C);
 	const uint64_t cap = (uint64_t)num_cus * wpc;
@@ -1417,10 +1423,10 @@ hipError_t launch_lpw(const KParams &p, int num_cus, hipStream_t st)
 	const size_t lds = 2 * kLpwSlot + 2 * 1024 + C * 64 * 5;
 	if (p.desc) {
 		CGCK_NOTE_KERNEL("lpw_kernel<true, %d>", C);
-		hipLaunchKernelGGL((lpw_kernel<true, C>), g, dim3(64), lds, st, p);
+		hipLaunchKernelGGL((lpw_kernel<true, C>), g, dim3(64), lds, st, q);
 	} else {
 		CGCK_NOTE_KERNEL("lpw_kernel<false, %d>", C);
-		hipLaunchKernelGGL((lpw_kernel<false, C>), g, dim3(64), lds, st, p);
+		hipLaunchKernelGGL((lpw_kernel<false, C>), g, dim3(64), lds, st, q);
 	}
 	return hipGetLastError();
 }
