@@ -66,9 +66,9 @@ EXPORTS = (
     "cgck_event_destroy", "cgck_event_record", "cgck_event_elapsed_ms", "cgck_probe_read",
     "toeplitz_hash", "rss_hash4", "cgck_toeplitz", "cgck_dst_cache", "cgck_dst_cache_host",
     "cgck_burst_open", "cgck_burst_close", "cgck_thread_ctx", "cgck_set_error_handler",
-    "cgck_rx_begin", "cgck_rx_end", "cgck_window_stats", "cgck_ctx_last_kernel",
+    "cgck_rx_begin", "cgck_rx_end", "cgck_window_stats", "cgck_ctx_last_kernel", "cgck_set_desc_layout",
 )
-# Descriptor layout hint of the lab build (cgck_lab_set_desc_layout; tools/, tests/test_gpu_span.py)
+# Descriptor layout hint (cgck_set_desc_layout)
 LAYOUT_ANY = 0
 LAYOUT_PACKED = 1
 LAB_PATH = os.path.join(os.path.dirname(HERE), "libcgck_lab.so")
@@ -114,8 +114,7 @@ def bind(path):
     L.cgck_ctx_stream.argtypes = [_vp]
     L.cgck_ctx_sync.argtypes = [_vp]
     L.cgck_set_desc_len_hint.argtypes = [_vp, _u32]
-    if hasattr(L, "cgck_lab_set_desc_layout"):
-        L.cgck_lab_set_desc_layout.argtypes = [_vp, _u32]
+    L.cgck_set_desc_layout.argtypes = [_vp, _u32]
     L.cgck_strided.argtypes = [_vp, _vp, _u64, _u64, _u32, _u32, _u32, _vp, _vp, _vp, _vp]
     L.cgck_desc.argtypes = [_vp, _vp, _vp, _u64, _u32, _vp, _vp, _vp, _vp]
     L.cgck_desc_host.argtypes = [_vp, _vp, ctypes.c_size_t, _vp, _u64, _u32, _vp, _vp]
@@ -370,12 +369,9 @@ class Engine:
         _check(load().cgck_set_desc_len_hint(self.ctx, n), "cgck_set_desc_len_hint")
 
     def set_desc_layout(self, layout):
-        """Lab build only (cgck_lab_set_desc_layout): LAYOUT_PACKED for frames
-        back to back, which picks the packed-span kernel."""
-        L = load()
-        if not hasattr(L, "cgck_lab_set_desc_layout"):
-            raise CgckError("the layout hint is a libcgck_lab.so entry point (CGCK_LIB)")
-        _check(L.cgck_lab_set_desc_layout(self.ctx, layout), "cgck_lab_set_desc_layout")
+        """cgck_set_desc_layout: LAYOUT_PACKED for descriptor batches whose
+        frames lie back to back (picks the streaming kernel, lpw)."""
+        _check(load().cgck_set_desc_layout(self.ctx, layout), "cgck_set_desc_layout")
 
     def strided(self, base, n, stride, l3_off, ip_len, flags, out=None, verdict=None, bad=None,
                 stream=None):

@@ -185,20 +185,15 @@ extern "C" int cgck_set_desc_len_hint(cgck_ctx_t *c, uint32_t max_ip_len)
 	return 0;
 }
 
-#if CGCK_LAB
-// Lab build only (not in include/cgck.h): layout hint for descriptor batches,
-// 1 = frames back to back in descriptor order, picks the packed-span kernel
-// (cgck_span.hip) for the A/B tools; results are exact for any layout.
-extern "C" int cgck_lab_set_desc_layout(cgck_ctx_t *c, uint32_t layout)
+extern "C" int cgck_set_desc_layout(cgck_ctx_t *c, uint32_t layout)
 {
 	if (!c)
-		return set_err(-EINVAL, "cgck_lab_set_desc_layout: NULL context");
-	if (layout > 1)
-		return set_err(-EINVAL, "cgck_lab_set_desc_layout: unknown layout %u", layout);
+		return set_err(-EINVAL, "cgck_set_desc_layout: NULL context");
+	if (layout > CGCK_LAYOUT_PACKED)
+		return set_err(-EINVAL, "cgck_set_desc_layout: unknown layout %u", layout);
 	c->desc_layout = layout;
 	return 0;
 }
-#endif
 
 static inline hipStream_t pick(cgck_ctx *c, void *stream)
 {

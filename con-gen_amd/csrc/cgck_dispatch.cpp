@@ -41,6 +41,8 @@ hipError_t launch_slot2(const KParams &p, int num_cus, bool nt, hipStream_t st);
 hipError_t launch_lpa(const KParams &p, int num_cus, bool nt, hipStream_t st);
 hipError_t launch_lpd(const KParams &p, int num_cus, hipStream_t st);
 bool lpd_ok(const KParams &p);
+hipError_t launch_lpw(const KParams &p, int num_cus, hipStream_t st);
+bool lpw_ok(const KParams &p);
 #if CGCK_LAB
 hipError_t launch_span(const KParams &p, int num_cus, bool nt, hipStream_t st);
 bool span_ok(const KParams &p);
@@ -49,8 +51,6 @@ hipError_t launch_lppp(const KParams &p, int num_cus, bool nt, hipStream_t st);
 hipError_t launch_stream(const KParams &p, int num_cus, hipStream_t st);
 bool stream_ok(const KParams &p);
 hipError_t launch_slotd(const KParams &p, int num_cus, hipStream_t st);
-hipError_t launch_lpw(const KParams &p, int num_cus, hipStream_t st);
-bool lpw_ok(const KParams &p);
 #endif
 
 // `kernel` = variant | flags (include/cgck.h is agnostic of this; $CGCK_KERNEL
@@ -60,19 +60,19 @@ bool lpw_ok(const KParams &p);
 //     default for mid-size packets), 10 lane per packet for aligned
 //     fixed-length strided 20..64-byte packets, A/B pipelined (lpa), 13 the
 //     same fed by LDS-DMA with staged output runs (lpd, the default there when
-//     the batch has no verdicts, counters or stores and stride <= 64).
-//     libcgck_lab.so only: 3 lane per 128-byte slot, 4 software-pipelined
-//     lane per packet, 5..8 lpp shapes 1..3, 0, 11 the lane-group kernel fed
-//     by LDS-DMA, 12 the packed span (descriptor batches whose frames lie back
-//     to back: coalesced stream + prefix sums, cgck_span.hip; picked under the
-//     lab's packed layout hint), 14 lane per slot fed by LDS-DMA (slotd), 15 lane per
-//     packet over DMA'd windows of the step's span (lpw).  A
-//     variant this build lacks falls back to the
-//     automatic choice; one whose preconditions a batch fails falls back to
-//     lpa, lpp or group;
+//     the batch has no verdicts, counters or stores and stride <= 64), 15
+//     lane per packet over DMA'd windows of a packed step's span (lpw, the
+//     default for descriptor batches of mixed lengths below 1 KiB under
+//     cgck_set_desc_layout(PACKED)).  libcgck_lab.so only: 3 lane per 128-byte
+//     slot, 4 software-pipelined lane per packet, 5..8 lpp shapes 1..3, 0, 11
+//     the lane-group kernel fed by LDS-DMA, 12 the packed span (coalesced
+//     register stream + prefix sums, cgck_span.hip), 14 lane per slot fed by
+//     LDS-DMA (slotd).  A variant this build lacks falls back to the automatic
+//     choice; one whose preconditions a batch fails falls back to lpa, lpp or
+//     group;
 //   kNT (bit 4) nontemporal loads, kContig (bit 5) contiguous block ranges,
 //   kExplicit (bit 6) take bits 4-5 as given instead of the measured defaults,
-//   kPacked (bit 7) the context's (lab-only) layout hint says packed.
+//   kPacked (bit 7) the context's layout hint says packed (cgck_set_desc_layout).
 // len_hint = the batch's packet length (strided) or typical length (descriptors).
 hipError_t launch_cksum(const KParams &p0, uint32_t len_hint, int num_cus, int kernel, hipStream_t st)
 {
@@ -86,14 +86,15 @@ hipError_t launch_cksum(const KParams &p0, uint32_t len_hint, int num_cus, int k
 			    ((reinterpret_cast<uintptr_t>(p.base) | p.stride | p.l3_off) & 15) == 0;
 #if CGCK_LAB
 	const bool known = variant <= 15;
-	const bool packed = (kernel & kPacked) && span_ok(p);
 #else
-	const bool known = variant == 1 || variant == 2 || variant == 9 || variant == 10 || variant == 13;
-	const bool packed = false;
+	const bool known = variant == 1 || variant == 2 || variant == 9 || variant == 10 || variant == 13 ||
+			   variant == 15;
 #endif
+	// a packed descriptor batch of mixed lengths below 1 KiB: lpw streams the buffer
+	const bool packed = (kernel & kPacked) && p.desc && lpw_ok(p);
 	if (variant == 0 || !known)
-		variant = !lane_ok ? 1 : lpa_ok ? (lpd_ok(p) ? 13 : 10) : packed ? 12 : len_hint >= kGroupFromLen ? 1
-			: len_hint <= kLppUpToLen ? 2 : 9;
+		variant = !lane_ok ? 1 : lpa_ok ? (lpd_ok(p) ? 13 : 10) : len_hint >= kGroupFromLen ? 1
+			: len_hint <= kLppUpToLen ? 2 : packed ? 15 : 9;
 	if (variant >= 2 && !lane_ok)
 		variant = 1;
 	if (variant == 10 && !lpa_ok)
@@ -105,9 +106,9 @@ hipError_t launch_cksum(const KParams &p0, uint32_t len_hint, int num_cus, int k
 		variant = 1;
 	if (variant == 11 && !stream_ok(p))
 		variant = 1;
+#endif
 	if (variant == 15 && !lpw_ok(p))
 		variant = 1;
-#endif
 	bool nt, contig;
 	if (kernel & kExplicit) {
 		nt = kernel & kNT;
@@ -129,6 +130,8 @@ hipError_t launch_cksum(const KParams &p0, uint32_t len_hint, int num_cus, int k
 		return launch_lpa(p, num_cus, nt, st);
 	case 13:
 		return launch_lpd(p, num_cus, st);
+	case 15:
+		return launch_lpw(p, num_cus, st);
 #if CGCK_LAB
 	case 12:
 		return launch_span(p, num_cus, nt, st);
@@ -148,8 +151,6 @@ hipError_t launch_cksum(const KParams &p0, uint32_t len_hint, int num_cus, int k
 		return launch_stream(p, num_cus, st);
 	case 14:
 		return launch_slotd(p, num_cus, st);
-	case 15:
-		return launch_lpw(p, num_cus, st);
 #endif
 	default:
 		return launch_group(p, len_hint, num_cus, nt, st);

@@ -1151,25 +1151,59 @@ __global__ __launch_bounds__(64) void slotd_kernel(KParams p)
 	}
 }
 
+hipError_t launch_slotd(const KParams &p, int num_cus, hipStream_t st)
+{
+	static const int wpc = [] { // $CGCK_SLOTD_WPC: waves per CU
+		const char *e = getenv("CGCK_SLOTD_WPC");
+		return e && atoi(e) > 0 ? atoi(e) : 6;
+	}();
+	const uint64_t want = (p.n + kSlotdChunk - 1) / kSlotdChunk;
+	const uint64_t cap = (uint64_t)num_cus * wpc;
+	const dim3 g((unsigned)(want < cap ? (want ? want : 1) : cap));
+	const size_t lds = 2 * 8192 + 64 * 4 + kWaveStage * 4 + kWaveStage;
+	if (p.desc) {
+		CGCK_NOTE_KERNEL("slotd_kernel<true>");
+		hipLaunchKernelGGL((slotd_kernel<true>), g, dim3(64), lds, st, p);
+	} else {
+		CGCK_NOTE_KERNEL("slotd_kernel<false>");
+		hipLaunchKernelGGL((slotd_kernel<false>), g, dim3(64), lds, st, p);
+	}
+	return hipGetLastError();
+}
+#endif // CGCK_LAB
+
 // --------------------------------------------------------------------------
-// Lane per packet over DMA'd windows of the batch's own span (lpw: IMIX)
+// Lane per packet over DMA'd windows of the batch's own span (lpw: packed
+// descriptor batches, the IMIX config under CGCK_LAYOUT_PACKED)
 // --------------------------------------------------------------------------
 //
 // A step is 64 consecutive descriptors, one per lane.  When their chunk
-// ranges chain (each packet starts at or before the furthest end so far, in
-// address order: a packed batch such as the IMIX set), every chunk of the
-// step's span [S, E) belongs to one of them, so the span is streamed with
-// contiguous DMA in windows of kLpwWin chunks (+64 chunks of overlap so a
-// header that starts near a window's end is complete) through a 2-deep LDS
-// ring, and lane L sums the chunks of its own packet that fall in each
-// window.  No slot map: a step's descriptors do not depend on the previous
-// step, and they travel by DMA with the data (768 B, one instruction, into
-// a 2-deep descriptor ring), two steps ahead, so no wait in the loop is on a
-// compiler-tracked load.  Every round issues kLpwDma + 1 DMA instructions
-// (zero lines where there is nothing to move), so the waits are counted.
-// Steps that do not chain are computed from global memory by the same lanes.
-constexpr int kLpwDma = 8;                       // data DMA instructions per window
-constexpr int kLpwWin = kLpwDma * 64 - 64;       // chunks a window owns (448)
+// ranges chain (each packet starts at or after the starts before it and at
+// or before the furthest end so far: frames back to back, as a burst copied
+// into one buffer or the IMIX set), every chunk of the step's span [S, E)
+// belongs to one of them.  The span is then streamed with contiguous DMA in
+// windows of kLpwWin chunks through a 2-deep LDS ring; per window, a lane per
+// chunk sums every chunk (conflict-free 16-byte LDS reads) and prefix-sums
+// them in lane order, and a lane per packet takes its chunks' sum as a
+// difference of two prefixes, minus the bytes of its edge chunks outside it;
+// its header chunks are gathered in registers from whichever windows hold
+// them and read once per step.  No slot map: a step's descriptors do not
+// depend on the previous step, and they travel by DMA with the data (768 B,
+// one instruction, into a 2-deep descriptor ring) two steps ahead, so no wait
+// in the loop is on a compiler-tracked load; every round issues kLpwDma + 1
+// DMA instructions (zero lines where there is nothing to move), so the waits
+// are counted.  Steps that do not chain are computed from global memory by
+// the same lanes (exact, slow): the layout hint says which batches chain.
+// In one process on the 16M IMIX batch (tools/sweep.py,
+// profiles/r02/dma/lpw/): 69.9 % of 8 TB/s against slot2's 63.8 %; windows of
+// 7 / 9 / 10+ DMA instructions, fewer waves per CU, or the lane-per-packet walk
+// of each window (21-23 %) lose.
+#ifndef CGCK_LPW_DMA
+#define CGCK_LPW_DMA 8
+#endif
+constexpr int kLpwDma = CGCK_LPW_DMA;            // data DMA instructions per window
+constexpr int kLpwWin = kLpwDma * 64;            // chunks a window owns (no overlap: a header
+						 // split over two windows is gathered from both)
 constexpr int kLpwSlot = kLpwDma * 1024;         // bytes per ring slot
 
 struct LpwStep {
@@ -1284,6 +1318,12 @@ __global__ __launch_bounds__(64) void lpw_kernel(KParams p)
 		uint32_t acc = 0, corr = 0;
 		Hdr h{};
 		if (first < p.n && cur.nwin > 0) {
+			// the header's chunks, loop-carried in native vectors (an array of
+			// uint4, a union type, was put in scratch)
+			u32x4_t t8[8];
+#pragma unroll
+			for (int u = 0; u < 8; ++u)
+				t8[u] = u32x4_t{0, 0, 0, 0};
 			if (!pre) {
 				lpw_issue<DESC>(p, cur.S, cur.E, true, lds0 + (kiss & 1) * kLpwSlot, first_of(j + 2), first_of(j + 2) < p.n,
 						ldsd + (uint32_t)((j + 2) & 1) * 1024, zero);
@@ -1305,29 +1345,14 @@ __global__ __launch_bounds__(64) void lpw_kernel(KParams p)
 				__builtin_amdgcn_s_barrier();
 				if (t == 0) // step j + 2's descriptors came with window 0 of this step
 					nn = lpw_step<DESC>(p, first_of(j + 2), lpw_desc_lds<DESC>(dring + ((j + 2) & 1) * 1024));
-				if (p.contig == 4) // $CGCK_LPW_NOCONS: rounds without the per-window work (A/B)
+				if (p.contig == 4) // lab $CGCK_LPW_NOCONS: rounds without the per-window work
 					continue;
 				const uint4 *win = reinterpret_cast<const uint4 *>(smem + (kiss & 1) * kLpwSlot); // round kiss - 2
 				const uint64_t wb = cur.S + (uint64_t)t * kLpwWin;
 				const uint64_t we = wb + kLpwWin;
-				const uint64_t lo = cur.cs > wb ? cur.cs : wb;
-				const uint64_t hi = cur.ce < we ? cur.ce : we;
-				const int cnt = cur.ok && hi > lo ? (int)(hi - lo) : 0;
-				const int o = (int)(lo - wb);
-				int i = 0;
-				for (; __any(i + 4 <= cnt); i += 4) {
-					uint4 v[4];
-#pragma unroll
-					for (int u = 0; u < 4; ++u)
-						v[u] = win[o + (i + u < cnt ? i + u : 0)];
-#pragma unroll
-					for (int u = 0; u < 4; ++u)
-						acc = i + u < cnt ? sum4(v[u], acc) : acc;
-				}
-				for (; __any(i < cnt); ++i) {
-					const uint4 v = win[o + (i < cnt ? i : 0)];
-					acc = i < cnt ? sum4(v, acc) : acc;
-				}
+				// 1. reads of single chunks: the packet's edge chunks and its
+				// header chunks cs .. cs + 7 that fall in this window (kept in
+				// registers across windows; the header is read once per step)
 				const bool head = cur.ok && cur.nch > 0 && cur.cs >= wb && cur.cs < we;
 				const bool tail = cur.ok && cur.nch > 0 && cur.ce - 1 >= wb && cur.ce - 1 < we;
 				const bool dw = !__any(cur.ok && ((cur.q | cur.len) & 3) != 0);
@@ -1335,20 +1360,49 @@ __global__ __launch_bounds__(64) void lpw_kernel(KParams p)
 					corr += head && cur.q != 0 ? lead_sum(win[(int)(cur.cs - wb)], cur.q, dw) : 0u;
 				if (__any(tail && cur.e != 16))
 					corr += tail && cur.e != 16 ? trail_sum(win[(int)(cur.ce - 1 - wb)], cur.e, dw) : 0u;
-				// the header's chunks: in this window and its overlap
-				const bool hstart = cur.ok && cur.cs >= wb && cur.cs < we;
-				if (!(p.flags & CGCK_RAW) && __any(hstart)) {
-					uint4 w8[8];
-					const int ho = hstart ? (int)(cur.cs - wb) : 0;
+				const bool hwin = cur.ok && cur.cs + 8 > wb && cur.cs < we;
+				if (!(p.flags & CGCK_RAW) && __any(hwin)) {
+					const u32x4_t *win4 = reinterpret_cast<const u32x4_t *>(win);
 #pragma unroll
-					for (int u = 0; u < 8; ++u)
-						w8[u] = win[ho + u];
-					const Hdr hh = header<8, false>(w8, reinterpret_cast<const uint4 *>(cur.a0 & ~(uint64_t)15),
-								    cur.nch, cur.q, cur.len, p.flags, hstart);
-					if (hstart)
-						h = hh;
+					for (int u = 0; u < 8; ++u) {
+						const uint64_t c = cur.cs + u;
+						const bool in = hwin && c >= wb && c < we;
+						const u32x4_t c8 = win4[in ? (int)(c - wb) : 0];
+						t8[u] = in ? c8 : t8[u];
+					}
 				}
+				// 2. lane per chunk: every owned chunk's sum (conflict-free 16-byte
+				// reads), prefix-summed over the window in lane order; the rows'
+				// scans are independent, their carries added after.  The prefix is
+				// written over the slot's first rows, already read.
+				uint32_t xs[kLpwDma];
+#pragma unroll
+				for (int r = 0; r < kLpwDma; ++r) {
+					const uint4 v = win[64 * r + l];
+					xs[r] = wave_scan_dpp(wb + 64 * r + l < cur.E ? sum4(v, 0u) : 0u);
+				}
+				asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // every read of the slot's chunks is done
+				uint32_t *pfx = reinterpret_cast<uint32_t *>(smem + (kiss & 1) * kLpwSlot);
+				uint32_t carry = 0;
+#pragma unroll
+				for (int r = 0; r < kLpwDma; ++r) {
+					pfx[64 * r + l] = xs[r] + carry;
+					carry += __builtin_amdgcn_readlane(xs[r], 63);
+				}
+				// 3. lane per packet: its chunks in this window as a prefix difference
+				const uint64_t lo = cur.cs > wb ? cur.cs : wb;
+				const uint64_t hi = cur.ce < we ? cur.ce : we;
+				if (cur.ok && hi > lo)
+					acc += pfx[(int)(hi - 1 - wb)] - (lo > wb ? pfx[(int)(lo - 1 - wb)] : 0u);
 				asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // the slots are refilled next round
+			}
+			if (!(p.flags & CGCK_RAW)) {
+				uint4 w8[8];
+#pragma unroll
+				for (int u = 0; u < 8; ++u)
+					w8[u] = make_uint4(t8[u].x, t8[u].y, t8[u].z, t8[u].w);
+				h = header<8, false>(w8, reinterpret_cast<const uint4 *>(cur.a0 & ~(uint64_t)15), cur.nch, cur.q,
+						     cur.len, p.flags, cur.ok);
 			}
 			if (!pre) // the last round was a zero round: drained before the next issue or a fallback
 				asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1412,11 +1466,14 @@ hipError_t launch_lpw(const KParams &p, int num_cus, hipStream_t st)
 		const char *e = getenv("CGCK_LPW_WPC");
 		return e && atoi(e) > 0 ? atoi(e) : 8;
 	}();
-	static const bool nocons = getenv("CGCK_LPW_NOCONS") != nullptr;
 	KParams q = p;
+	q.contig = 0;
+#if CGCK_LAB
+	static const bool nocons = getenv("CGCK_LPW_NOCONS") != nullptr;
 	if (nocons)
 		q.contig = 4;
-	constexpr int C = 4; // 20.5 KiB of LDS per wave: 8 waves per CU
+#endif
+	constexpr int C = 4; // 8 KiB windows: 19.3 KiB of LDS per wave, 8 waves per CU
 	const uint64_t want = (p.n + 64 * C - 1) / (64 * C);
 	const uint64_t cap = (uint64_t)num_cus * wpc;
 	const dim3 g((unsigned)(want < cap ? (want ? want : 1) : cap));
@@ -1431,26 +1488,6 @@ hipError_t launch_lpw(const KParams &p, int num_cus, hipStream_t st)
 	return hipGetLastError();
 }
 
-hipError_t launch_slotd(const KParams &p, int num_cus, hipStream_t st)
-{
-	static const int wpc = [] { // $CGCK_SLOTD_WPC: waves per CU
-		const char *e = getenv("CGCK_SLOTD_WPC");
-		return e && atoi(e) > 0 ? atoi(e) : 6;
-	}();
-	const uint64_t want = (p.n + kSlotdChunk - 1) / kSlotdChunk;
-	const uint64_t cap = (uint64_t)num_cus * wpc;
-	const dim3 g((unsigned)(want < cap ? (want ? want : 1) : cap));
-	const size_t lds = 2 * 8192 + 64 * 4 + kWaveStage * 4 + kWaveStage;
-	if (p.desc) {
-		CGCK_NOTE_KERNEL("slotd_kernel<true>");
-		hipLaunchKernelGGL((slotd_kernel<true>), g, dim3(64), lds, st, p);
-	} else {
-		CGCK_NOTE_KERNEL("slotd_kernel<false>");
-		hipLaunchKernelGGL((slotd_kernel<false>), g, dim3(64), lds, st, p);
-	}
-	return hipGetLastError();
-}
-#endif // CGCK_LAB
 
 // --------------------------------------------------------------------------
 // Launchers

@@ -128,6 +128,16 @@ int cgck_desc(cgck_ctx_t *ctx, void *base, const cgck_desc_t *desc, uint64_t n,
  * handled correctly; the hint only picks the faster kernel. */
 int cgck_set_desc_len_hint(cgck_ctx_t *ctx, uint32_t max_ip_len);
 
+/* Layout hint for descriptor batches.  CGCK_LAYOUT_PACKED: the frames of a
+ * batch lie back to back in descriptor order (a receive burst copied into
+ * one buffer, the IMIX set of BASELINE configs[3]); the dispatcher then
+ * streams the buffer itself (contiguous DMA through LDS) instead of gathering
+ * each frame, for mixed lengths below 1 KiB.  Results are exact for any
+ * layout: 64-frame steps that are not back to back are computed frame by
+ * frame, only slower.  Default CGCK_LAYOUT_ANY. */
+enum { CGCK_LAYOUT_ANY = 0, CGCK_LAYOUT_PACKED = 1 };
+int cgck_set_desc_layout(cgck_ctx_t *ctx, uint32_t layout);
+
 /* Host-resident batch (ring memory), synchronous.  Registered memory
  * (cgck_host_register) is read where it lies and in-place stores land there;
  * a small pageable burst (packet bytes <= 512 KiB) is copied packet by packet

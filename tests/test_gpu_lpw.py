@@ -1,0 +1,151 @@
+"""The packed-buffer streaming kernel (lpw_kernel, cgck_lane.hip): descriptor
+batches of mixed lengths under cgck_set_desc_layout(CGCK_LAYOUT_PACKED).
+Bit-exact against the oracle referee (oracle/cksum_oracle.c) on packed
+batches of every length class and alignment, on batches that are NOT packed
+(gapped, reversed, overlapping: its frame-by-frame steps must stay exact
+whatever the hint says), through the dispatcher's own choice, and on the
+full-size IMIX batch (BASELINE configs[3]) against the default slot2 path."""
+import os
+
+import numpy as np
+import pytest
+
+import cgck
+from test_gpu_parity import FLAG_SETS, random_batch
+from test_gpu_span import MIXES, packed_batch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def lpw():
+    """An engine forced to the lpw family ($CGCK_KERNEL=lpw, variant 15)."""
+    os.environ["CGCK_KERNEL"] = "lpw"
+    try:
+        e = cgck.Engine(0)
+    finally:
+        os.environ.pop("CGCK_KERNEL", None)
+    e.set_desc_layout(cgck.LAYOUT_PACKED)
+    yield e
+    e.close()
+
+
+def run(engine, port, buf, desc, flags):
+    exp, ever = port.batch_desc(buf.copy(), desc.view(np.uint8), len(desc), flags)
+    got = buf.copy()
+    out, ver = engine.run_host_desc(got, desc, flags)
+    bad = np.nonzero((out != exp) | (ver != ever))[0]
+    assert len(bad) == 0, (f"{len(bad)} mismatches, first {bad[:5]}: got {out[bad[:5]]} want {exp[bad[:5]]} "
+                           f"len {desc['ip_len'][bad[:5]]}")
+    return got, engine.last_kernel
+
+
+@pytest.mark.parametrize("mix", sorted(MIXES))
+@pytest.mark.parametrize("flags", [f for f in FLAG_SETS if not f & cgck.STORE])
+def test_packed_batches(lpw, port, mix, flags):
+    rng = np.random.default_rng(hash(mix) % 1000 + flags + 7)
+    n = 40 if mix == "jumbo" else 3000
+    buf, desc = packed_batch(rng, n, MIXES[mix], first_off=int(rng.integers(0, 16)))
+    got, kernel = run(lpw, port, buf, desc, flags)
+    assert kernel.startswith("lpw_kernel<")
+    assert np.array_equal(got, buf)
+
+
+@pytest.mark.parametrize("flags", [cgck.FILL_BOTH, cgck.VERIFY_BSD | cgck.STORE])
+def test_store_takes_other_family(lpw, port, flags):
+    """In-place stores are not lpw's (it reads the bytes it would rewrite
+    through LDS copies): those batches go to the group kernel, exact."""
+    rng = np.random.default_rng(15 + flags)
+    buf, desc = packed_batch(rng, 2000, MIXES["imix"])
+    exp_buf = buf.copy()
+    exp, ever = port.batch_desc(exp_buf, desc.view(np.uint8), len(desc), flags)
+    got = buf.copy()
+    out, ver = lpw.run_host_desc(got, desc, flags)
+    assert not lpw.last_kernel.startswith("lpw_kernel")
+    assert np.array_equal(out, exp) and np.array_equal(ver, ever) and np.array_equal(got, exp_buf)
+
+
+@pytest.mark.parametrize("max_len", [80, 600, 1600])
+def test_unpacked_batches(lpw, port, max_len):
+    """Gapped, odd-offset batches and a 2048-byte-slot ring under the packed
+    hint: every step is computed frame by frame, exact."""
+    rng = np.random.default_rng(max_len + 3)
+    buf, desc = random_batch(rng, 1500, max_len)
+    for flags in (cgck.GEN_BOTH, cgck.VERIFY_BSD, cgck.RAW):
+        run(lpw, port, buf, desc, flags)
+    n = 700
+    ring = rng.integers(0, 256, n * 2048 + 64, dtype=np.uint8)
+    rd = np.zeros(n, cgck.DESC_DTYPE)
+    rd["frame_off"] = np.arange(n) * 2048
+    rd["l3_off"] = 14
+    rd["ip_len"] = rng.integers(20, max_len + 1, n)
+    for k in range(n):
+        ring[k * 2048 + 14] = 0x45
+        ring[k * 2048 + 14 + 9] = 6
+    for flags in (cgck.GEN_BOTH, cgck.VERIFY_TOY):
+        run(lpw, port, ring, rd, flags)
+
+
+def test_reversed_overlapping_and_mixed_steps(lpw, port):
+    """Descriptors walking a packed buffer backwards, pairs over the same
+    bytes, and packed and unpacked 64-frame steps interleaved in one batch."""
+    rng = np.random.default_rng(78)
+    buf, desc = packed_batch(rng, 2000, MIXES["imix"])
+    run(lpw, port, buf, desc[::-1].copy(), cgck.GEN_BOTH)
+    run(lpw, port, buf, np.repeat(desc, 2), cgck.VERIFY_BSD)
+    mixed = desc.copy()
+    for s in range(0, len(mixed) - 64, 192):   # every third step reversed
+        mixed[s:s + 64] = mixed[s:s + 64][::-1]
+    run(lpw, port, buf, mixed, cgck.GEN_BOTH)
+
+
+def test_dispatcher_picks_lpw_under_the_hint(engine, port):
+    """The default dispatch: typical length below 1 KiB + CGCK_LAYOUT_PACKED
+    -> lpw; without the hint -> slot2; both exact."""
+    rng = np.random.default_rng(91)
+    buf, desc = packed_batch(rng, 5000, MIXES["imix"])
+    engine.set_desc_len_hint(354)
+    try:
+        engine.set_desc_layout(cgck.LAYOUT_PACKED)
+        _, k = run(engine, port, buf, desc, cgck.GEN_BOTH)
+        assert k.startswith("lpw_kernel<"), k
+        engine.set_desc_layout(cgck.LAYOUT_ANY)
+        _, k = run(engine, port, buf, desc, cgck.GEN_BOTH)
+        assert k.startswith("slot2_kernel<"), k
+    finally:
+        engine.set_desc_layout(cgck.LAYOUT_ANY)
+        engine.set_desc_len_hint(1500)
+    with pytest.raises(cgck.CgckError, match="unknown layout"):
+        engine.set_desc_layout(2)
+
+
+@pytest.mark.slow
+def test_full_size_imix(lpw, port):
+    """BASELINE configs[3] (16M IMIX packets, packed by cgck_synth_imix)
+    through lpw: every 64th packet against the referee, and the whole batch
+    against the default (slot2) path."""
+    n = 16 << 20
+    nbytes = cgck.load().cgck_imix_bytes(n)
+    buf = cgck.DeviceBuffer(nbytes)
+    desc = cgck.DeviceBuffer(12 * n)
+    out = cgck.DeviceBuffer(4 * n)
+    ref = cgck.DeviceBuffer(4 * n)
+    lpw.synth_imix(buf.ptr, desc.ptr, n, 0xC0C1)
+    e = cgck.Engine(0)
+    e.set_desc_len_hint(nbytes // n)
+    e.desc(buf.ptr, desc.ptr, n, cgck.GEN_BOTH, ref.ptr)
+    assert e.last_kernel.startswith("slot2_kernel<")
+    e.sync()
+    e.close()
+    lpw.desc(buf.ptr, desc.ptr, n, cgck.GEN_BOTH, out.ptr)
+    assert lpw.last_kernel.startswith("lpw_kernel<")
+    o = np.zeros(n, np.uint32)
+    r = np.zeros(n, np.uint32)
+    out.download(o, stream=lpw.stream)
+    ref.download(r, stream=lpw.stream)
+    lpw.sync()
+    for b in (buf, desc, out, ref):
+        b.free()
+    bad, chk = port.check_synth_imix(n, 0xC0C1, cgck.GEN_BOTH, o, 64)
+    assert bad == 0 and chk == n // 64
+    assert np.array_equal(o, r)

@@ -1,8 +1,8 @@
-"""Packed-span kernel (cgck_span.hip, an A/B family of libcgck_lab.so picked
-by the lab's layout hint): bit-exact against the oracle referee
+"""Packed-span kernel (cgck_span.hip, an A/B family of libcgck_lab.so, forced
+as variant 12 by $CGCK_KERNEL=span): bit-exact against the oracle referee
 (oracle/cksum_oracle.c) on packed batches of every length class and
 alignment, on batches that are NOT packed (its gap / lane-per-packet
-fallbacks must stay exact whatever the hint says), and on the full-size IMIX
+fallbacks must stay exact whatever the layout), and on the full-size IMIX
 batch (BASELINE configs[3]).  The module runs against the lab build: it swaps
 the binding for its own duration."""
 import os
@@ -25,7 +25,11 @@ def engine():
     try:
         if cgck.device_count() < 1:
             pytest.fail("no HIP device visible: the -m gpu tests need an MI355X")
-        e = cgck.Engine(0)
+        os.environ["CGCK_KERNEL"] = "span"
+        try:
+            e = cgck.Engine(0)
+        finally:
+            os.environ.pop("CGCK_KERNEL", None)
         yield e
         e.close()
     finally:
@@ -72,13 +76,9 @@ def packed_batch(rng, n, lens, first_off=0):
 
 def run_packed(engine, port, buf, desc, flags):
     exp, ever = port.batch_desc(buf.copy(), desc.view(np.uint8), len(desc), flags)
-    engine.set_desc_layout(cgck.LAYOUT_PACKED)
-    try:
-        got = buf.copy()
-        out, ver = engine.run_host_desc(got, desc, flags)
-        kernel = engine.last_kernel
-    finally:
-        engine.set_desc_layout(cgck.LAYOUT_ANY)
+    got = buf.copy()
+    out, ver = engine.run_host_desc(got, desc, flags)
+    kernel = engine.last_kernel
     bad = np.nonzero((out != exp) | (ver != ever))[0]
     assert len(bad) == 0, (f"{len(bad)} mismatches, first {bad[:5]}: got {out[bad[:5]]} want {exp[bad[:5]]} "
                            f"len {desc['ip_len'][bad[:5]]}")
@@ -98,19 +98,15 @@ def test_packed_batches(engine, port, mix, flags):
 
 @pytest.mark.parametrize("flags", [cgck.FILL_BOTH, cgck.VERIFY_BSD | cgck.STORE])
 def test_packed_hint_with_store_uses_other_family(engine, port, flags):
-    """STORE batches ignore the packed hint (in-place field stores would race
-    with neighbours' span reads) and stay exact."""
+    """STORE batches do not take the span kernel (in-place field stores would
+    race with neighbours' span reads) and stay exact."""
     rng = np.random.default_rng(5 + flags)
     buf, desc = packed_batch(rng, 2000, MIXES["imix"])
     exp_buf = buf.copy()
     exp, ever = port.batch_desc(exp_buf, desc.view(np.uint8), len(desc), flags)
-    engine.set_desc_layout(cgck.LAYOUT_PACKED)
-    try:
-        got = buf.copy()
-        out, ver = engine.run_host_desc(got, desc, flags)
-        assert not engine.last_kernel.startswith("span_kernel")
-    finally:
-        engine.set_desc_layout(cgck.LAYOUT_ANY)
+    got = buf.copy()
+    out, ver = engine.run_host_desc(got, desc, flags)
+    assert not engine.last_kernel.startswith("span_kernel")
     assert np.array_equal(out, exp) and np.array_equal(ver, ever) and np.array_equal(got, exp_buf)
 
 
@@ -159,14 +155,14 @@ def test_full_size_imix_packed(engine, port):
     ref = cgck.DeviceBuffer(4 * n)
     engine.synth_imix(buf.ptr, desc.ptr, n, 0xC0C0)
     engine.set_desc_len_hint(nbytes // n)
-    engine.desc(buf.ptr, desc.ptr, n, cgck.GEN_BOTH, ref.ptr)
-    engine.set_desc_layout(cgck.LAYOUT_PACKED)
-    try:
-        engine.desc(buf.ptr, desc.ptr, n, cgck.GEN_BOTH, out.ptr)
-        assert engine.last_kernel.startswith("span_kernel<")
-    finally:
-        engine.set_desc_layout(cgck.LAYOUT_ANY)
-        engine.set_desc_len_hint(1500)
+    ref_engine = cgck.Engine(0)   # the default (slot2) path
+    ref_engine.set_desc_len_hint(nbytes // n)
+    ref_engine.desc(buf.ptr, desc.ptr, n, cgck.GEN_BOTH, ref.ptr)
+    ref_engine.sync()
+    ref_engine.close()
+    engine.desc(buf.ptr, desc.ptr, n, cgck.GEN_BOTH, out.ptr)
+    assert engine.last_kernel.startswith("span_kernel<")
+    engine.set_desc_len_hint(1500)
     o = np.zeros(n, np.uint32)
     r = np.zeros(n, np.uint32)
     out.download(o, stream=engine.stream)

@@ -57,7 +57,7 @@ def main():
             for L, c in zip(libs, ctxs):
                 L.cgck_set_desc_len_hint(c, nbytes // n)
                 if w == "imixp":
-                    L.cgck_lab_set_desc_layout(c, cgck.LAYOUT_PACKED)
+                    L.cgck_set_desc_layout(c, cgck.LAYOUT_PACKED)
             work[w] = (lambda L, c, buf=buf, desc=desc: L.cgck_desc(c, buf.ptr, desc.ptr, n, cgck.GEN_BOTH,
                                                                      out.ptr, None, None, None),
                        nbytes + 16 * n)

@@ -18,7 +18,7 @@ import sys
 KERNELS = {
     "1500": "cksum_kernel<16, 6, 1, false, true>",
     "64": "lpd_kernel<2, 32, 2>",
-    "imix": "slot2_kernel<true, false>",
+    "imix": "lpw_kernel<true, 4>",
     "rss_hash": "toeplitz12x4_ab_kernel",
     "dst_cache": "dst_cache_kernel<true>",
 }

@@ -64,14 +64,15 @@ def main():
                        m * (L + 12) + (4 * m if "out" in out_list else 0), [buf, desc])
         elif w in ("imix", "imixp"):
             # imixp: the SAME batch (same allocation: a different one can land
-            # in another HBM state) with the packed layout hint
+            # in another HBM state) with the packed layout hint;
+            # imix: without it
             nbytes = cgck.load().cgck_imix_bytes(n)
             if "imix_bufs" not in locals():
                 imix_bufs = (cgck.DeviceBuffer(nbytes), cgck.DeviceBuffer(12 * n))
                 e0.synth_imix(imix_bufs[0].ptr, imix_bufs[1].ptr, n, 0xC0C0)
             buf, desc = imix_bufs
             algo = nbytes + 12 * n + (4 * n if "out" in out_list else 0)
-            if w == "imixp":   # the lab build's layout hint (CGCK_LIB=.../libcgck_lab.so)
+            if w == "imixp":   # the packed layout hint (cgck_set_desc_layout)
                 work[w] = (lambda e, f, o, buf=buf, desc=desc, h=nbytes // n: (
                     e.set_desc_len_hint(h), e.set_desc_layout(cgck.LAYOUT_PACKED), e.desc(buf.ptr, desc.ptr, n, f, o),
                     e.set_desc_layout(cgck.LAYOUT_ANY)), algo, [buf, desc])
