@@ -90,8 +90,13 @@ hipError_t launch_cksum(const KParams &p0, uint32_t len_hint, int num_cus, int k
 	const bool known = variant == 1 || variant == 2 || variant == 9 || variant == 10 || variant == 13 ||
 			   variant == 15;
 #endif
-	// a packed descriptor batch of mixed lengths below 1 KiB: lpw streams the buffer
-	const bool packed = (kernel & kPacked) && p.desc && lpw_ok(p);
+	// 256 B <= typical length < 1 KiB and the frames back to back (a descriptor
+	// batch under the packed hint, or a strided batch whose stride is at most
+	// its length): lpw streams the buffer (tools/sweep.py, profiles/r02/dma/lpw:
+	// dense strided 256 / 576 / 1000 B 69.6 / 73.1 / 74.7 % vs slot2's
+	// 52.1 / 56.6 / 48.4 %; 160 B 46.9 vs 59.8 %; 1500 B 75.6 vs group 79.9 %)
+	const bool packed = len_hint >= kLpwFromLen && lpw_ok(p) &&
+			    (p.desc ? (kernel & kPacked) != 0 : p.stride <= p.ip_len && p.stride > 0);
 	if (variant == 0 || !known)
 		variant = !lane_ok ? 1 : lpa_ok ? (lpd_ok(p) ? 13 : 10) : len_hint >= kGroupFromLen ? 1
 			: len_hint <= kLppUpToLen ? 2 : packed ? 15 : 9;

@@ -81,6 +81,7 @@ constexpr int kNT = 16, kContig = 32, kExplicit = 64;
 constexpr int kPacked = 128; // the context's descriptor layout hint is CGCK_LAYOUT_PACKED
 constexpr uint32_t kGroupFromLen = 1024; // typical length from which the group kernel is used
 constexpr uint32_t kLppUpToLen = 128;    // lane-per-packet up to here, lane-per-slot above
+constexpr uint32_t kLpwFromLen = 256;    // back-to-back frames from here stream through LDS (lpw)
 constexpr int kDefaultLppShape = 2;       // see launch_lpp (6 chunks up front, predicated: best on 64 B)
 constexpr bool kDefaultGroupNT = true, kDefaultGroupContig = true;
 constexpr bool kDefaultLaneNT = false, kDefaultLaneContig = false;

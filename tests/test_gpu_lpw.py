@@ -149,3 +149,23 @@ def test_full_size_imix(lpw, port):
     bad, chk = port.check_synth_imix(n, 0xC0C1, cgck.GEN_BOTH, o, 64)
     assert bad == 0 and chk == n // 64
     assert np.array_equal(o, r)
+
+
+@pytest.mark.parametrize("stride,ln,want", [(576, 576, "lpw_kernel<"), (300, 300, "lpw_kernel<"),
+                                            (1024, 576, "slot2_kernel<"), (160, 160, "slot2_kernel<"),
+                                            (1500, 1500, "cksum_kernel<")])
+def test_dispatcher_strided(engine, port, stride, ln, want):
+    """Strided batches need no hint: frames back to back (stride <= length)
+    from 256 B to 1 KiB stream (lpw); gapped or smaller ones gather (slot2),
+    1 KiB and up take the group kernel; all exact."""
+    n = 3001
+    rng = np.random.default_rng(stride + ln)
+    buf = rng.integers(0, 256, n * stride + ln + 64, dtype=np.uint8)
+    for k in range(n):
+        buf[k * stride] = 0x45 if k % 5 else 0x46
+        buf[k * stride + 9] = (6, 17, 1)[k % 3]
+    for flags in (cgck.GEN_BOTH, cgck.VERIFY_BSD, cgck.RAW):
+        exp, ever = port.batch_strided(buf.copy(), n, stride, 0, ln, flags)
+        out, ver = engine.run_host_strided(buf.copy(), n, stride, 0, ln, flags)
+        assert np.array_equal(out, exp) and np.array_equal(ver, ever), (stride, ln, flags)
+        assert engine.last_kernel.startswith(want), engine.last_kernel
