@@ -371,4 +371,23 @@ __device__ __forceinline__ uint32_t wave_scan_dpp(uint32_t x)
 	return x;
 }
 
+// inclusive max-scan over the wave in DPP (same pattern as wave_scan_dpp;
+// lanes whose DPP source is out of range read 0, which max leaves alone)
+__device__ __forceinline__ uint32_t wave_max_scan_dpp(uint32_t x)
+{
+#define CGCK_MAXDPP(ctrl, rmask)                                                                         \
+	{                                                                                                \
+		const uint32_t y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, ctrl, rmask, 0xf, false); \
+		x = y > x ? y : x;                                                                       \
+	}
+	CGCK_MAXDPP(0x111, 0xf) // row_shr:1
+	CGCK_MAXDPP(0x112, 0xf) // row_shr:2
+	CGCK_MAXDPP(0x114, 0xf) // row_shr:4
+	CGCK_MAXDPP(0x118, 0xf) // row_shr:8
+	CGCK_MAXDPP(0x142, 0xa) // row_bcast:15
+	CGCK_MAXDPP(0x143, 0xc) // row_bcast:31
+#undef CGCK_MAXDPP
+	return x;
+}
+
 } // namespace cgck

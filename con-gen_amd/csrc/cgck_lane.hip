@@ -1201,6 +1201,21 @@ hipError_t launch_slotd(const KParams &p, int num_cus, hipStream_t st)
 #ifndef CGCK_LPW_DMA
 #define CGCK_LPW_DMA 8
 #endif
+// 0: instruction i moves chunks [64 i, 64 i + 64) of the window (1 KiB
+// contiguous); 1: lane l moves chunks [8 l, 8 l + 8) over the 8 instructions,
+// so its own run lands in conflict-free LDS places (A/B builds)
+#ifndef CGCK_LPW_SLOTMAJOR
+#define CGCK_LPW_SLOTMAJOR 0
+#endif
+// LDS index (in 16-byte units) of window chunk idx
+__device__ __forceinline__ int lpw_at(int idx)
+{
+#if CGCK_LPW_SLOTMAJOR
+	return ((idx & 7) << 6) | (idx >> 3);
+#else
+	return idx;
+#endif
+}
 constexpr int kLpwDma = CGCK_LPW_DMA;            // data DMA instructions per window
 constexpr int kLpwWin = kLpwDma * 64;            // chunks a window owns (no overlap: a header
 						 // split over two windows is gathered from both)
@@ -1230,25 +1245,22 @@ __device__ __forceinline__ LpwStep lpw_step(const KParams &p, uint64_t first, co
 	s.cs = pk.a0 >> 4;
 	s.ce = s.cs + (uint64_t)s.nch;
 	// Over the non-empty packets in lane order: running maxima of the starts
-	// and of the ends (inclusive scans, then shifted by one lane).  The step
-	// chains when every start is >= the starts before it and <= the furthest
-	// end before it: then [S, E) is exactly the union of the packets' chunks.
+	// and of the ends (inclusive DPP scans of 32-bit offsets from the first
+	// non-empty packet, then shifted by one lane).  The step chains when every
+	// start is >= the starts before it and <= the furthest end before it: then
+	// [S, E) is exactly the union of the packets' chunks.
 	const bool ne = s.ok && s.nch > 0;
-	uint64_t mE = ne ? s.ce : 0, mS = ne ? s.cs : 0;
-#pragma unroll
-	for (int d2 = 1; d2 < 64; d2 <<= 1) {
-		const uint64_t yE = shfl64(mE, l >= d2 ? l - d2 : l), yS = shfl64(mS, l >= d2 ? l - d2 : l);
-		if (l >= d2) {
-			mE = yE > mE ? yE : mE;
-			mS = yS > mS ? yS : mS;
-		}
-	}
-	const uint64_t prev_e = shfl64(mE, l > 0 ? l - 1 : 0), prev_s = shfl64(mS, l > 0 ? l - 1 : 0);
 	const uint64_t nonempty = __ballot(ne);
 	const int f = nonempty ? __ffsll((long long)nonempty) - 1 : 0; // first non-empty lane
-	const bool brk = ne && l > f && (s.cs < prev_s || s.cs > prev_e);
-	s.S = nonempty ? shfl64(s.cs, f) : 0;
-	s.E = nonempty ? shfl64(mE, 63) : 0;
+	const uint64_t base = shfl64(s.cs, f);
+	const uint64_t ds = s.cs - base, de = s.ce - base;
+	const bool far = ne && (s.cs < base || de > 0x7fffffffull); // before the first, or too far for 32 bits
+	const uint32_t rs = ne && !far ? (uint32_t)ds : 0u, re = ne && !far ? (uint32_t)de : 0u;
+	const uint32_t mS = wave_max_scan_dpp(rs), mE = wave_max_scan_dpp(re);
+	const uint32_t prev_s = (uint32_t)__shfl_up((int)mS, 1, 64), prev_e = (uint32_t)__shfl_up((int)mE, 1, 64);
+	const bool brk = far || (ne && l > f && (rs < prev_s || rs > prev_e));
+	s.S = nonempty ? base : 0;
+	s.E = nonempty ? base + (uint64_t)__builtin_amdgcn_readlane(mE, 63) : 0;
 	const uint64_t span = s.E - s.S;
 	s.nwin = __any(brk) || span > 16 * kLpwWin ? 0u : (uint32_t)((span + kLpwWin - 1) / kLpwWin);
 	if (!__any(brk) && span == 0)
@@ -1268,7 +1280,11 @@ __device__ __forceinline__ void lpw_issue(const KParams &p, uint64_t wb, uint64_
 	const uint32_t base = __builtin_amdgcn_readfirstlane(lds_slot); // wave-uniform: M0
 #pragma unroll
 	for (int i = 0; i < kLpwDma; ++i) {
+#if CGCK_LPW_SLOTMAJOR
+		const uint64_t c = wb + 8 * l + i; // lane l's 8 chunks land at +16 l of each KiB
+#else
 		const uint64_t c = wb + 64 * i + l;
+#endif
 		glds16_nt(live && c < E ? reinterpret_cast<const void *>(c << 4) : zero, base + 1024 * i);
 	}
 	const uint64_t doff = 12 * dfirst + 16 * (uint64_t)l;
@@ -1357,9 +1373,9 @@ __global__ __launch_bounds__(64) void lpw_kernel(KParams p)
 				const bool tail = cur.ok && cur.nch > 0 && cur.ce - 1 >= wb && cur.ce - 1 < we;
 				const bool dw = !__any(cur.ok && ((cur.q | cur.len) & 3) != 0);
 				if (__any(head && cur.q != 0))
-					corr += head && cur.q != 0 ? lead_sum(win[(int)(cur.cs - wb)], cur.q, dw) : 0u;
+					corr += head && cur.q != 0 ? lead_sum(win[lpw_at((int)(cur.cs - wb))], cur.q, dw) : 0u;
 				if (__any(tail && cur.e != 16))
-					corr += tail && cur.e != 16 ? trail_sum(win[(int)(cur.ce - 1 - wb)], cur.e, dw) : 0u;
+					corr += tail && cur.e != 16 ? trail_sum(win[lpw_at((int)(cur.ce - 1 - wb))], cur.e, dw) : 0u;
 				const bool hwin = cur.ok && cur.cs + 8 > wb && cur.cs < we;
 				if (!(p.flags & CGCK_RAW) && __any(hwin)) {
 					const u32x4_t *win4 = reinterpret_cast<const u32x4_t *>(win);
@@ -1367,7 +1383,7 @@ __global__ __launch_bounds__(64) void lpw_kernel(KParams p)
 					for (int u = 0; u < 8; ++u) {
 						const uint64_t c = cur.cs + u;
 						const bool in = hwin && c >= wb && c < we;
-						const u32x4_t c8 = win4[in ? (int)(c - wb) : 0];
+						const u32x4_t c8 = win4[in ? lpw_at((int)(c - wb)) : 0];
 						t8[u] = in ? c8 : t8[u];
 					}
 				}
@@ -1375,6 +1391,27 @@ __global__ __launch_bounds__(64) void lpw_kernel(KParams p)
 				// reads), prefix-summed over the window in lane order; the rows'
 				// scans are independent, their carries added after.  The prefix is
 				// written over the slot's first rows, already read.
+#if CGCK_LPW_SLOTMAJOR
+				static_assert(kLpwDma == 8, "slot-major windows are 64 lanes x 8 chunks");
+				// lane l owns chunks [8 l, 8 l + 8): local prefix, one wave scan
+				uint32_t xs[8];
+				uint32_t run = 0;
+#pragma unroll
+				for (int i = 0; i < 8; ++i) {
+					const uint4 v = win[64 * i + l];
+					run += wb + 8 * l + i < cur.E ? sum4(v, 0u) : 0u;
+					xs[i] = run;
+				}
+				const uint32_t before = wave_scan_dpp(run) - run;
+				asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // every read of the slot's chunks is done
+				uint32_t *pfx = reinterpret_cast<uint32_t *>(smem + (kiss & 1) * kLpwSlot);
+				{
+					typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+					u32x4v *p4 = reinterpret_cast<u32x4v *>(pfx + 8 * l);
+					p4[0] = u32x4v{before + xs[0], before + xs[1], before + xs[2], before + xs[3]};
+					p4[1] = u32x4v{before + xs[4], before + xs[5], before + xs[6], before + xs[7]};
+				}
+#else
 				uint32_t xs[kLpwDma];
 #pragma unroll
 				for (int r = 0; r < kLpwDma; ++r) {
@@ -1389,6 +1426,7 @@ __global__ __launch_bounds__(64) void lpw_kernel(KParams p)
 					pfx[64 * r + l] = xs[r] + carry;
 					carry += __builtin_amdgcn_readlane(xs[r], 63);
 				}
+#endif
 				// 3. lane per packet: its chunks in this window as a prefix difference
 				const uint64_t lo = cur.cs > wb ? cur.cs : wb;
 				const uint64_t hi = cur.ce < we ? cur.ce : we;

@@ -50,7 +50,7 @@ def main():
     keep = []
     for w in args.workloads.split(","):
         if w in ("imix", "imixp"):
-            # imixp: the packed layout hint on both contexts (span kernel)
+            # imixp: the packed layout hint on both contexts (lpw)
             nbytes = cgck.load().cgck_imix_bytes(n)
             buf, desc = cgck.DeviceBuffer(nbytes), cgck.DeviceBuffer(12 * n)
             e0.synth_imix(buf.ptr, desc.ptr, n, 0xC0C0)
