@@ -117,7 +117,7 @@ extern "C" int cgck_ctx_create(int device, cgck_ctx_t **out)
 	c->desc_len_hint = 1500;
 	if (const char *kf = getenv("CGCK_KERNEL"))
 		c->family = !strcmp(kf, "group") ? 1 : !strcmp(kf, "lpp") ? 2 : !strcmp(kf, "slot") ? 3
-			  : !strcmp(kf, "slot2") ? 9 : !strcmp(kf, "lpa") ? 10 : !strcmp(kf, "str") ? 11
+			  : !strcmp(kf, "slot2") ? 9 : !strcmp(kf, "lpa") ? 10 : !strcmp(kf, "str") || !strcmp(kf, "dstr") ? 11
 			  : !strcmp(kf, "span") ? 12 : !strcmp(kf, "lpd") ? 13 : !strcmp(kf, "slotd") ? 14 : !strcmp(kf, "lpw") ? 15
 			  : !strncmp(kf, "lpp", 3) ? atoi(kf + 3) : atoi(kf);
 	hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);

@@ -1,7 +1,8 @@
 // cgck_dispatch.cpp — picks the kernel family and launch shape for a batch.
 //
 // The product library (libcgck.so) carries only the families the dispatcher
-// picks by itself: group (>= 1 KiB typical length, drop-in and window calls),
+// picks by itself: dstr (dense strided >= 1 KiB frames, the 1500 B config),
+// group (>= 1 KiB typical length otherwise, drop-in and window calls),
 // lpd / lpa (aligned fixed-length 20..64-byte strided batches), lpp (small
 // unaligned or descriptor packets) and slot2 (mid-size / mixed lengths).  The
 // A/B-only variants measured against them (slot, lppp, the other lpp shapes,
@@ -43,6 +44,8 @@ hipError_t launch_lpd(const KParams &p, int num_cus, hipStream_t st);
 bool lpd_ok(const KParams &p);
 hipError_t launch_lpw(const KParams &p, int num_cus, hipStream_t st);
 bool lpw_ok(const KParams &p);
+hipError_t launch_dstr(const KParams &p, int num_cus, hipStream_t st);
+bool dstr_ok(const KParams &p);
 #if CGCK_LAB
 hipError_t launch_span(const KParams &p, int num_cus, bool nt, hipStream_t st);
 bool span_ok(const KParams &p);
@@ -63,9 +66,13 @@ hipError_t launch_slotd(const KParams &p, int num_cus, hipStream_t st);
 //     the batch has no verdicts, counters or stores and stride <= 64), 15
 //     lane per packet over DMA'd windows of a packed step's span (lpw, the
 //     default for descriptor batches of mixed lengths below 1 KiB under
-//     cgck_set_desc_layout(PACKED)).  libcgck_lab.so only: 3 lane per 128-byte
-//     slot, 4 software-pipelined lane per packet, 5..8 lpp shapes 1..3, 0, 11
-//     the lane-group kernel fed by LDS-DMA, 12 the packed span (coalesced
+//     cgck_set_desc_layout(PACKED)), 11 dense strided frames streamed through
+//     LDS by DMA, four per step, with a writer wave (dstr, cgck_dense.hip: the
+//     default for strided batches of >= 1 KiB frames it accepts, dstr_ok;
+//     $CGCK_STR_OLD in the lab build: the first stream kernel,
+//     cgck_stream.hip).  libcgck_lab.so only: 3 lane per 128-byte
+//     slot, 4 software-pipelined lane per packet, 5..8 lpp shapes 1..3, 0,
+//     12 the packed span (coalesced
 //     register stream + prefix sums, cgck_span.hip), 14 lane per slot fed by
 //     LDS-DMA (slotd).  A variant this build lacks falls back to the automatic
 //     choice; one whose preconditions a batch fails falls back to lpa, lpp or
@@ -87,8 +94,8 @@ hipError_t launch_cksum(const KParams &p0, uint32_t len_hint, int num_cus, int k
 #if CGCK_LAB
 	const bool known = variant <= 15;
 #else
-	const bool known = variant == 1 || variant == 2 || variant == 9 || variant == 10 || variant == 13 ||
-			   variant == 15;
+	const bool known = variant == 1 || variant == 2 || variant == 9 || variant == 10 || variant == 11 ||
+			   variant == 13 || variant == 15;
 #endif
 	// 256 B <= typical length < 1 KiB and the frames back to back (a descriptor
 	// batch under the packed hint, or a strided batch whose stride is at most
@@ -98,7 +105,8 @@ hipError_t launch_cksum(const KParams &p0, uint32_t len_hint, int num_cus, int k
 	const bool packed = len_hint >= kLpwFromLen && lpw_ok(p) &&
 			    (p.desc ? (kernel & kPacked) != 0 : p.stride <= p.ip_len && p.stride > 0);
 	if (variant == 0 || !known)
-		variant = !lane_ok ? 1 : lpa_ok ? (lpd_ok(p) ? 13 : 10) : len_hint >= kGroupFromLen ? 1
+		variant = !lane_ok ? 1 : lpa_ok ? (lpd_ok(p) ? 13 : 10)
+			: len_hint >= kGroupFromLen ? (!p.desc && dstr_ok(p) ? 11 : 1)
 			: len_hint <= kLppUpToLen ? 2 : packed ? 15 : 9;
 	if (variant >= 2 && !lane_ok)
 		variant = 1;
@@ -109,9 +117,9 @@ hipError_t launch_cksum(const KParams &p0, uint32_t len_hint, int num_cus, int k
 #if CGCK_LAB
 	if (variant == 12 && !span_ok(p))
 		variant = 1;
-	if (variant == 11 && !stream_ok(p))
-		variant = 1;
 #endif
+	if (variant == 11 && !dstr_ok(p))
+		variant = 1;
 	if (variant == 15 && !lpw_ok(p))
 		variant = 1;
 	bool nt, contig;
@@ -137,6 +145,12 @@ hipError_t launch_cksum(const KParams &p0, uint32_t len_hint, int num_cus, int k
 		return launch_lpd(p, num_cus, st);
 	case 15:
 		return launch_lpw(p, num_cus, st);
+	case 11:
+#if CGCK_LAB
+		if (getenv("CGCK_STR_OLD") && stream_ok(p)) // the first stream kernel (cgck_stream.hip)
+			return launch_stream(p, num_cus, st);
+#endif
+		return launch_dstr(p, num_cus, st);
 #if CGCK_LAB
 	case 12:
 		return launch_span(p, num_cus, nt, st);
@@ -152,8 +166,6 @@ hipError_t launch_cksum(const KParams &p0, uint32_t len_hint, int num_cus, int k
 		return launch_lpp(p, num_cus, nt, 3, st);
 	case 8:
 		return launch_lpp(p, num_cus, nt, 0, st);
-	case 11:
-		return launch_stream(p, num_cus, st);
 	case 14:
 		return launch_slotd(p, num_cus, st);
 #endif

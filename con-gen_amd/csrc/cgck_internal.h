@@ -85,10 +85,11 @@ constexpr uint32_t kLpwFromLen = 256;    // back-to-back frames from here stream
 constexpr int kDefaultLppShape = 2;       // see launch_lpp (6 chunks up front, predicated: best on 64 B)
 constexpr bool kDefaultGroupNT = true, kDefaultGroupContig = true;
 constexpr bool kDefaultLaneNT = false, kDefaultLaneContig = false;
-// The LDS-DMA stream kernel (cgck_stream.hip) for dense 1500 B batches: off
-// by default — measured 76.9 % vs 77.9 % of HBM peak for the register-load
-// group kernel on the same box (tools/str_sweep.sh).  CGCK_KERNEL=str.
-constexpr bool kDefaultStream = false;
+// Dense strided batches of >= 1 KiB frames take dstr_kernel (cgck_dense.hip,
+// LDS-DMA steps of 4 frames with a writer wave): 80.3-82.0 % vs the group
+// kernel's 78.6-81.5 % in the same process (tools/dstr_sweep.sh,
+// profiles/r02/dense/).  The first LDS-DMA stream kernel (cgck_stream.hip,
+// 76.9 % vs 77.9 %) stays in the lab build.
 // Batched Toeplitz hash over dense 12-byte tuples: 0 two-group loop, 2 A/B
 // pipelined (cgck_rss.hip).
 constexpr int kDefaultRssVariant = 2;

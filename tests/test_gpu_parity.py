@@ -209,7 +209,7 @@ def test_fuzz_strided_vs_oracle(engine, port, stride, l3, ln, flags):
 # Every kernel family forced through $CGCK_KERNEL (read at context creation),
 # on the strided shapes each one accepts; a family falls back to the group
 # kernel where its preconditions fail, so every cell is a valid comparison.
-FAMILIES = ["group", "lpp", "lpa", "lpd", "slot2", "lpw"]   # every family libcgck.so dispatches to
+FAMILIES = ["group", "lpp", "lpa", "lpd", "slot2", "lpw", "dstr"]   # every family libcgck.so dispatches to
 FAMILY_SHAPES = [  # (stride, l3_off, ip_len, packets); odd counts: every ip_hl = 5
     (64, 0, 64, 3000), (64, 0, 64, 4097), (64, 16, 64, 999), (64, 0, 48, 333), (32, 0, 20, 333), (128, 16, 64, 333), (72, 2, 60, 333),
     (256, 0, 255, 333), (1500, 0, 1500, 3000), (1504, 4, 1500, 333), (1520, 0, 1517, 333),
@@ -255,6 +255,8 @@ def test_family_strided_vs_oracle(family_engines, port, family, stride, l3, ln, 
     assert np.array_equal(got, ref)
     if family == "lpd" and stride <= 64 and (stride | l3) % 16 == 0 and 20 <= ln <= 64:
         assert e.last_kernel.startswith("lpd_kernel<"), e.last_kernel
+    if family == "dstr" and stride <= 1520 and (stride | l3) % 4 == 0 and not flags & cgck.VERIFY:
+        assert e.last_kernel.startswith("dstr_kernel<"), e.last_kernel
 
 
 def test_edges(engine, port):

@@ -4,8 +4,8 @@ oracle on strided batches, in one process on the lab build:
 
     CGCK_LIB=con-gen_amd/libcgck_lab.so python tools/lpd_check.py [ref,cand] [small|mtu]
 
-(default lpa,lpd on the 64 B shapes; e.g. `group,str mtu` for the 1500 B
-LDS-DMA stream kernel).
+(default lpa,lpd on the 64 B shapes; e.g. `group,dstr mtu` for the 1500 B
+LDS-DMA dense stream kernel).
 For every shape and flag set the two kernels' outputs must be identical, and
 GEN_BOTH batches are also checked against the referee (every 7th packet).
 """
@@ -36,7 +36,8 @@ def main():
               (300001, 48, 44), (100000, 32, 20), (4097, 64, 52), (64 * 2048 + 5, 64, 64)]
     if preset == "mtu":
         shapes = [(16 << 20, 1500, 1500), (1000003, 1500, 1500), (777, 1500, 1500), (5, 1500, 1500),
-                  (300001, 1504, 1499), (100000, 1024, 1000), (4097, 1516, 1516), (123457, 576, 576)]
+                  (300001, 1504, 1499), (100000, 1024, 1000), (4097, 1516, 1516), (123457, 576, 576),
+                  (4099, 1520, 1520), (3, 1500, 1500), (50001, 20, 20), (9999, 1500, 40)]
     if preset == "imix":   # descriptor batches: the synthetic IMIX set (BASELINE configs[3])
         for n in (16 << 20, 100003, 4097, 65, 1):
             nbytes = cgck.load().cgck_imix_bytes(n)
