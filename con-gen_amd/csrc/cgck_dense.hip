@@ -99,7 +99,7 @@ __global__ __launch_bounds__(128) void dstr_kernel(KParams p)
 				const uint4 v4 = reinterpret_cast<const uint4 *>(sb)[lane];
 				const u32x4_t v = {v4.x, v4.y, v4.z, v4.w};
 				uint4 *dst = reinterpret_cast<uint4 *>(p.out + first) + lane;
-				asm volatile("s_waitcnt lgkmcnt(0)\n\tglobal_store_dwordx4 %0, %1, off sc1" ::"v"(dst), "v"(v)
+				asm volatile("s_waitcnt lgkmcnt(0)\n\tglobal_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(dst), "v"(v)
 					     : "memory");
 			}
 		} else { // the batch's last, partial chunk: per-frame stores
@@ -116,9 +116,9 @@ __global__ __launch_bounds__(128) void dstr_kernel(KParams p)
 		// later step's DMA, and the per-frame finish leaves its VALU.  Same
 		// barrier sequence as wave 0: one per step, one more per chunk.
 		for (uint32_t j = 0; j < nsteps; ++j) {
-			__builtin_amdgcn_s_barrier();
+			wg_barrier();
 			if ((j + 1) % C == 0) {
-				__builtin_amdgcn_s_barrier(); // chunk j / C staged
+				wg_barrier(); // chunk j / C staged
 				const uint32_t k = j / C;
 				const uint32_t *sb = so + (k & 1) * 8 * C;
 				const uint64_t first = (b + (uint64_t)k * G) * C * 4;
@@ -168,7 +168,7 @@ __global__ __launch_bounds__(128) void dstr_kernel(KParams p)
 			asm volatile("s_waitcnt vmcnt(%0)" ::"i"(kDsS * (D - 1) + 1) : "memory");
 		else
 			asm volatile("s_waitcnt vmcnt(%0)" ::"i"(kDsS * (D - 1)) : "memory");
-		__builtin_amdgcn_s_barrier();
+		wg_barrier();
 		uint32_t *sc = so + (W ? ((j / C) & 1) * 8 * C : 0); // this chunk's staging
 		if (mode == 3) { // lab: the DMA pipeline alone
 			issue(j + D);
@@ -243,7 +243,7 @@ __global__ __launch_bounds__(128) void dstr_kernel(KParams p)
 		if ((j + 1) % C == 0) {
 			asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // the chunk's outputs are in LDS
 			if (W)
-				__builtin_amdgcn_s_barrier(); // hand the chunk to the writer wave
+				wg_barrier(); // hand the chunk to the writer wave
 			else if (mode != 2) // lab mode 2: no output flush
 				flush(j / C, sc);
 		}

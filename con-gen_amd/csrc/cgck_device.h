@@ -164,6 +164,21 @@ __device__ __forceinline__ void glds16_nt(const void *gsrc, uint32_t lds_dst)
 		     : "memory");
 }
 
+// Inline-asm stores of more than 8 bytes end in "s_nop 1": the hardware needs a
+// wait state between such a store and a VALU write of its data VGPRs, and the
+// compiler, which inserts it after its own stores, cannot see an asm one (a
+// writer wave that reused the registers right away stored the next address
+// over two dwords of the data).
+
+// s_barrier that the optimizer cannot move memory operations across: the
+// builtin alone carries no memory semantics, so LDS loads after it may be
+// hoisted above it (a wave handing staged LDS data to another wave needs
+// both sides ordered).
+__device__ __forceinline__ void wg_barrier()
+{
+	asm volatile("s_barrier" ::: "memory");
+}
+
 // Write count u32 outputs staged in LDS (src) to global dst, threads t of nt
 // cooperating.  CGCK_FLUSH_POLICY (A/B builds): 0 nontemporal u32 stores, 1 u32
 // with sc1, 2 16-byte stores with sc1 (dst aligned up by a u32 head, u32
@@ -191,9 +206,9 @@ __device__ __forceinline__ void flush_u32(const uint32_t *src, uint32_t *dst, in
 		const uint32_t *s4 = src + head + 4 * i;
 		const u32x4_t v = {s4[0], s4[1], s4[2], s4[3]};
 #if CGCK_FLUSH_POLICY == 3
-		asm volatile("global_store_dwordx4 %0, %1, off nt" ::"v"(dst + head + 4 * i), "v"(v) : "memory");
+		asm volatile("global_store_dwordx4 %0, %1, off nt\n\ts_nop 1" ::"v"(dst + head + 4 * i), "v"(v) : "memory");
 #else
-		asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(dst + head + 4 * i), "v"(v) : "memory");
+		asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(dst + head + 4 * i), "v"(v) : "memory");
 #endif
 	}
 	for (int i = head + 4 * body + t; i < count; i += nt)

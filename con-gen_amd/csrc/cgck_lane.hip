@@ -431,13 +431,13 @@ __global__ __launch_bounds__(64) void lpd_kernel(KParams p)
 					const u32x4 v = {w.x, w.y, w.z, w.w};
 					uint4 *dst = reinterpret_cast<uint4 *>(p.out + first) + i * 64 + lane;
 					if (SP == 0)
-						asm volatile("s_waitcnt lgkmcnt(0)\n\tglobal_store_dwordx4 %0, %1, off nt"
+						asm volatile("s_waitcnt lgkmcnt(0)\n\tglobal_store_dwordx4 %0, %1, off nt\n\ts_nop 1"
 							     ::"v"(dst), "v"(v) : "memory");
 					else if (SP == 1)
-						asm volatile("s_waitcnt lgkmcnt(0)\n\tglobal_store_dwordx4 %0, %1, off"
+						asm volatile("s_waitcnt lgkmcnt(0)\n\tglobal_store_dwordx4 %0, %1, off\n\ts_nop 1"
 							     ::"v"(dst), "v"(v) : "memory");
 					else
-						asm volatile("s_waitcnt lgkmcnt(0)\n\tglobal_store_dwordx4 %0, %1, off sc1"
+						asm volatile("s_waitcnt lgkmcnt(0)\n\tglobal_store_dwordx4 %0, %1, off sc1\n\ts_nop 1"
 							     ::"v"(dst), "v"(v) : "memory");
 				}
 			} else {
@@ -524,6 +524,97 @@ __global__ __launch_bounds__(256) void lpd_lc_kernel(KParams p)
 	}
 }
 
+// lpd with a writer wave (A/B): wave 0 of a 128-thread workgroup is
+// lpd_kernel's DMA ring and reduce without any global store; at the end of a
+// chunk it hands the staged outputs to wave 1 across a barrier, and wave 1
+// reads them into registers (before the next step's barrier, so wave 0 may
+// refill the staging) and stores them as 16-byte sc1 runs.  The stores then
+// count only in the writer's vmcnt, not in front of wave 0's DMA waits.
+template <int D, int C>
+__global__ __launch_bounds__(128) void lpdw_kernel(KParams p)
+{
+	extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+	const int lane = threadIdx.x & 63;
+	const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+	const int len = (int)p.ip_len, nch = (len + 15) >> 4;
+	const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)smem);
+	uint32_t *so = reinterpret_cast<uint32_t *>(smem + D * 4096); // a chunk's outputs
+	const uint8_t *zero = (const uint8_t *)p.zero + (blockIdx.x & 63) * 64;
+	const uint64_t base = reinterpret_cast<uint64_t>(p.base) + p.l3_off;
+	const uint64_t last_chunk = (base + (p.n - 1) * p.stride + len - 1) & ~(uint64_t)15;
+	const uint64_t NS = (p.n + 63) / 64, NC = (NS + C - 1) / C, G = gridDim.x, b = blockIdx.x;
+	if (b >= NC)
+		return;
+	const uint64_t nsteps = (NC - b + G - 1) / G * C;
+	if (wave == 1) {
+		for (uint64_t j = 0; j < nsteps; ++j) {
+			wg_barrier();
+			if ((j + 1) % C != 0)
+				continue;
+			wg_barrier(); // chunk j / C staged
+			const uint64_t first = (b + (j / C) * G) * C * 64;
+			if (first + C * 64 <= p.n) {
+				u32x4_t v[C / 4];
+				const uint4 *s4 = reinterpret_cast<const uint4 *>(so);
+#pragma unroll
+				for (int i = 0; i < C / 4; ++i) {
+					const uint4 w = s4[i * 64 + lane];
+					v[i] = u32x4_t{w.x, w.y, w.z, w.w};
+				}
+				asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // staging free before the next barrier
+#pragma unroll
+				for (int i = 0; i < C / 4; ++i) {
+					uint4 *dst = reinterpret_cast<uint4 *>(p.out + first) + i * 64 + lane;
+					asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(dst), "v"(v[i]) : "memory");
+				}
+			} else {
+				for (int i = lane; i < C * 64; i += 64)
+					if (first + i < p.n)
+						gbl(p.out)[first + i] = so[i];
+				asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+			}
+		}
+		return;
+	}
+	auto gstep = [&](uint64_t j) { return (b + (j / C) * G) * C + j % C; };
+	const uint32_t span = (uint32_t)(63 * p.stride) + (uint32_t)len;
+	auto issue = [&](uint64_t j) {
+		const uint64_t gs = gstep(j);
+		const uint64_t a = base + gs * 64 * p.stride;
+		const uint32_t slot = lds0 + (uint32_t)(j % D) * 4096;
+#pragma unroll
+		for (int i = 0; i < 4; ++i) {
+			const uint32_t at = 1024 * i + 16 * lane;
+			const uint64_t src = a + at;
+			glds16_nt(j < nsteps && gs < NS && at < span && src <= last_chunk ? reinterpret_cast<const void *>(src)
+											  : zero,
+				  slot + 1024 * i);
+		}
+	};
+#pragma unroll
+	for (int d = 0; d < D - 1; ++d)
+		issue(d);
+	const int o = lane * (int)p.stride;
+	for (uint64_t j = 0; j < nsteps; ++j) {
+		issue(j + D - 1);
+		asm volatile("s_waitcnt vmcnt(%0)" ::"i"(4 * (D - 1)) : "memory");
+		wg_barrier();
+		const uint8_t *sl = smem + (uint32_t)(j % D) * 4096;
+		Quad q;
+#pragma unroll
+		for (int i = 0; i < 4; ++i)
+			q.c[i] = *reinterpret_cast<const uint4 *>(sl + o + 16 * (i < nch ? i : nch - 1));
+		asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // the slot is refilled next step
+		const uint64_t k = gstep(j) * 64 + lane;
+		lpa_reduce<false, true>(p, k, len, nch, q, so + (j % C) * 64 + lane);
+		if ((j + 1) % C == 0) {
+			asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // the chunk's outputs are in LDS
+			wg_barrier();                      // hand them to the writer
+		}
+	}
+	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 #endif // CGCK_LAB
 
 bool lpd_ok(const KParams &p)
@@ -573,6 +664,20 @@ hipError_t launch_lpd(const KParams &p, int num_cus, hipStream_t st)
 		default: CGCK_LPDLC(3); break;
 		}
 #undef CGCK_LPDLC
+		return hipGetLastError();
+	}
+	static const int wr = [] { // $CGCK_LPD_W: lpdw_kernel (writer wave), steps per chunk 16 | 32
+		const char *e = getenv("CGCK_LPD_W");
+		return e ? atoi(e) : 0;
+	}();
+	if (wr == 16 || wr == 32) {
+		if (wr == 16) {
+			CGCK_NOTE_KERNEL("lpdw_kernel<%d, 16>", 2);
+			hipLaunchKernelGGL((lpdw_kernel<2, 16>), g, dim3(128), 2 * 4096 + 16 * 256, st, p);
+		} else {
+			CGCK_NOTE_KERNEL("lpdw_kernel<%d, 32>", 2);
+			hipLaunchKernelGGL((lpdw_kernel<2, 32>), g, dim3(128), 2 * 4096 + 32 * 256, st, p);
+		}
 		return hipGetLastError();
 	}
 	static const bool sink = getenv("CGCK_LPD_SINK") != nullptr; // measure without output stores

@@ -162,7 +162,7 @@ __device__ __forceinline__ void t12_load(const u32x4_t CGCK_GLOBAL *src, uint64_
 __device__ __forceinline__ void t12_store(uint32_t *out, uint64_t g, const u32x4_t &v)
 {
 	u32x4_t *o = reinterpret_cast<u32x4_t *>(out) + g;
-	asm volatile("global_store_dwordx4 %0, %1, off nt" ::"v"(o), "v"(v) : "memory");
+	asm volatile("global_store_dwordx4 %0, %1, off nt\n\ts_nop 1" ::"v"(o), "v"(v) : "memory");
 }
 
 template <int DEPTH>
