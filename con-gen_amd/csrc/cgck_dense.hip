@@ -50,7 +50,7 @@ constexpr int kDsS = 6;                     // DMA instructions (KiB) per step
 constexpr uint32_t kDsSlot = kDsS * 1024;   // bytes per ring slot
 constexpr int kDsChunks = kDsS * 64;        // 16-byte chunks per slot
 
-template <int D, int C, bool W>
+template <int D, int C, bool W, int F>
 __global__ __launch_bounds__(128) void dstr_kernel(KParams p)
 {
 	extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -65,11 +65,17 @@ __global__ __launch_bounds__(128) void dstr_kernel(KParams p)
 	const uint8_t *zero = (const uint8_t *)p.zero + (blockIdx.x & 63) * 64;
 	const uint64_t base = reinterpret_cast<uint64_t>(p.base) + p.l3_off;
 	const uint64_t n = p.n, stride = p.stride;
-	const uint64_t NS = (n + 3) / 4, NC = (NS + C - 1) / C, G = gridDim.x, b = blockIdx.x;
+	// Super-chunks of SC frames, grid-interleaved: the first 4C are wave 0's
+	// C steps, the last F the writer wave's (W, F > 0: read by register loads
+	// while it waits for wave 0's chunk, so more bytes are in flight per CU
+	// than the LDS ring holds).
+	constexpr uint32_t SC = 4 * C + F;
+	const uint64_t NC = (n + SC - 1) / SC, G = gridDim.x, b = blockIdx.x;
 	if (b >= NC)
 		return;
 	const uint32_t nsteps = (uint32_t)((NC - b + G - 1) / G * C);
 	const uint32_t mode = p.contig; // lab A/B modes (launch_dstr); 0 in the product
+	auto cfirst = [&](uint32_t k) { return (b + (uint64_t)k * G) * SC; }; // chunk k's first frame
 
 	// a frame's result from its folded sums (tot over the frame, ip over the
 	// header, ps over src/dst), ip_hl and ip_p: result() of cgck_group.hip
@@ -93,7 +99,7 @@ __global__ __launch_bounds__(128) void dstr_kernel(KParams p)
 
 	// the outputs of chunk k (its 4C frames, staged at sb) to global memory
 	auto flush = [&](uint32_t k, const uint32_t *sb) {
-		const uint64_t first = (b + (uint64_t)k * G) * C * 4;
+		const uint64_t first = cfirst(k);
 		if (first + 4 * C <= n) {
 			if (lane < C) { // one 16-byte store per lane
 				const uint4 v4 = reinterpret_cast<const uint4 *>(sb)[lane];
@@ -109,19 +115,101 @@ __global__ __launch_bounds__(128) void dstr_kernel(KParams p)
 		}
 	};
 
+	// A frame read into registers by its 16 lanes (chunks c0 + 16 s + gl,
+	// clamped): the same sums as wave 0 takes from LDS; lane 0 stores it.
+	auto reg_frame = [&](uint64_t f, uint64_t a, int nch, const uint4 (&w)[kDsS]) __attribute__((always_inline)) {
+		const int q = (int)(a & 15);
+		uint32_t body = 0;
+		uint4 tw = make_uint4(0, 0, 0, 0); // the frame's last chunk, in the lane holding it
+		bool ht = false;
+#pragma unroll
+		for (int s2 = 0; s2 < kDsS; ++s2) {
+			const int c = 16 * s2 + gl;
+			body += c < nch ? sum4(w[s2], 0u) : 0u;
+			const bool t = c == nch - 1;
+			// opaque masks: a select chain over array elements would be turned
+			// into a dynamically indexed (scratch) load
+			const uint32_t mt = opaque(t ? ~0u : 0u);
+			tw = make_uint4(pick(mt, w[s2].x, tw.x), pick(mt, w[s2].y, tw.y), pick(mt, w[s2].z, tw.z),
+					pick(mt, w[s2].w, tw.w));
+			ht = ht || t;
+		}
+		uint32_t corr = 0;
+		if (gl == 0) { // the q bytes (whole dwords) before the frame
+			corr = hsum(q >= 4 ? w[0].x : 0u, 0);
+			corr = hsum(q >= 8 ? w[0].y : 0u, corr);
+			corr = hsum(q >= 12 ? w[0].z : 0u, corr);
+		}
+		if (ht) { // the bytes of the last chunk after the frame
+			const int e = q + len - 16 * (nch - 1);
+			if ((len & 3) == 0) {
+				corr = hsum(e <= 4 ? tw.y : 0u, corr);
+				corr = hsum(e <= 8 ? tw.z : 0u, corr);
+				corr = hsum(e <= 12 ? tw.w : 0u, corr);
+			} else {
+				corr = msum(tw, 0, e, 16, corr);
+			}
+		}
+		uint32_t tot = fold16(body) + (0xffffu - fold16(corr));
+		tot = fold16(gsum<16>(tot));
+		// header dwords: chunk c0 (this lane) and c0 + 1 (lane gl + 1, DPP row_shl:1)
+		const uint32_t n0 = __builtin_amdgcn_mov_dpp(w[0].x, 0x101, 0xF, 0xF, false);
+		const uint32_t n1 = __builtin_amdgcn_mov_dpp(w[0].y, 0x101, 0xF, 0xF, false);
+		const uint32_t n2 = __builtin_amdgcn_mov_dpp(w[0].z, 0x101, 0xF, 0xF, false);
+		const uint32_t n3 = __builtin_amdgcn_mov_dpp(w[0].w, 0x101, 0xF, 0xF, false);
+		const uint32_t d[8] = {w[0].x, w[0].y, w[0].z, w[0].w, n0, n1, n2, n3};
+		const int q4 = q >> 2;
+		const uint32_t m0 = opaque(q4 == 0 ? ~0u : 0u), m1 = opaque(q4 == 1 ? ~0u : 0u),
+			       m2 = opaque(q4 == 2 ? ~0u : 0u);
+		uint32_t h[5];
+#pragma unroll
+		for (int i = 0; i < 5; ++i)
+			h[i] = pick(m0, d[i], pick(m1, d[i + 1], pick(m2, d[i + 2], d[i + 3])));
+		const uint32_t hd = h[0] & 15;
+		uint32_t ip = hsum(h[4], hsum(h[3], hsum(h[2], hsum(h[1], hsum(h[0], 0)))));
+		if (gl == 0 && f < n) {
+			if (hd != 5) { // options or a short header (rare): from global memory
+				ip = 0;
+				for (uint32_t i = 0; i < hd; ++i)
+					ip = hsum(*gbl_at<const uint32_t>(a + 4 * i), ip);
+			}
+			const uint32_t r = fin(tot, fold16(ip), fold16(hsum(h[4], hsum(h[3], 0))), hd, (h[2] >> 8) & 0xffu);
+			gbl(p.out)[f] = r;
+			if (p.verdict)
+				gbl(p.verdict)[f] = (uint8_t)(!raw && len < (int)hd * 4 ? CGCK_BAD_LEN : 0);
+		}
+	};
+
 	if (W && wave == 1) {
 		// The writer wave finishes and stores each chunk's frames, a lane per
 		// frame, from the sums wave 0 staged: no store sits in the reducing
 		// wave's vmcnt, where (in order) it would hold the wait for every
-		// later step's DMA, and the per-frame finish leaves its VALU.  Same
-		// barrier sequence as wave 0: one per step, one more per chunk.
+		// later step's DMA, and the per-frame finish leaves its VALU.  One
+		// barrier per chunk (the staging is double-buffered: wave 0 refills a
+		// buffer only after the next chunk's barrier, which this wave reaches
+		// once it has read it); lab mode 6 adds wave 0's per-step barrier.
 		for (uint32_t j = 0; j < nsteps; ++j) {
-			wg_barrier();
+			if (mode == 6)
+				wg_barrier();
 			if ((j + 1) % C == 0) {
-				wg_barrier(); // chunk j / C staged
 				const uint32_t k = j / C;
+				// the chunk's F register frames: loads in flight across the wait
+				uint4 rw[F > 0 ? F / 4 : 1][kDsS];
+				uint64_t ra[F > 0 ? F / 4 : 1];
+				int rn[F > 0 ? F / 4 : 1];
+#pragma unroll
+				for (int u = 0; u < F / 4; ++u) {
+					const uint64_t f = cfirst(k) + 4 * C + 4 * u + g;
+					ra[u] = base + (f < n ? f : 0) * stride;
+					rn[u] = f < n ? (int)(((ra[u] & 15) + len + 15) >> 4) : 0;
+					const uint4 *c0 = reinterpret_cast<const uint4 *>(ra[u] & ~(uint64_t)15);
+#pragma unroll
+					for (int s2 = 0; s2 < kDsS; ++s2)
+						rw[u][s2] = ldc<true>(c0, 16 * s2 + gl, rn[u], p.zero);
+				}
+				wg_barrier(); // chunk j / C staged
 				const uint32_t *sb = so + (k & 1) * 8 * C;
-				const uint64_t first = (b + (uint64_t)k * G) * C * 4;
+				const uint64_t first = cfirst(k);
 				for (int i = lane; i < 4 * C; i += 64) {
 					const uint32_t v0 = sb[i], v1 = sb[4 * C + i];
 					const uint32_t hd = (v1 >> 16) & 15u;
@@ -134,16 +222,18 @@ __global__ __launch_bounds__(128) void dstr_kernel(KParams p)
 					else if (first + i < n)
 						gbl(p.out)[first + i] = r;
 				}
+#pragma unroll
+				for (int u = 0; u < F / 4; ++u)
+					reg_frame(cfirst(k) + 4 * C + 4 * u + g, ra[u], rn[u], rw[u]);
 			}
 		}
 		return;
 	}
 
-	auto gstep = [&](uint32_t j) { return (b + (uint64_t)(j / C) * G) * C + j % C; };
+	auto sfirst = [&](uint32_t j) { return cfirst(j / C) + 4 * (j % C); }; // step j's first frame
 	auto issue = [&](uint32_t j) { // step j of this wave into slot j % D
-		const uint64_t gs = gstep(j);
-		const bool live = j < nsteps && gs < NS;
-		const uint64_t f0 = gs * 4;
+		const uint64_t f0 = sfirst(j);
+		const bool live = j < nsteps && f0 < n;
 		const uint64_t fl = f0 + 3 < n ? f0 + 3 : n - 1;
 		const uint64_t a = (base + f0 * stride) & ~(uint64_t)15;
 		const uint64_t e = (base + fl * stride + len - 1) & ~(uint64_t)15; // the step's last chunk
@@ -168,13 +258,16 @@ __global__ __launch_bounds__(128) void dstr_kernel(KParams p)
 			asm volatile("s_waitcnt vmcnt(%0)" ::"i"(kDsS * (D - 1) + 1) : "memory");
 		else
 			asm volatile("s_waitcnt vmcnt(%0)" ::"i"(kDsS * (D - 1)) : "memory");
-		wg_barrier();
+		// The covering vmcnt alone orders this wave's own ds_reads behind its
+		// LDS-DMA (MI355X_MICROARCH.md: a barrier is needed only for other
+		// waves' reads), so no barrier per step.
+		if (!W || mode == 6)
+			wg_barrier();
 		uint32_t *sc = so + (W ? ((j / C) & 1) * 8 * C : 0); // this chunk's staging
 		if (mode == 3) { // lab: the DMA pipeline alone
 			issue(j + D);
 		} else {
-			const uint64_t gs = gstep(j);
-			const uint64_t f0 = gs * 4;
+			const uint64_t f0 = sfirst(j);
 			const uint64_t a = (base + f0 * stride) & ~(uint64_t)15;
 			const int o = (int)(base + (f0 + g) * stride - a); // frame g's byte offset in the slot
 			const int q = o & 15, c0 = o >> 4;
@@ -274,35 +367,39 @@ hipError_t launch_dstr(const KParams &p, int num_cus, hipStream_t st)
 	q.contig = 0;
 #if CGCK_LAB
 	// $CGCK_DSTR_D (ring slots 2 | 3 | 4), $CGCK_DSTR_C (steps per chunk 8 |
-	// 16 | 32), $CGCK_DSTR_W (1: the writer wave), $CGCK_DSTR_WPC (workgroups
+	// 16 | 32), $CGCK_DSTR_W (1: the writer wave), $CGCK_DSTR_F (frames per
+	// chunk the writer reads by register loads: 0 | 4 | 8), $CGCK_DSTR_WPC (workgroups
 	// per CU), $CGCK_DSTR_MODE (2 no output flush, 3 the DMA alone; results
-	// then undefined): A/B knobs of the lab build, read once
+	// then undefined; 6 a barrier per step in both waves): A/B knobs of the
+	// lab build, read once
 	static const int D = env_int("CGCK_DSTR_D", 3), C = env_int("CGCK_DSTR_C", 16),
-			 Wr = env_int("CGCK_DSTR_W", 1), wpc = env_int("CGCK_DSTR_WPC", 8);
+			 Wr = env_int("CGCK_DSTR_W", 1), wpc = env_int("CGCK_DSTR_WPC", 8),
+			 Fr = env_int("CGCK_DSTR_F", 0);
 	static const int mode = env_int("CGCK_DSTR_MODE", 0);
 	q.contig = mode;
-	const uint64_t NS = (p.n + 3) / 4, NC = (NS + C - 1) / C;
+	const uint64_t NC = (p.n + 4 * C + Fr - 1) / (4 * C + Fr);
 	const uint64_t waves = (uint64_t)num_cus * wpc;
 	const dim3 g((unsigned)(NC < waves ? NC : waves));
-#define CGCK_DSTR(DD, CC, WW)                                                                           \
-	if (D == DD && C == CC && (Wr == 1 || p.verdict) == WW) {                                                    \
-		CGCK_NOTE_KERNEL("dstr_kernel<%d, %d, %s>", DD, CC, tf(WW));                             \
-		hipLaunchKernelGGL((dstr_kernel<DD, CC, WW>), g, dim3((WW) ? 128 : 64),                   \
+#define CGCK_DSTR(DD, CC, WW, FF)                                                                       \
+	if (D == DD && C == CC && (Wr == 1 || p.verdict) == WW && Fr == FF) {                           \
+		CGCK_NOTE_KERNEL("dstr_kernel<%d, %d, %s, %d>", DD, CC, tf(WW), FF);                     \
+		hipLaunchKernelGGL((dstr_kernel<DD, CC, WW, FF>), g, dim3((WW) ? 128 : 64),               \
 				   (DD) * kDsSlot + ((WW) ? 64 : 16) * (CC), st, q);                        \
 		return hipGetLastError();                                                               \
 	}
-	CGCK_DSTR(3, 32, true) CGCK_DSTR(3, 8, true) CGCK_DSTR(2, 32, true) CGCK_DSTR(4, 16, true)
-	CGCK_DSTR(3, 16, false) CGCK_DSTR(3, 32, false) CGCK_DSTR(2, 32, false)
+	CGCK_DSTR(3, 16, true, 4) CGCK_DSTR(3, 16, true, 8) CGCK_DSTR(3, 32, true, 8) CGCK_DSTR(3, 32, true, 4)
+	CGCK_DSTR(3, 32, true, 0) CGCK_DSTR(3, 8, true, 0) CGCK_DSTR(2, 32, true, 0) CGCK_DSTR(4, 16, true, 0)
+	CGCK_DSTR(3, 16, false, 0) CGCK_DSTR(3, 32, false, 0) CGCK_DSTR(2, 32, false, 0)
 #undef CGCK_DSTR
 #else
 	// 8 workgroups (a reducing wave + the writer wave) per CU: 19 KiB of LDS
 	// each (three 6 KiB slots + two chunks of staged sums)
-	const uint64_t NS = (p.n + 3) / 4, NC = (NS + 15) / 16;
+	const uint64_t NC = (p.n + 63) / 64;
 	const uint64_t waves = (uint64_t)num_cus * 8;
 	const dim3 g((unsigned)(NC < waves ? NC : waves));
 #endif
-	CGCK_NOTE_KERNEL("dstr_kernel<3, 16, true>");
-	hipLaunchKernelGGL((dstr_kernel<3, 16, true>), g, dim3(128), 3 * kDsSlot + 64 * 16, st, q);
+	CGCK_NOTE_KERNEL("dstr_kernel<3, 16, true, 0>");
+	hipLaunchKernelGGL((dstr_kernel<3, 16, true, 0>), g, dim3(128), 3 * kDsSlot + 64 * 16, st, q);
 	return hipGetLastError();
 }
 
