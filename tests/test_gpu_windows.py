@@ -240,7 +240,7 @@ def test_last_kernel_names(engine):
     out = cgck.DeviceBuffer(4 * n)
     engine.synth_strided(buf.ptr, n, 1500, 1500, 5)
     engine.strided(buf.ptr, n, 1500, 0, 1500, cgck.GEN_BOTH, out.ptr)
-    assert engine.last_kernel == "dstr_kernel<3, 16, true>"
+    assert engine.last_kernel == "dstr_kernel<3, 16, true, 0>"
     engine.strided(buf.ptr, n, 1500, 0, 1500, cgck.VERIFY_TOY, out.ptr)   # verify: group
     assert engine.last_kernel == "cksum_kernel<16, 6, 1, false, true>"
     engine.strided(buf.ptr, n, 64, 0, 64, cgck.GEN_BOTH, out.ptr)

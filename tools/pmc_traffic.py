@@ -16,7 +16,7 @@ import statistics
 import sys
 
 KERNELS = {
-    "1500": "dstr_kernel<3, 16, true>",
+    "1500": "dstr_kernel<3, 16, true, 0>",
     "64": "lpd_kernel<2, 32, 2>",
     "imix": "lpw_kernel<true, 4>",
     "rss_hash": "toeplitz12x4_ab_kernel",
