@@ -1411,8 +1411,8 @@ __device__ __forceinline__ DescW lpw_desc_lds(const uint8_t *dslot)
 	return d;
 }
 
-template <bool DESC, int C>
-__global__ __launch_bounds__(64) void lpw_kernel(KParams p)
+template <bool DESC, int C, bool W>
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(W ? 4 : 1))) void lpw_kernel(KParams p)
 {
 	extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
 	uint8_t *dring = smem + 2 * kLpwSlot; // 2 x 1 KiB descriptor slots (64 lanes x 16 B; 768 B used)
@@ -1429,10 +1429,57 @@ __global__ __launch_bounds__(64) void lpw_kernel(KParams p)
 	auto gstep = [&](uint64_t j) { return (b + (j / C) * G) * C + j % C; };
 	auto first_of = [&](uint64_t j) { return j < nsteps ? gstep(j) * 64 : p.n; };
 
+	if (W && __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 1) {
+		// The writer wave (as dstr_kernel's): wave 0 stages a chunk's outputs
+		// and verdicts and hands them over at barrier H; this wave reads them
+		// into registers, releases the staging at barrier R (wave 0 meets it
+		// just before its first staging write of the next chunk) and stores
+		// them, so no output store sits in wave 0's in-order vmcnt (IMIX: the
+		// flush alone cost 3-7 points, profiles/r02/imix/README.md).
+		const uint64_t KD = nsteps / C;
+		for (uint64_t k = 0; k < KD; ++k) {
+			wg_barrier(); // H_k
+			const uint64_t f0 = gstep(k * C) * 64;
+			const uint64_t cntp = f0 < p.n ? (p.n - f0 < (uint64_t)C * 64 ? p.n - f0 : (uint64_t)C * 64) : 0;
+			uint32_t vo[C];
+			uint8_t vv[C];
+#pragma unroll
+			for (int i = 0; i < C; ++i) {
+				vo[i] = so[64 * i + l];
+				vv[i] = sv[64 * i + l];
+			}
+			asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+			if (k + 1 < KD)
+				wg_barrier(); // R_k: the staging is free
+#pragma unroll
+			for (int i = 0; i < C; ++i) {
+				if ((uint64_t)(64 * i + l) < cntp) {
+					if (p.out)
+						gbl(p.out)[f0 + 64 * i + l] = vo[i];
+					if (p.verdict)
+						gbl(p.verdict)[f0 + 64 * i + l] = vv[i];
+				}
+			}
+		}
+		return;
+	}
+
 	LpwStep cur = lpw_step<DESC>(p, first_of(0), load_desc<DESC>(p, first_of(0) + l, p.n));
 	LpwStep nxt = lpw_step<DESC>(p, first_of(1), load_desc<DESC>(p, first_of(1) + l, p.n));
 	LpwStep nn = nxt;
 	uint32_t kiss = 0;      // rounds issued (round k uses data slot k & 1)
+	// A full chunk's outputs leave as one 16-byte store per lane (C = 4: 256
+	// outputs) issued right AFTER the next DMA round, whose wait then leaves
+	// it in flight (vmcnt + 1): the store has a whole round to complete before
+	// a wait must cover it.  Stored at the end of its chunk instead (in front
+	// of the next round in the in-order vmcnt), the flush cost IMIX 3-7 points
+	// (profiles/r02/imix/README.md).  Lab mode 6: the end-of-chunk flush.
+	static_assert(C == 4, "one 16-byte store per lane per chunk");
+	const bool defer_ok = !W && p.out && !p.verdict && (reinterpret_cast<uintptr_t>(p.out) & 15) == 0 &&
+			      p.contig != 6 && p.contig != 5;
+	bool pend = false; // a chunk's outputs wait in the staging for the next round
+	int sage = 0;      // waits left that may leave the chunk store in flight
+	uint64_t pf0 = 0;  // its first packet
 	bool pre = false;       // cur's window 0 (with step j + 2's descriptors) already issued
 	for (uint64_t j = 0; j < nsteps; ++j) {
 		const uint64_t first = first_of(j);
@@ -1462,8 +1509,29 @@ __global__ __launch_bounds__(64) void lpw_kernel(KParams p)
 						ldsd + (uint32_t)((j + 3) & 1) * 1024, zero);
 				++kiss;
 				pre = nx;
-				asm volatile("s_waitcnt vmcnt(%0)" ::"i"(kLpwDma + 1) : "memory");
-				__builtin_amdgcn_s_barrier();
+				if (pend) {
+					typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+					const u32x4v v = reinterpret_cast<const u32x4v *>(so)[l];
+					u32x4v *dst = reinterpret_cast<u32x4v *>(p.out + pf0) + l;
+					asm volatile("s_waitcnt lgkmcnt(0)\n\tglobal_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(dst),
+						     "v"(v)
+						     : "memory");
+					pend = false;
+					sage = 2;
+				}
+				// The wait for the previous round.  A store issued after this
+				// round (sage 2) or after the previous one (sage 1) may stay in
+				// flight: it sits between the two rounds in the in-order count.
+				if (sage > 0) {
+					--sage;
+					asm volatile("s_waitcnt vmcnt(%0)" ::"i"(kLpwDma + 2) : "memory");
+				} else {
+					asm volatile("s_waitcnt vmcnt(%0)" ::"i"(kLpwDma + 1) : "memory");
+				}
+				// (the covering vmcnt alone orders this wave's reads behind its
+				// DMA; the barrier is kept in the one-wave form as measured)
+				if (!W)
+					__builtin_amdgcn_s_barrier();
 				if (t == 0) // step j + 2's descriptors came with window 0 of this step
 					nn = lpw_step<DESC>(p, first_of(j + 2), lpw_desc_lds<DESC>(dring + ((j + 2) & 1) * 1024));
 				if (p.contig == 4) // lab $CGCK_LPW_NOCONS: rounds without the per-window work
@@ -1547,11 +1615,14 @@ __global__ __launch_bounds__(64) void lpw_kernel(KParams p)
 				h = header<8, false>(w8, reinterpret_cast<const uint4 *>(cur.a0 & ~(uint64_t)15), cur.nch, cur.q,
 						     cur.len, p.flags, cur.ok);
 			}
-			if (!pre) // the last round was a zero round: drained before the next issue or a fallback
+			if (!pre) { // the last round was a zero round: drained before the next issue or a fallback
 				asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+				sage = 0; // (a looser count would no longer cover a round)
+			}
 		} else if (first < p.n) {
 			// not chained: the lane's packet straight from global memory
 			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+			sage = 0;
 			pre = false;
 			nn = lpw_step<DESC>(p, first_of(j + 2), load_desc<DESC>(p, first_of(j + 2) + l, p.n));
 			const uint4 *c0 = reinterpret_cast<const uint4 *>(cur.a0 & ~(uint64_t)15);
@@ -1572,6 +1643,14 @@ __global__ __launch_bounds__(64) void lpw_kernel(KParams p)
 				h = header<8, false>(w8, c0, cur.nch, cur.q, cur.len, p.flags, cur.ok);
 			}
 		}
+		if (W && j % C == 0 && j > 0)
+			wg_barrier(); // R: the writer has read the last chunk's staging
+		if (pend) { // no round came (a fallback or an empty step): flush before the staging is reused
+			asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+			for (int i = l; i < C * 64; i += 64)
+				gbl(p.out)[pf0 + i] = so[i];
+			pend = false;
+		}
 		if (first < p.n) {
 			const uint32_t r = fold16(acc) + (0xffffu - fold16(corr));
 			const Res res = result(p, cur.a0, cur.len, fold16(r), h);
@@ -1579,16 +1658,24 @@ __global__ __launch_bounds__(64) void lpw_kernel(KParams p)
 			so[slot] = res.out;
 			sv[slot] = (uint8_t)res.verdict;
 		}
-		if ((j + 1) % C == 0 || j + 1 == nsteps) {
+		if (W && (j + 1) % C == 0) {
+			asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // the chunk's outputs are in LDS
+			wg_barrier();                                      // H: hand them to the writer
+		} else if (!W && ((j + 1) % C == 0 || j + 1 == nsteps) && p.contig != 5) { // lab mode 5: no flush
 			// flush the chunk's outputs (packets [f0, f0 + 64 C) of the batch)
 			const uint64_t f0 = gstep(j - j % C) * 64;
 			asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 			const uint64_t cntp = f0 < p.n ? (p.n - f0 < (uint64_t)C * 64 ? p.n - f0 : (uint64_t)C * 64) : 0;
-			for (uint64_t i = l; i < cntp; i += 64) {
-				if (p.out)
-					gbl(p.out)[f0 + i] = so[i];
-				if (p.verdict)
-					gbl(p.verdict)[f0 + i] = sv[i];
+			if (defer_ok && cntp == (uint64_t)C * 64 && j + 1 < nsteps) {
+				pend = true; // stored after the next round's issue
+				pf0 = f0;
+			} else {
+				for (uint64_t i = l; i < cntp; i += 64) {
+					if (p.out)
+						gbl(p.out)[f0 + i] = so[i];
+					if (p.verdict)
+						gbl(p.verdict)[f0 + i] = sv[i];
+				}
 			}
 		}
 		cur = nxt;
@@ -1613,21 +1700,42 @@ hipError_t launch_lpw(const KParams &p, int num_cus, hipStream_t st)
 	q.contig = 0;
 #if CGCK_LAB
 	static const bool nocons = getenv("CGCK_LPW_NOCONS") != nullptr;
+	static const bool noflush = getenv("CGCK_LPW_NOFLUSH") != nullptr;
+	static const bool nodefer = getenv("CGCK_LPW_NODEFER") != nullptr; // the end-of-chunk flush
 	if (nocons)
 		q.contig = 4;
+	else if (noflush)
+		q.contig = 5;
+	else if (nodefer)
+		q.contig = 6;
 #endif
-	constexpr int C = 4; // 8 KiB windows: 19.3 KiB of LDS per wave, 8 waves per CU
+	constexpr int C = 4; // 8 KiB windows: 19.3 KiB of LDS per workgroup, 8 per CU
 	const uint64_t want = (p.n + 64 * C - 1) / (64 * C);
 	const uint64_t cap = (uint64_t)num_cus * wpc;
 	const dim3 g((unsigned)(want < cap ? (want ? want : 1) : cap));
 	const size_t lds = 2 * kLpwSlot + 2 * 1024 + C * 64 * 5;
-	if (p.desc) {
-		CGCK_NOTE_KERNEL("lpw_kernel<true, %d>", C);
-		hipLaunchKernelGGL((lpw_kernel<true, C>), g, dim3(64), lds, st, q);
-	} else {
-		CGCK_NOTE_KERNEL("lpw_kernel<false, %d>", C);
-		hipLaunchKernelGGL((lpw_kernel<false, C>), g, dim3(64), lds, st, q);
+#define CGCK_LPW(DD, WW)                                                                  \
+	do {                                                                              \
+		CGCK_NOTE_KERNEL("lpw_kernel<%s, %d, %s>", tf(DD), C, tf(WW));              \
+		hipLaunchKernelGGL((lpw_kernel<DD, C, WW>), g, dim3((WW) ? 128 : 64), lds, st, q); \
+	} while (0)
+#if CGCK_LAB
+	// $CGCK_LPW_W=1: the writer wave (lost: capped at 128 VGPRs it spills,
+	// 52.5-53.7 % vs 70.3-70.4 %, profiles/r02/imix/README.md)
+	static const bool wr = getenv("CGCK_LPW_W") && atoi(getenv("CGCK_LPW_W")) != 0;
+	if (wr) {
+		if (p.desc)
+			CGCK_LPW(true, true);
+		else
+			CGCK_LPW(false, true);
+		return hipGetLastError();
 	}
+#endif
+	if (p.desc)
+		CGCK_LPW(true, false);
+	else
+		CGCK_LPW(false, false);
+#undef CGCK_LPW
 	return hipGetLastError();
 }
 

@@ -18,7 +18,7 @@ import sys
 KERNELS = {
     "1500": "dstr_kernel<3, 16, true, 0>",
     "64": "lpd_kernel<2, 32, 2>",
-    "imix": "lpw_kernel<true, 4>",
+    "imix": "lpw_kernel<true, 4, false>",
     "rss_hash": "toeplitz12x4_ab_kernel",
     "dst_cache": "dst_cache_kernel<true>",
 }
