@@ -1446,7 +1446,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(W ? 4 : 1))
 #pragma unroll
 			for (int i = 0; i < C; ++i) {
 				vo[i] = so[64 * i + l];
-				vv[i] = sv[64 * i + l];
+				vv[i] = p.verdict ? sv[64 * i + l] : 0;
 			}
 			asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 			if (k + 1 < KD)
@@ -1474,7 +1474,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(W ? 4 : 1))
 	// a wait must cover it.  Stored at the end of its chunk instead (in front
 	// of the next round in the in-order vmcnt), the flush cost IMIX 3-7 points
 	// (profiles/r02/imix/README.md).  Lab mode 6: the end-of-chunk flush.
-	static_assert(C == 4, "one 16-byte store per lane per chunk");
+	static_assert(C % 4 == 0, "C / 4 16-byte stores per lane per chunk");
 	const bool defer_ok = !W && p.out && !p.verdict && (reinterpret_cast<uintptr_t>(p.out) & 15) == 0 &&
 			      p.contig != 6 && p.contig != 5;
 	bool pend = false; // a chunk's outputs wait in the staging for the next round
@@ -1511,11 +1511,14 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(W ? 4 : 1))
 				pre = nx;
 				if (pend) {
 					typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
-					const u32x4v v = reinterpret_cast<const u32x4v *>(so)[l];
-					u32x4v *dst = reinterpret_cast<u32x4v *>(p.out + pf0) + l;
-					asm volatile("s_waitcnt lgkmcnt(0)\n\tglobal_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(dst),
-						     "v"(v)
-						     : "memory");
+#pragma unroll
+					for (int i = 0; i < C / 4; ++i) {
+						const u32x4v v = reinterpret_cast<const u32x4v *>(so)[64 * i + l];
+						u32x4v *dst = reinterpret_cast<u32x4v *>(p.out + pf0) + 64 * i + l;
+						asm volatile("s_waitcnt lgkmcnt(0)\n\tglobal_store_dwordx4 %0, %1, off sc1\n\ts_nop 1"
+							     ::"v"(dst), "v"(v)
+							     : "memory");
+					}
 					pend = false;
 					sage = 2;
 				}
@@ -1524,7 +1527,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(W ? 4 : 1))
 				// flight: it sits between the two rounds in the in-order count.
 				if (sage > 0) {
 					--sage;
-					asm volatile("s_waitcnt vmcnt(%0)" ::"i"(kLpwDma + 2) : "memory");
+					asm volatile("s_waitcnt vmcnt(%0)" ::"i"(kLpwDma + 1 + C / 4) : "memory");
 				} else {
 					asm volatile("s_waitcnt vmcnt(%0)" ::"i"(kLpwDma + 1) : "memory");
 				}
@@ -1656,7 +1659,8 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(W ? 4 : 1))
 			const Res res = result(p, cur.a0, cur.len, fold16(r), h);
 			const int slot = (int)(j % C) * 64 + l;
 			so[slot] = res.out;
-			sv[slot] = (uint8_t)res.verdict;
+			if (p.verdict) // (the verdict staging is allocated only with verdicts)
+				sv[slot] = (uint8_t)res.verdict;
 		}
 		if (W && (j + 1) % C == 0) {
 			asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // the chunk's outputs are in LDS
@@ -1713,13 +1717,30 @@ hipError_t launch_lpw(const KParams &p, int num_cus, hipStream_t st)
 	const uint64_t want = (p.n + 64 * C - 1) / (64 * C);
 	const uint64_t cap = (uint64_t)num_cus * wpc;
 	const dim3 g((unsigned)(want < cap ? (want ? want : 1) : cap));
-	const size_t lds = 2 * kLpwSlot + 2 * 1024 + C * 64 * 5;
+	const size_t lds = 2 * kLpwSlot + 2 * 1024 + C * 64 * (p.verdict ? 5 : 4);
 #define CGCK_LPW(DD, WW)                                                                  \
 	do {                                                                              \
 		CGCK_NOTE_KERNEL("lpw_kernel<%s, %d, %s>", tf(DD), C, tf(WW));              \
 		hipLaunchKernelGGL((lpw_kernel<DD, C, WW>), g, dim3((WW) ? 128 : 64), lds, st, q); \
 	} while (0)
 #if CGCK_LAB
+	// $CGCK_LPW_C=8: chunks of 8 steps for batches without verdicts (20 KiB
+	// of LDS per workgroup)
+	static const bool c8 = getenv("CGCK_LPW_C") && atoi(getenv("CGCK_LPW_C")) == 8;
+	if (c8 && !p.verdict) {
+		constexpr int C8 = 8;
+		const uint64_t want8 = (p.n + 64 * C8 - 1) / (64 * C8);
+		const dim3 g8((unsigned)(want8 < cap ? (want8 ? want8 : 1) : cap));
+		const size_t lds8 = 2 * kLpwSlot + 2 * 1024 + C8 * 64 * 4;
+		if (p.desc) {
+			CGCK_NOTE_KERNEL("lpw_kernel<true, 8, false>");
+			hipLaunchKernelGGL((lpw_kernel<true, C8, false>), g8, dim3(64), lds8, st, q);
+		} else {
+			CGCK_NOTE_KERNEL("lpw_kernel<false, 8, false>");
+			hipLaunchKernelGGL((lpw_kernel<false, C8, false>), g8, dim3(64), lds8, st, q);
+		}
+		return hipGetLastError();
+	}
 	// $CGCK_LPW_W=1: the writer wave (lost: capped at 128 VGPRs it spills,
 	// 52.5-53.7 % vs 70.3-70.4 %, profiles/r02/imix/README.md)
 	static const bool wr = getenv("CGCK_LPW_W") && atoi(getenv("CGCK_LPW_W")) != 0;

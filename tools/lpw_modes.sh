@@ -12,6 +12,7 @@ for m in ${CELLS:-full nodefer noflush full nodefer}; do
   noflush) E="CGCK_LPW_NOFLUSH=1" ;;
   nocons) E="CGCK_LPW_NOCONS=1" ;;
   w1) E="CGCK_LPW_W=1" ;;
+  c8) E="CGCK_LPW_C=8" ;;
   nodefer) E="CGCK_LPW_NODEFER=1" ;;
   *) E="CGCK_LPW_X=0" ;;
   esac
