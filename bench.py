@@ -14,11 +14,15 @@ cpu_baseline_cfg0.
     python bench.py --gpus N --steps K --warmup W
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
+Without a launcher, --gpus N > 1 starts torch.distributed.run with N ranks
+as a child process (before anything touches the GPU) and relays rank 0's
+line; under a launcher --gpus must equal WORLD_SIZE.
 Rank 0 prints one JSON line.  One process per GPU: WORLD_SIZE above the
 visible device count is refused unless --allow-shared-devices (rehearsals on
 a one-GPU box).  The checker leg is the only part that touches oracle/: every
 rank checks a sample of its own shard's outputs of this run against the
-oracle referee (the mismatch total is summed over ranks), and at N = 1 rank 0
+oracle referee (every 64 B packet, every 64th 1500 B / IMIX packet across
+the whole shard; the totals are summed over ranks), and at N = 1 rank 0
 times the reference's own subr.c checksum unit (oracle/_ref, when built) or
 the oracle restatement on a bounded sample of the same workload as the CPU
 baseline.  Host-resident burst rates of SURVEY §8(f) ranks 1-2 (tools/txburst,
@@ -57,9 +61,11 @@ def device_for(local_rank, world, ndev, allow_shared=False):
     return local_rank % ndev
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (= ranks, one process each); without WORLD_SIZE in the environment "
+                         "N > 1 starts torch.distributed.run with N ranks as a child process")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--packets", type=int, default=16 << 20, help="packets per GPU")
@@ -73,7 +79,67 @@ def parse():
     ap.add_argument("--allow-shared-devices", action="store_true",
                     help="let ranks share GPUs when WORLD_SIZE exceeds the visible devices "
                          "(rehearsals only: the line then says so)")
-    return ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def launch_decision(gpus, env):
+    """How this invocation runs (one process per GPU, as
+    con-gen runs one worker per RSS queue, con-gen.c:1062-1100).
+    Returns ("inprocess", world) or ("spawn", N).  Under a launcher
+    (WORLD_SIZE set) --gpus must equal WORLD_SIZE; without one, --gpus N > 1
+    asks this process to start the N ranks itself."""
+    ws = env.get("WORLD_SIZE")
+    if ws is None:
+        n = 1 if gpus is None else gpus
+        if n < 1:
+            raise SystemExit(f"bench.py: --gpus {n} < 1")
+        return ("spawn", n) if n > 1 else ("inprocess", 1)
+    ws = int(ws)
+    if gpus is not None and gpus != ws:
+        raise SystemExit(f"bench.py: --gpus {gpus} but WORLD_SIZE {ws} "
+                         "(one rank per GPU: launch with --nproc-per-node equal to --gpus)")
+    return ("inprocess", ws)
+
+
+def child_command(n, argv, port):
+    """torch.distributed.run over N local ranks, rendezvous on 127.0.0.1,
+    re-running this script with the same arguments (each rank then finds
+    WORLD_SIZE = N and runs in-process)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr", "127.0.0.1", "--master-port", str(port),
+            os.path.abspath(__file__)] + list(argv)
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n, argv):
+    """Run the N ranks as a child process (never exec: this process has not
+    touched the GPU, and an exec after HIP init is forbidden on this pool).
+    Rank 0's JSON line is relayed on stdout, everything else the child prints
+    on stdout goes to stderr; the exit code is the child's."""
+    import subprocess
+    cmd = child_command(n, argv, free_port())
+    print("bench.py: launching " + " ".join(cmd), file=sys.stderr, flush=True)
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, bufsize=1)
+    lines = 0
+    for line in p.stdout:
+        if line.startswith("{") and '"metric"' in line:
+            sys.stdout.write(line)
+            sys.stdout.flush()
+            lines += 1
+        else:
+            sys.stderr.write(line)
+            sys.stderr.flush()
+    rc = p.wait()
+    if rc == 0 and lines != 1:
+        print(f"bench.py: the {n}-rank child printed {lines} result lines", file=sys.stderr)
+        return 1
+    return rc
 
 
 class Dist:
@@ -154,8 +220,8 @@ def bench_strided(torch, dist, eng, cgck, n, size, plan, steps, warmup):
 
     wall, ev_ms = timed(torch, dist, eng, cgck, step, steps, warmup)
     kernel = eng.last_kernel
-    # this run's first outputs, for the checker leg
-    o = __import__("numpy").zeros(min(n, 65536), "uint32")
+    # every output of this run, downloaded once after the timed region, for the checker leg
+    o = __import__("numpy").zeros(n, "uint32")
     out.download(o, stream=eng.stream)
     eng.sync()
     buf.free()
@@ -183,7 +249,7 @@ def bench_imix(torch, dist, eng, cgck, n, plan, steps, warmup):
     eng.set_desc_layout(cgck.LAYOUT_PACKED)
     wall, ev_ms = timed(torch, dist, eng, cgck, step, steps, warmup)
     kernel = eng.last_kernel
-    o = __import__("numpy").zeros(min(n, 65536), "uint32")
+    o = __import__("numpy").zeros(n, "uint32")
     out.download(o, stream=eng.stream)
     eng.sync()
     eng.set_desc_layout(cgck.LAYOUT_ANY)
@@ -316,11 +382,17 @@ def burst_crossover(rows, cpu):
     return res
 
 
+# SURVEY §8(d) parity gate: 100 % of the 64 B batch (configs[1]); a strided
+# 1/64 sample over the WHOLE shard for 1500 B and IMIX (configs[2]-[4])
+CHECK_EVERY = {"64": 1, "1500": 64, "imix": 64}
+
+
 def checker_leg(res, plan, cgck):
     """Parity of this rank's outputs of this run against the oracle (the
     oracle is only the checker here), on its own shard (seed 0xC0C0 + rank):
-    the first 65536 packets of each workload, every 16th, and the first 4096
-    hashed tuples.  Returns {workload: [checked, mismatches]}."""
+    every packet of the 64 B batch, every 64th packet across the whole 1500 B
+    and IMIX batches (CHECK_EVERY), and the first 4096 hashed tuples.
+    Returns {workload: [checked, mismatches]}."""
     import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
@@ -329,11 +401,12 @@ def checker_leg(res, plan, cgck):
     for key, size in (("1500", 1500), ("64", 64)):
         if key in res:
             o = res[key]["out"]
-            bad, chk = P.check_synth_strided(len(o), size, size, plan["seed"], cgck.GEN_BOTH, o, 16)
+            bad, chk = P.check_synth_strided(len(o), size, size, plan["seed"], cgck.GEN_BOTH, o,
+                                             CHECK_EVERY[key])
             par[key] = [chk, bad]
     if "imix" in res:
         o = res["imix"]["out"]
-        bad, chk = P.check_synth_imix(len(o), plan["seed"], cgck.GEN_BOTH, o, 16)
+        bad, chk = P.check_synth_imix(len(o), plan["seed"], cgck.GEN_BOTH, o, CHECK_EVERY["imix"])
         par["imix"] = [chk, bad]
     if "rss" in res:
         host, got = res["rss"]["hash_sample"]
@@ -505,8 +578,12 @@ def roofline(n, size, ev_ms, kernel, traffic_key, extra_bytes=0):
 
 def main():
     args = parse()
+    how, world = launch_decision(args.gpus, os.environ)
+    if how == "spawn":   # before torch is imported: nothing here has touched the GPU
+        sys.exit(spawn_ranks(world, sys.argv[1:]))
     import torch   # first: the process then shares torch's HIP runtime
     dist = Dist()
+    assert dist.world == world
     # one rank per GPU; a rehearsal on fewer GPUs must say so
     dev = device_for(dist.local, dist.world, torch.cuda.device_count(), args.allow_shared_devices)
     torch.cuda.set_device(dev)

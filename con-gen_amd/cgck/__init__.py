@@ -67,6 +67,7 @@ EXPORTS = (
     "toeplitz_hash", "rss_hash4", "cgck_toeplitz", "cgck_dst_cache", "cgck_dst_cache_host",
     "cgck_burst_open", "cgck_burst_close", "cgck_thread_ctx", "cgck_set_error_handler",
     "cgck_rx_begin", "cgck_rx_end", "cgck_window_stats", "cgck_ctx_last_kernel", "cgck_set_desc_layout",
+    "cgck_ctx_set_kernel",
 )
 # Descriptor layout hint (cgck_set_desc_layout)
 LAYOUT_ANY = 0
@@ -113,6 +114,7 @@ def bind(path):
     L.cgck_ctx_stream.restype = _vp
     L.cgck_ctx_stream.argtypes = [_vp]
     L.cgck_ctx_sync.argtypes = [_vp]
+    L.cgck_ctx_set_kernel.argtypes = [_vp, ctypes.c_char_p]
     L.cgck_set_desc_len_hint.argtypes = [_vp, _u32]
     L.cgck_set_desc_layout.argtypes = [_vp, _u32]
     L.cgck_strided.argtypes = [_vp, _vp, _u64, _u64, _u32, _u32, _u32, _vp, _vp, _vp, _vp]
@@ -327,12 +329,19 @@ class Event:
 class Engine:
     """One context (stream + staging) on one device — use one per thread."""
 
-    def __init__(self, device=0):
+    def __init__(self, device=0, kernel=None):
         L = load()
         p = _vp()
         _check(L.cgck_ctx_create(device, ctypes.byref(p)), "cgck_ctx_create")
         self.ctx = p.value
         self.device = device
+        if kernel is not None:
+            self.set_kernel(kernel)
+
+    def set_kernel(self, family):
+        """cgck_ctx_set_kernel: pin the kernel family ("auto", "group", "lpp",
+        "lpa", "slot2", "dstr", "lpd", "lpw"; the lab build knows more)."""
+        _check(load().cgck_ctx_set_kernel(self.ctx, family.encode()), "cgck_ctx_set_kernel")
 
     def close(self):
         if self.ctx:

@@ -92,6 +92,32 @@ extern "C" int cgck_device_count(void)
 	return n;
 }
 
+// Kernel family by name (cgck_ctx_set_kernel): 0 = the dispatcher's choice.
+// The product library knows its own families; the lab build also the A/B-only
+// ones and raw variant numbers (tools/sweep.py, $CGCK_KERNEL).  -1: unknown.
+static int family_of(const char *kf)
+{
+	static const struct {
+		const char *name;
+		int family;
+	} kFamilies[] = {
+		{"auto", 0}, {"group", 1}, {"lpp", 2}, {"slot2", 9}, {"lpa", 10}, {"dstr", 11}, {"lpd", 13}, {"lpw", 15},
+#if CGCK_LAB
+		{"slot", 3}, {"str", 11}, {"span", 12}, {"slotd", 14},
+#endif
+	};
+	for (const auto &f : kFamilies)
+		if (!strcmp(kf, f.name))
+			return f.family;
+#if CGCK_LAB
+	if (!strncmp(kf, "lpp", 3))
+		return atoi(kf + 3);
+	if (*kf >= '0' && *kf <= '9')
+		return atoi(kf);
+#endif
+	return -1;
+}
+
 extern "C" int cgck_ctx_create(int device, cgck_ctx_t **out)
 {
 	if (!out)
@@ -115,11 +141,8 @@ extern "C" int cgck_ctx_create(int device, cgck_ctx_t **out)
 	c->num_cus = prop.multiProcessorCount;
 	c->last_kernel = "";
 	c->desc_len_hint = 1500;
-	if (const char *kf = getenv("CGCK_KERNEL"))
-		c->family = !strcmp(kf, "group") ? 1 : !strcmp(kf, "lpp") ? 2 : !strcmp(kf, "slot") ? 3
-			  : !strcmp(kf, "slot2") ? 9 : !strcmp(kf, "lpa") ? 10 : !strcmp(kf, "str") || !strcmp(kf, "dstr") ? 11
-			  : !strcmp(kf, "span") ? 12 : !strcmp(kf, "lpd") ? 13 : !strcmp(kf, "slotd") ? 14 : !strcmp(kf, "lpw") ? 15
-			  : !strncmp(kf, "lpp", 3) ? atoi(kf + 3) : atoi(kf);
+	if (const char *kf = CGCK_ENV("CGCK_KERNEL")) // lab build only
+		c->family = family_of(kf);
 	hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
 	if (e != hipSuccess) {
 		free(c);
@@ -132,6 +155,17 @@ extern "C" int cgck_ctx_create(int device, cgck_ctx_t **out)
 		return set_err(-EIO, "zero chunk: %s", hipGetErrorString(e));
 	}
 	*out = c;
+	return 0;
+}
+
+extern "C" int cgck_ctx_set_kernel(cgck_ctx_t *c, const char *name)
+{
+	if (!c || !name)
+		return set_err(-EINVAL, "cgck_ctx_set_kernel: NULL argument");
+	const int f = family_of(name);
+	if (f < 0)
+		return set_err(-EINVAL, "cgck_ctx_set_kernel: unknown kernel family \"%s\"", name);
+	c->family = f;
 	return 0;
 }
 
@@ -211,7 +245,7 @@ static int check_flags(uint32_t flags)
 	if (flags & ~known)
 		return set_err(-EINVAL, "cgck: unknown flag bits 0x%x", flags & ~known);
 	if ((flags & CGCK_RAW) && (flags & ~CGCK_RAW))
-		return set_err(-EINVAL, "cgck: CGCK_RAW excludes every other flag");
+		return set_err(-EINVAL, "cgck: the RAW flag excludes every other flag");
 	if (!(flags & (CGCK_RAW | CGCK_IP | CGCK_L4)))
 		return set_err(-EINVAL, "cgck: flags select no checksum (RAW, IP or L4)");
 	return 0;
@@ -279,7 +313,8 @@ static int burst_launch(cgck_ctx *c)
 {
 	__atomic_store_n(&c->bbox->alive, 1u, __ATOMIC_RELEASE);
 	hipError_t e = launch_burst_server(c->bbox_dev, c->bstage_dev, c->bscratch, (uint32_t *)c->bresp_dev,
-					   c->bresp_dev + c->bresp_ver, c->d_zero, c->bstream);
+					   c->bresp_dev + c->bresp_ver, c->d_zero, (uint32_t)c->bstage_cap, c->bmax,
+					   c->bstream);
 	if (e != hipSuccess) {
 		__atomic_store_n(&c->bbox->alive, 0u, __ATOMIC_RELEASE);
 		return set_err(-EIO, "burst server launch: %s", hipGetErrorString(e));
@@ -298,15 +333,14 @@ static int burst_launch(cgck_ctx *c)
 // caps are where the server stopped beating the launch path on the registered
 // RX window at 64 / 576 / 1500 B (tools/txburst, profiles/r02/burst).  TX
 // flushes (mixed 20 B / full-size entries) keep the launch path.
-// $CGCK_SERVER_PKTS / _BYTES / _COPY override the caps for A/B runs.
-static size_t env_size(const char *name, size_t dflt)
+// $CGCK_SERVER_PKTS / _BYTES / _COPY override the caps for A/B runs (lab build).
+static size_t env_size(const char *v, size_t dflt)
 {
-	const char *v = getenv(name);
 	return v && *v ? (size_t)strtoull(v, nullptr, 0) : dflt;
 }
-static const size_t kServerBytes = env_size("CGCK_SERVER_BYTES", 96 << 10);
-static const uint64_t kServerPkts = env_size("CGCK_SERVER_PKTS", 64); // 4x for packets <= 80 B
-static const size_t kServerCopy = env_size("CGCK_SERVER_COPY", 32 << 10);
+static const size_t kServerBytes = env_size(CGCK_ENV("CGCK_SERVER_BYTES"), 96 << 10);
+static const uint64_t kServerPkts = env_size(CGCK_ENV("CGCK_SERVER_PKTS"), 64); // 4x for packets <= 80 B
+static const size_t kServerCopy = env_size(CGCK_ENV("CGCK_SERVER_COPY"), 32 << 10);
 
 // Offsets in the request block of n descriptors and `staged` packet bytes
 // copied into it (0: read in place).
@@ -369,6 +403,12 @@ static int burst_serve(cgck_ctx *c, const uint8_t *base_dev, uint64_t n, uint32_
 		}
 		if (now_s() - t0 > 2.0)
 			return set_err(-ETIMEDOUT, "burst server: request %u not served in 2 s", seq);
+	}
+	const uint32_t bad = __atomic_load_n(&b->bad_req, __ATOMIC_ACQUIRE);
+	if (bad != c->bbad) {
+		c->bbad = bad;
+		return set_err(-EIO, "burst server: request %u refused (block header or descriptors outside the block)",
+			       seq);
 	}
 	return 0;
 }
@@ -704,6 +744,7 @@ extern "C" int cgck_burst_open(cgck_ctx_t *c, uint32_t max_pkts, size_t max_byte
 	c->bscratch = (uint8_t *)sc;
 	c->bmax = max_pkts;
 	c->bseq = 0;
+	c->bbad = 0;
 	return burst_launch(c);
 }
 
@@ -793,8 +834,14 @@ static int rss_wait_users(cgck_ctx *c)
 	RssUsers *u = (RssUsers *)c->rss_users;
 	if (!u)
 		return 0;
-	for (auto &x : u->ev)
-		HIP_TRY(hipEventSynchronize(x.second));
+	// every read of the old tables has finished: the list starts over, so it
+	// holds only the streams used since the last key change (an event
+	// recorded on a stream the caller has destroyed since still completes)
+	while (!u->ev.empty()) {
+		HIP_TRY(hipEventSynchronize(u->ev.back().second));
+		(void)hipEventDestroy(u->ev.back().second);
+		u->ev.pop_back();
+	}
 	return 0;
 }
 
@@ -1029,11 +1076,11 @@ extern "C" int cgck_dev_alloc(size_t bytes, void **ptr)
 	// $CGCK_DEV_ALLOC_FLAGS sets hipExtMallocWithFlags flags for requests up to
 	// $CGCK_DEV_ALLOC_CONTIG_MAX bytes (default 8 GiB).
 	static const unsigned cflags = [] {
-		const char *e = getenv("CGCK_DEV_ALLOC_FLAGS");
+		const char *e = CGCK_ENV("CGCK_DEV_ALLOC_FLAGS");
 		return e ? (unsigned)strtoul(e, nullptr, 0) : 0u;
 	}();
 	static const size_t cmax = [] {
-		const char *e = getenv("CGCK_DEV_ALLOC_CONTIG_MAX");
+		const char *e = CGCK_ENV("CGCK_DEV_ALLOC_CONTIG_MAX");
 		return e ? (size_t)strtoull(e, nullptr, 0) : (size_t)8 << 30;
 	}();
 	const unsigned aflags = bytes <= cmax ? cflags : 0u;
@@ -1042,7 +1089,7 @@ extern "C" int cgck_dev_alloc(size_t bytes, void **ptr)
 		if (e == hipSuccess)
 			return 0;
 		(void)hipGetLastError();
-		if (getenv("CGCK_ALLOC_VERBOSE"))
+		if (CGCK_ENV("CGCK_ALLOC_VERBOSE"))
 			fprintf(stderr, "cgck_dev_alloc: flags %#x for %zu bytes failed (%s), plain hipMalloc\n",
 				aflags, bytes, hipGetErrorString(e));
 	}

@@ -56,8 +56,8 @@ bool stream_ok(const KParams &p);
 hipError_t launch_slotd(const KParams &p, int num_cus, hipStream_t st);
 #endif
 
-// `kernel` = variant | flags (include/cgck.h is agnostic of this; $CGCK_KERNEL
-// overrides it for A/B runs):
+// `kernel` = variant | flags (cgck_ctx_set_kernel pins the variant by family
+// name; in the lab build so does $CGCK_KERNEL):
 //   variant (bits 0-3): 0 auto, 1 group (G lanes per packet), 2 lane per
 //     packet (lpp), 9 lane per 128-byte slot pipelined two deep (slot2, the
 //     default for mid-size packets), 10 lane per packet for aligned
@@ -147,7 +147,7 @@ hipError_t launch_cksum(const KParams &p0, uint32_t len_hint, int num_cus, int k
 		return launch_lpw(p, num_cus, st);
 	case 11:
 #if CGCK_LAB
-		if (getenv("CGCK_STR_OLD") && stream_ok(p)) // the first stream kernel (cgck_stream.hip)
+		if (CGCK_ENV("CGCK_STR_OLD") && stream_ok(p)) // the first stream kernel (cgck_stream.hip)
 			return launch_stream(p, num_cus, st);
 #endif
 		return launch_dstr(p, num_cus, st);

@@ -140,15 +140,18 @@ struct ThreadState {
 // The drop-ins read this on every call, so it is a plain pointer in the
 // initial-exec TLS model (one fs-relative load; a thread_local object with a
 // constructor costs a TLS wrapper call and an init guard per access).  The
-// state itself is allocated on the thread's first use and lives as long as
-// the thread's context does not need it any more (cgck_thread_release keeps
-// it for the counters).
+// state itself is allocated on the thread's first use and freed by
+// cgck_thread_release, which keeps only the counters.
 __attribute__((tls_model("initial-exec"))) thread_local ThreadState *t_st = nullptr;
+// the window counters of a released state (cgck_thread_release frees the state)
+__attribute__((tls_model("initial-exec"))) thread_local uint64_t t_stats_kept[4] = {0, 0, 0, 0};
 
 ThreadState &tstate()
 {
-	if (__builtin_expect(!t_st, 0))
+	if (__builtin_expect(!t_st, 0)) {
 		t_st = new ThreadState;
+		memcpy(t_st->stats, t_stats_kept, sizeof(t_stats_kept));
+	}
 	return *t_st;
 }
 
@@ -280,15 +283,17 @@ extern "C" cgck_ctx_t *cgck_thread_ctx(void) { return thread_ctx(); }
 
 extern "C" int cgck_thread_release(void)
 {
-	ThreadState &t = tstate();
-	t.txq.clear();
-	t.tx_open = false;
-	t.rx.clear();
-	t.rx_open = false;
-	if (t.ctx) {
-		cgck_ctx_destroy(t.ctx);
-		t.ctx = nullptr;
-	}
+	ThreadState *t = t_st;
+	if (!t)
+		return 0;
+	if (t->ctx)
+		cgck_ctx_destroy(t->ctx);
+	// Only the counters outlive the release (cgck_window_stats, in plain
+	// TLS): the state with its window queues, maps and burst-sized buffers is
+	// freed, so a pool that retires threads keeps nothing per thread.
+	memcpy(t_stats_kept, t->stats, sizeof(t_stats_kept));
+	delete t;
+	t_st = nullptr;
 	return 0;
 }
 
@@ -296,7 +301,7 @@ extern "C" int cgck_window_stats(uint64_t stats[4])
 {
 	if (!stats)
 		return set_err(-EINVAL, "cgck_window_stats: NULL");
-	memcpy(stats, tstate().stats, sizeof(tstate().stats));
+	memcpy(stats, t_st ? t_st->stats : t_stats_kept, sizeof(t_stats_kept));
 	return 0;
 }
 
@@ -314,6 +319,7 @@ extern "C" uint16_t in_cksum(void *data, int len)
 	}
 	ThreadState &t = tstate();
 	const uint8_t *b = (const uint8_t *)data;
+	bool rx_miss = false; // counted in stats[1] only when the call is computed here
 	if (t.rx_open) {
 		// ip_cksum(ip) at ip_input.c:51 / inet.c:322, or the ICMP message at
 		// ip_icmp.c:189, after the caller zeroed the field
@@ -329,7 +335,7 @@ extern "C" uint16_t in_cksum(void *data, int len)
 				return (uint16_t)(e.out >> 16);
 			}
 		}
-		t.stats[1]++;
+		rx_miss = true;
 	}
 	if (t.tx_open && len >= 20 && (b[0] >> 4) == 4 && len == (b[0] & 15) * 4) {
 		RegRange r;
@@ -340,6 +346,7 @@ extern "C" uint16_t in_cksum(void *data, int len)
 		}
 		t.stats[3]++;
 	}
+	t.stats[1] += rx_miss;
 	return (uint16_t)sync_region(data, (uint32_t)len, (uint32_t)len, CGCK_RAW);
 }
 
@@ -353,6 +360,7 @@ extern "C" uint16_t udp_cksum(struct ip *ipp, int len)
 	ThreadState &t = tstate();
 	const uint32_t hl = (ip[0] & 15) * 4;
 	const uint32_t ip_len = hl + (uint32_t)len;
+	bool rx_miss = false; // counted in stats[1] only when the call is computed here
 	if (t.rx_open) {
 		// tcp_cksum(ip, ip->ip_len) at tcp_input.c:78 / inet.c:145, or
 		// udp_cksum(ip, len) at udp_usrreq.c:89
@@ -364,7 +372,7 @@ extern "C" uint16_t udp_cksum(struct ip *ipp, int len)
 				return (uint16_t)(e.out >> 16);
 			}
 		}
-		t.stats[1]++;
+		rx_miss = true;
 	}
 	if (t.tx_open && hl >= 20 && ip_len <= 0xffff && (ip[9] == 6 || ip[9] == 17)) {
 		const int fo = ip[9] == 6 ? 16 : 6;
@@ -381,6 +389,7 @@ extern "C" uint16_t udp_cksum(struct ip *ipp, int len)
 	// The pseudo-header reads ip+9 and ip+12..19 whatever ip_hl says
 	// (subr.c:205-207), so at least 20 bytes are staged.
 	const uint32_t span = ip_len < 20 ? 20 : ip_len;
+	t.stats[1] += rx_miss;
 	return (uint16_t)(sync_region(ip, span, ip_len, CGCK_L4 | kFlagNoLenCheck) >> 16);
 }
 

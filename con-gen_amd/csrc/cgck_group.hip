@@ -225,7 +225,8 @@ __device__ __forceinline__ uint32_t sys_relaxed(const uint32_t *p)
 }
 
 __global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const uint8_t *req, uint8_t *scratch,
-							   uint32_t *out, uint8_t *verdict, const void *zero)
+							   uint32_t *out, uint8_t *verdict, const void *zero, uint32_t cap,
+							   uint32_t max_pkts)
 {
 	__shared__ uint32_t cmd; // 1 run the pending request, 2 exit
 	__shared__ uint4 hdr_w[4];
@@ -274,7 +275,12 @@ __global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const 
 			hdr_w[t] = v[0];
 		__syncthreads();
 		const BurstReq &h = *reinterpret_cast<const BurstReq *>(hdr_w);
-		const uint32_t chunks = (h.bytes + 15) / 16;
+		// The block is host-written: a header or descriptor that does not fit
+		// the block the context allocated is refused (counted in bad_req, the
+		// host's call fails) instead of steering the loads below out of it.
+		bool ok = h.n <= max_pkts && h.bytes <= cap && h.d_off >= sizeof(BurstReq) &&
+			  (uint64_t)h.d_off + 12ull * h.n <= h.bytes && (h.base || h.p_off <= h.bytes);
+		const uint32_t chunks = ok ? (h.bytes + 15) / 16 : 0;
 		// the rest of a larger block, 16 loads in flight per thread (64 KiB a
 		// round trip)
 		for (uint32_t at = kBurstFirst / 16; at < chunks; at += 16 * 256) {
@@ -296,16 +302,32 @@ __global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const 
 		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
 		__syncthreads();
 		__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-		const KParams p = {h.base ? reinterpret_cast<const uint8_t *>(h.base) : scratch + h.p_off,
-				   reinterpret_cast<const cgck_desc_t *>(scratch + h.d_off),
-				   h.n, 0, 0, 0, h.flags, out, verdict, nullptr, 0, zero};
-		if (h.max_len <= 80)
-			cksum_body<4, 2, 4, true, false>(p);
-		else
-			cksum_body<16, 6, 4, true, false>(p);
-		// every thread's outputs (and in-place stores) performed; thread 0's
-		// system-scope release then writes them back ahead of seq_done
-		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+		if (ok && !h.base) // packet bytes in the block: every descriptor inside it
+			for (uint32_t i = t; i < h.n; i += 256) {
+				const cgck_desc_t *d = reinterpret_cast<const cgck_desc_t *>(scratch + h.d_off) + i;
+				uint32_t fo_lo, fo_hi, w2;
+				__builtin_memcpy(&fo_lo, reinterpret_cast<const uint8_t *>(d), 4);
+				__builtin_memcpy(&fo_hi, reinterpret_cast<const uint8_t *>(d) + 4, 4);
+				__builtin_memcpy(&w2, reinterpret_cast<const uint8_t *>(d) + 8, 4);
+				const uint64_t end = ((uint64_t)fo_hi << 32 | fo_lo) + (w2 & 0xffffu) + (w2 >> 16);
+				ok = ok && fo_hi == 0 && end + h.p_off <= h.bytes;
+			}
+		ok = __syncthreads_and(ok);
+		if (ok) {
+			const KParams p = {h.base ? reinterpret_cast<const uint8_t *>(h.base) : scratch + h.p_off,
+					   reinterpret_cast<const cgck_desc_t *>(scratch + h.d_off),
+					   h.n, 0, 0, 0, h.flags, out, verdict, nullptr, 0, zero};
+			if (h.max_len <= 80)
+				cksum_body<4, 2, 4, true, false>(p);
+			else
+				cksum_body<16, 6, 4, true, false>(p);
+		} else if (t == 0) {
+			__hip_atomic_fetch_add(&box->bad_req, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+		}
+		// every thread's outputs (and in-place stores) written back to host
+		// memory before thread 0 publishes seq_done: a system-scope release per
+		// thread (one fence per request, noise next to the ~5 us round trip)
+		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
 		__syncthreads();
 		if (t == 0)
 			__hip_atomic_store(&box->seq_done, last, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -315,9 +337,10 @@ __global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const 
 }
 
 hipError_t launch_burst_server(BurstBox *box, const uint8_t *req, uint8_t *scratch, uint32_t *out, uint8_t *verdict,
-			       const void *zero, hipStream_t st)
+			       const void *zero, uint32_t cap, uint32_t max_pkts, hipStream_t st)
 {
-	hipLaunchKernelGGL(burst_server_kernel, dim3(1), dim3(256), 0, st, box, req, scratch, out, verdict, zero);
+	hipLaunchKernelGGL(burst_server_kernel, dim3(1), dim3(256), 0, st, box, req, scratch, out, verdict, zero, cap,
+			   max_pkts);
 	return hipGetLastError();
 }
 
@@ -344,7 +367,7 @@ hipError_t launch_group(const KParams &p, uint32_t max_len, int num_cus, bool nt
 	// 48 blocks per CU: 80.4 % vs 78.5-78.9 % at 24 and 78.2 % at 16 on one box
 	// (tools/bpc_sweep.sh): shorter contiguous block ranges
 	static const int bpc = [] { // $CGCK_GRP_BPC: blocks per CU (A/B runs)
-		const char *e = getenv("CGCK_GRP_BPC");
+		const char *e = CGCK_ENV("CGCK_GRP_BPC");
 		return e && atoi(e) > 0 ? atoi(e) : 48;
 	}();
 	const int max_blocks = num_cus * bpc;

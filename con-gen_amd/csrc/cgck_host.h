@@ -53,6 +53,7 @@ struct cgck_ctx {
 	size_t bresp_ver;           // offset of the verdicts in bresp
 	uint8_t *bscratch;          // device: the server's copy of the block (bstage_cap bytes)
 	uint32_t bmax;              // packets per request
+	uint32_t bbad;              // bbox->bad_req as last seen
 	uint32_t bseq;
 	hipStream_t bstream; // the server's own stream (it stays resident)
 };

@@ -5,6 +5,18 @@
 
 #include "../../include/cgck.h"
 
+// Run-time A/B knobs ($CGCK_KERNEL, $CGCK_LPW_WPC, ...) exist only in the lab
+// build (libcgck_lab.so, -DCGCK_LAB): there CGCK_ENV reads the environment;
+// in the product library it is a null pointer, so every knob takes its
+// measured default and its name is not even in the binary.  $CGCK_DEVICE
+// (the drop-in symbols' device) is the product's one environment variable.
+#if CGCK_LAB
+#include <stdlib.h>
+#define CGCK_ENV(name) getenv(name)
+#else
+#define CGCK_ENV(name) ((const char *)nullptr)
+#endif
+
 namespace cgck {
 
 // Internal flag (never part of the public enum): skip the BAD_LEN rule so the
@@ -49,6 +61,8 @@ struct BurstBox {
 	uint32_t stop;       // host -> device: exit now
 	uint32_t alive;      // host sets 1 at launch; the server clears it on exit
 	uint64_t idle_ticks; // 100 MHz ticks without a request before the server exits
+	uint32_t bad_req;    // device -> host: requests refused by the server's block check
+	uint32_t pad;
 };
 
 // Header of a request block (the first 64 bytes of the burst staging).  The
@@ -70,7 +84,7 @@ static_assert(sizeof(BurstReq) == 64, "one header line");
 constexpr uint32_t kBurstFirst = 8192;
 
 hipError_t launch_burst_server(BurstBox *box, const uint8_t *req, uint8_t *scratch, uint32_t *out, uint8_t *verdict,
-			       const void *zero, hipStream_t st);
+			       const void *zero, uint32_t cap, uint32_t max_pkts, hipStream_t st);
 
 // Kernel selection flags (see cgck_dispatch.cpp) and the measured defaults
 // (tools/sweep.py; profiles/r01).  The group kernel streams whole lines per

@@ -627,7 +627,7 @@ bool lpd_ok(const KParams &p)
 hipError_t launch_lpd(const KParams &p, int num_cus, hipStream_t st)
 {
 	static const int wpc = [] { // $CGCK_LPD_WPC: waves per CU
-		const char *e = getenv("CGCK_LPD_WPC");
+		const char *e = CGCK_ENV("CGCK_LPD_WPC");
 		return e && atoi(e) > 0 ? atoi(e) : 8;
 	}();
 	const uint64_t want = (p.n + 64 * 16 - 1) / (64 * 16); // >= 16 steps per wave
@@ -635,18 +635,18 @@ hipError_t launch_lpd(const KParams &p, int num_cus, hipStream_t st)
 	const dim3 g((unsigned)(want < cap ? (want ? want : 1) : cap));
 #if CGCK_LAB
 	static const int depth = [] { // $CGCK_LPD_D: ring slots 2..4
-		const char *e = getenv("CGCK_LPD_D");
+		const char *e = CGCK_ENV("CGCK_LPD_D");
 		const int d = e ? atoi(e) : 0;
 		return d >= 2 && d <= 4 ? d : 2;
 	}();
 	static const int lc = [] { // $CGCK_LPD_LC: ring phases of the loader/consumer form (0: per-wave form)
-		const char *e = getenv("CGCK_LPD_LC");
+		const char *e = CGCK_ENV("CGCK_LPD_LC");
 		const int v = e ? atoi(e) : 0;
 		return v >= 2 && v <= 5 ? v : 0;
 	}();
 	if (lc) {
 		static const int wgpc = [] { // $CGCK_LPD_WGPC: workgroups per CU
-			const char *e = getenv("CGCK_LPD_WGPC");
+			const char *e = CGCK_ENV("CGCK_LPD_WGPC");
 			return e && atoi(e) > 0 ? atoi(e) : 3;
 		}();
 		const uint64_t want_lc = (p.n + 192 * 16 - 1) / (192 * 16); // >= 16 phases per workgroup
@@ -667,7 +667,7 @@ hipError_t launch_lpd(const KParams &p, int num_cus, hipStream_t st)
 		return hipGetLastError();
 	}
 	static const int wr = [] { // $CGCK_LPD_W: lpdw_kernel (writer wave), steps per chunk 16 | 32
-		const char *e = getenv("CGCK_LPD_W");
+		const char *e = CGCK_ENV("CGCK_LPD_W");
 		return e ? atoi(e) : 0;
 	}();
 	if (wr == 16 || wr == 32) {
@@ -680,17 +680,17 @@ hipError_t launch_lpd(const KParams &p, int num_cus, hipStream_t st)
 		}
 		return hipGetLastError();
 	}
-	static const bool sink = getenv("CGCK_LPD_SINK") != nullptr; // measure without output stores
+	static const bool sink = CGCK_ENV("CGCK_LPD_SINK") != nullptr; // measure without output stores
 	KParams q = p;
 	if (sink)
 		q.contig = 2;
 	static const int chunk = [] { // $CGCK_LPD_C: steps per output chunk (1, 4, 8, 16, 32, 64)
-		const char *e = getenv("CGCK_LPD_C");
+		const char *e = CGCK_ENV("CGCK_LPD_C");
 		const int c = e ? atoi(e) : 32;
 		return c == 1 || c == 4 || c == 8 || c == 16 || c == 64 ? c : 32;
 	}();
 	static const int sp = [] { // $CGCK_LPD_SP: flush store policy 0 nt, 1 default, 2 sc1
-		const char *e = getenv("CGCK_LPD_SP");
+		const char *e = CGCK_ENV("CGCK_LPD_SP");
 		const int v = e ? atoi(e) : 2;
 		return v >= 0 && v <= 2 ? v : 2;
 	}();
@@ -746,11 +746,11 @@ hipError_t launch_lpa(const KParams &p, int num_cus, bool nt, hipStream_t st)
 	// The per-packet reduce is short, so fewer waves with deeper register
 	// rings keep more bytes in flight per instruction issued.
 	static const int bpc = [] { // $CGCK_LPA_BPC: blocks per CU (A/B runs)
-		const char *e = getenv("CGCK_LPA_BPC");
+		const char *e = CGCK_ENV("CGCK_LPA_BPC");
 		return e && atoi(e) > 0 ? atoi(e) : 1;
 	}();
 	static const int depth = [] { // $CGCK_LPA_DEPTH: packet groups per lane in flight, 2..4
-		const char *e = getenv("CGCK_LPA_DEPTH");
+		const char *e = CGCK_ENV("CGCK_LPA_DEPTH");
 		const int d = e ? atoi(e) : 0;
 		return d >= 2 && d <= 4 ? d : 4;
 	}();
@@ -1110,7 +1110,8 @@ __device__ __forceinline__ void slot_reduce(const KParams &p, uint64_t cur, cons
 		wave_stage_put(ws, cur + M.owner, result(p, a0, len, fold16(r), h));
 }
 
-#ifndef CGCK_SLOT2_CHUNK
+#if !CGCK_LAB || !defined(CGCK_SLOT2_CHUNK) // compile-time A/B knob of the lab build only
+#undef CGCK_SLOT2_CHUNK
 #define CGCK_SLOT2_CHUNK 0
 #endif
 template <bool DESC, bool NT>
@@ -1259,7 +1260,7 @@ __global__ __launch_bounds__(64) void slotd_kernel(KParams p)
 hipError_t launch_slotd(const KParams &p, int num_cus, hipStream_t st)
 {
 	static const int wpc = [] { // $CGCK_SLOTD_WPC: waves per CU
-		const char *e = getenv("CGCK_SLOTD_WPC");
+		const char *e = CGCK_ENV("CGCK_SLOTD_WPC");
 		return e && atoi(e) > 0 ? atoi(e) : 6;
 	}();
 	const uint64_t want = (p.n + kSlotdChunk - 1) / kSlotdChunk;
@@ -1303,13 +1304,15 @@ hipError_t launch_slotd(const KParams &p, int num_cus, hipStream_t st)
 // profiles/r02/dma/lpw/): 69.9 % of 8 TB/s against slot2's 63.8 %; windows of
 // 7 / 9 / 10+ DMA instructions, fewer waves per CU, or the lane-per-packet walk
 // of each window (21-23 %) lose.
-#ifndef CGCK_LPW_DMA
+#if !CGCK_LAB || !defined(CGCK_LPW_DMA) // compile-time A/B knobs of the lab build only
+#undef CGCK_LPW_DMA
 #define CGCK_LPW_DMA 8
 #endif
 // 0: instruction i moves chunks [64 i, 64 i + 64) of the window (1 KiB
 // contiguous); 1: lane l moves chunks [8 l, 8 l + 8) over the 8 instructions,
 // so its own run lands in conflict-free LDS places (A/B builds)
-#ifndef CGCK_LPW_SLOTMAJOR
+#if !CGCK_LAB || !defined(CGCK_LPW_SLOTMAJOR)
+#undef CGCK_LPW_SLOTMAJOR
 #define CGCK_LPW_SLOTMAJOR 0
 #endif
 // LDS index (in 16-byte units) of window chunk idx
@@ -1697,15 +1700,15 @@ bool lpw_ok(const KParams &p)
 hipError_t launch_lpw(const KParams &p, int num_cus, hipStream_t st)
 {
 	static const int wpc = [] { // $CGCK_LPW_WPC: waves per CU
-		const char *e = getenv("CGCK_LPW_WPC");
+		const char *e = CGCK_ENV("CGCK_LPW_WPC");
 		return e && atoi(e) > 0 ? atoi(e) : 8;
 	}();
 	KParams q = p;
 	q.contig = 0;
 #if CGCK_LAB
-	static const bool nocons = getenv("CGCK_LPW_NOCONS") != nullptr;
-	static const bool noflush = getenv("CGCK_LPW_NOFLUSH") != nullptr;
-	static const bool nodefer = getenv("CGCK_LPW_NODEFER") != nullptr; // the end-of-chunk flush
+	static const bool nocons = CGCK_ENV("CGCK_LPW_NOCONS") != nullptr;
+	static const bool noflush = CGCK_ENV("CGCK_LPW_NOFLUSH") != nullptr;
+	static const bool nodefer = CGCK_ENV("CGCK_LPW_NODEFER") != nullptr; // the end-of-chunk flush
 	if (nocons)
 		q.contig = 4;
 	else if (noflush)
@@ -1726,7 +1729,7 @@ hipError_t launch_lpw(const KParams &p, int num_cus, hipStream_t st)
 #if CGCK_LAB
 	// $CGCK_LPW_C=8: chunks of 8 steps for batches without verdicts (20 KiB
 	// of LDS per workgroup)
-	static const bool c8 = getenv("CGCK_LPW_C") && atoi(getenv("CGCK_LPW_C")) == 8;
+	static const bool c8 = CGCK_ENV("CGCK_LPW_C") && atoi(CGCK_ENV("CGCK_LPW_C")) == 8;
 	if (c8 && !p.verdict) {
 		constexpr int C8 = 8;
 		const uint64_t want8 = (p.n + 64 * C8 - 1) / (64 * C8);
@@ -1743,7 +1746,7 @@ hipError_t launch_lpw(const KParams &p, int num_cus, hipStream_t st)
 	}
 	// $CGCK_LPW_W=1: the writer wave (lost: capped at 128 VGPRs it spills,
 	// 52.5-53.7 % vs 70.3-70.4 %, profiles/r02/imix/README.md)
-	static const bool wr = getenv("CGCK_LPW_W") && atoi(getenv("CGCK_LPW_W")) != 0;
+	static const bool wr = CGCK_ENV("CGCK_LPW_W") && atoi(CGCK_ENV("CGCK_LPW_W")) != 0;
 	if (wr) {
 		if (p.desc)
 			CGCK_LPW(true, true);
@@ -1826,7 +1829,7 @@ hipError_t launch_slot2(const KParams &p, int num_cus, bool nt, hipStream_t st)
 	// resident) and 3072 (2) measured the same.  $CGCK_BPC overrides the
 	// blocks per CU for A/B runs.
 	static const int bpc = [] {
-		const char *e = getenv("CGCK_BPC");
+		const char *e = CGCK_ENV("CGCK_BPC");
 		return e && atoi(e) > 0 ? atoi(e) : 8;
 	}();
 	const int mb = num_cus * bpc;

@@ -214,14 +214,14 @@ hipError_t launch_toeplitz(const RssParams &p0, int num_cus, hipStream_t st)
 		// tuples (the kernel is bound by the mixed read/write stream, not by
 		// LDS conflicts).
 		static const int var = [] { // $CGCK_RSS_VAR: 0 two-group loop, 1 nibble tables, 2 A/B pipelined
-			const char *e = getenv("CGCK_RSS_VAR");
+			const char *e = CGCK_ENV("CGCK_RSS_VAR");
 			return e ? atoi(e) : kDefaultRssVariant;
 		}();
 		// 1 block per CU with a deep register ring (below); at the earlier
 		// depth 3, 2 blocks per CU read 65.4 % of HBM peak vs 62.5 % at 8
 		// (tools/rss_sweep.sh)
 		static const int bpc = [] {
-			const char *e = getenv("CGCK_RSS_BPC");
+			const char *e = CGCK_ENV("CGCK_RSS_BPC");
 			return e && atoi(e) > 0 ? atoi(e) : 1;
 		}();
 		// ring depth 12 at 1 block per CU (181 VGPRs, no spills), in-process
@@ -230,7 +230,7 @@ hipError_t launch_toeplitz(const RssParams &p0, int num_cus, hipStream_t st)
 		// over 4; 8 +1.2 %, 10 +3.6 % over 6; 12 +2.9 %, 16 -1.7 % over 10
 		// (76.7 % of peak); 2 blocks/CU at depth 6 -8 %
 		static const int depth = [] { // $CGCK_RSS_DEPTH: groups per lane in flight, 2..6, 8, 10, 12, 16
-			const char *e = getenv("CGCK_RSS_DEPTH");
+			const char *e = CGCK_ENV("CGCK_RSS_DEPTH");
 			const int d = e ? atoi(e) : 0;
 			return (d >= 2 && d <= 6) || d == 8 || d == 10 || d == 12 || d == 16 ? d : 12;
 		}();
@@ -606,7 +606,7 @@ uint32_t dst_iters(uint32_t n, uint32_t cap, bool filter, uint64_t pass_lo, uint
 {
 	const uint64_t work = dst_expected(n, cap, filter, pass_lo, pass_hi);
 	const uint64_t per = work / ((uint64_t)num_cus * 256);
-	if (const char *e = getenv("CGCK_DST_ITERS")) // A/B sweeps (tools/rss_bench.py)
+	if (const char *e = CGCK_ENV("CGCK_DST_ITERS")) // A/B sweeps (tools/rss_bench.py)
 		return (uint32_t)atoi(e);
 	uint32_t it = 32;
 	while (it < (uint32_t)kDstIters && it < per)
@@ -623,7 +623,7 @@ hipError_t launch_dst_cache(const DstParams &p, int num_cus, hipStream_t st)
 	const uint64_t tile = (uint64_t)kDstWaves * 64 * p.iters;
 	uint64_t g = (dst_expected(p.n, p.cap, p.filter, p.pass_lo, p.pass_hi) + 2 * tile - 1) / tile;
 	uint64_t gmax = (uint64_t)num_cus * 4;
-	if (const char *e = getenv("CGCK_DST_WGS")) // A/B sweeps: workgroups per CU
+	if (const char *e = CGCK_ENV("CGCK_DST_WGS")) // A/B sweeps: workgroups per CU
 		gmax = (uint64_t)num_cus * atoi(e);
 	g = g < 8 ? 8 : g;
 	g = g > gmax ? gmax : g;

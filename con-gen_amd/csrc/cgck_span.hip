@@ -229,7 +229,7 @@ hipError_t launch_span(const KParams &p, int num_cus, bool nt, hipStream_t st)
 	// batch, so a grid larger than what fits at once (registers, LDS) would
 	// run its last blocks alone.  $CGCK_SPAN_BPC overrides (A/B runs).
 	static const int bpc_env = [] {
-		const char *e = getenv("CGCK_SPAN_BPC");
+		const char *e = CGCK_ENV("CGCK_SPAN_BPC");
 		return e ? atoi(e) : 0;
 	}();
 	static const int fit[2] = {

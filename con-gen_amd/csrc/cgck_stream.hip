@@ -333,16 +333,16 @@ bool stream_ok(const KParams &p)
 hipError_t launch_stream(const KParams &p, int num_cus, hipStream_t st)
 {
 	static const int wpc = [] { // $CGCK_STR_WPC: waves per CU (A/B runs)
-		const char *e = getenv("CGCK_STR_WPC");
+		const char *e = CGCK_ENV("CGCK_STR_WPC");
 		return e && atoi(e) > 0 ? atoi(e) : 8;
 	}();
 	static const bool lc = [] { // $CGCK_STR_LC=1: the loader/consumer form
-		const char *e = getenv("CGCK_STR_LC");
+		const char *e = CGCK_ENV("CGCK_STR_LC");
 		return e && *e == '1';
 	}();
 	if (lc) {
 		static const int ph = [] { // $CGCK_STR_LCPH: ring phases 3 or 4 (vmcnt counts <= 63)
-			const char *e = getenv("CGCK_STR_LCPH");
+			const char *e = CGCK_ENV("CGCK_STR_LCPH");
 			return e && atoi(e) == 3 ? 3 : 4;
 		}();
 		const uint64_t want = (p.n + 12 * 16 - 1) / (12 * 16); // >= 16 phases per workgroup
@@ -355,10 +355,10 @@ hipError_t launch_stream(const KParams &p, int num_cus, hipStream_t st)
 		return hipGetLastError();
 	}
 	static const int ring = [] { // $CGCK_STR_RING: ring slots (A/B runs)
-		const char *e = getenv("CGCK_STR_RING");
+		const char *e = CGCK_ENV("CGCK_STR_RING");
 		return e && atoi(e) >= 2 && atoi(e) <= 4 ? atoi(e) : 3;
 	}();
-	static const bool nocons = getenv("CGCK_STR_NOCONS") != nullptr;
+	static const bool nocons = CGCK_ENV("CGCK_STR_NOCONS") != nullptr;
 	KParams q = p;
 	if (nocons)
 		q.contig = 3;

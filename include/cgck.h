@@ -110,6 +110,12 @@ int cgck_ctx_create(int device, cgck_ctx_t **out);
 int cgck_ctx_destroy(cgck_ctx_t *ctx);
 void *cgck_ctx_stream(cgck_ctx_t *ctx);
 int cgck_ctx_sync(cgck_ctx_t *ctx);
+/* Pin the context's kernel family instead of the dispatcher's choice (parity
+ * tests of every family, A/B runs): "auto" (the default), "group", "lpp",
+ * "lpa", "slot2", "dstr", "lpd", "lpw".  A family that cannot take a batch
+ * (alignment, flags, lengths) still falls back to one that can, so results
+ * stay exact.  -EINVAL for an unknown name. */
+int cgck_ctx_set_kernel(cgck_ctx_t *ctx, const char *family);
 
 /* Device-resident batches.  `out` (u32 per packet: lo16 = IP/RAW result,
  * hi16 = L4 result), `verdict` (u8 per packet) and `bad` (u32[2] running

@@ -14,6 +14,19 @@ for p in (os.path.join(ROOT, "con-gen_amd"), os.path.join(ROOT, "oracle"), ROOT)
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU; run with -m gpu")
     config.addinivalue_line("markers", "slow: full-size (BASELINE config) parity runs")
+    config.addinivalue_line("markers", "lab: needs libcgck_lab.so (make -C tools lab); runs only when "
+                                       "the -m expression names it")
+
+
+def pytest_collection_modifyitems(config, items):
+    """Lab-build tests (A/B-only kernel families) stay out of the product
+    runs (`-m gpu`, `-m "not gpu"`) unless the marker expression asks."""
+    if "lab" in (config.getoption("markexpr") or ""):
+        return
+    skip = pytest.mark.skip(reason="lab build only: run with -m \"gpu and lab\"")
+    for it in items:
+        if "lab" in it.keywords:
+            it.add_marker(skip)
 
 
 def load_golden(name):

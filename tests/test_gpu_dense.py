@@ -12,7 +12,6 @@ while the next chunk is in flight), against the oracle referee
   store per lane issued after the next DMA round; batches without verdicts
   take that path, with verdicts (or an unaligned output array) the
   end-of-chunk flush."""
-import os
 
 import numpy as np
 import pytest
@@ -57,12 +56,8 @@ def run_device_strided(engine, buf, n, stride, l3, ln, flags, verdict=False, out
 
 @pytest.fixture(scope="module")
 def dstr_engine():
-    """An engine forced to the dstr family ($CGCK_KERNEL=dstr, variant 11)."""
-    os.environ["CGCK_KERNEL"] = "dstr"
-    try:
-        e = cgck.Engine(0)
-    finally:
-        os.environ.pop("CGCK_KERNEL", None)
+    """An engine pinned to the dstr family (cgck_ctx_set_kernel)."""
+    e = cgck.Engine(0, kernel="dstr")
     yield e
     e.close()
 

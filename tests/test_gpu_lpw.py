@@ -5,26 +5,20 @@ batches of every length class and alignment, on batches that are NOT packed
 (gapped, reversed, overlapping: its frame-by-frame steps must stay exact
 whatever the hint says), through the dispatcher's own choice, and on the
 full-size IMIX batch (BASELINE configs[3]) against the default slot2 path."""
-import os
-
 import numpy as np
 import pytest
 
 import cgck
 from test_gpu_parity import FLAG_SETS, random_batch
-from test_gpu_span import MIXES, packed_batch
+from batches import MIXES, packed_batch
 
 pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture(scope="module")
 def lpw():
-    """An engine forced to the lpw family ($CGCK_KERNEL=lpw, variant 15)."""
-    os.environ["CGCK_KERNEL"] = "lpw"
-    try:
-        e = cgck.Engine(0)
-    finally:
-        os.environ.pop("CGCK_KERNEL", None)
+    """An engine pinned to the lpw family (cgck_ctx_set_kernel)."""
+    e = cgck.Engine(0, kernel="lpw")
     e.set_desc_layout(cgck.LAYOUT_PACKED)
     yield e
     e.close()

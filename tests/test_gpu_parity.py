@@ -219,14 +219,7 @@ FAMILY_SHAPES = [  # (stride, l3_off, ip_len, packets); odd counts: every ip_hl 
 
 @pytest.fixture(scope="module")
 def family_engines():
-    import os
-    engines = {}
-    for f in FAMILIES:
-        os.environ["CGCK_KERNEL"] = f
-        try:
-            engines[f] = cgck.Engine(0)
-        finally:
-            os.environ.pop("CGCK_KERNEL", None)
+    engines = {f: cgck.Engine(0, kernel=f) for f in FAMILIES}
     yield engines
     for e in engines.values():
         e.close()

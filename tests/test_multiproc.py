@@ -133,3 +133,62 @@ def test_cpu_burst_leg_runs():
     assert r["cores"] == 1 and r["kind"] in ("reference", "port")
     assert {(x["pkt_len"], x["burst"]) for x in r["rows"]} == {(ln, b) for ln in bench.BURST_LENS for b in bench.BURSTS}
     assert all(x["us_per_burst"] > 0 for x in r["rows"])
+
+
+def test_launch_decision():
+    """--gpus 1 (or no flag) stays in-process; --gpus N > 1 without a launcher
+    spawns N ranks; under a launcher --gpus must equal WORLD_SIZE."""
+    assert bench.launch_decision(None, {}) == ("inprocess", 1)
+    assert bench.launch_decision(1, {}) == ("inprocess", 1)
+    assert bench.launch_decision(2, {}) == ("spawn", 2)
+    assert bench.launch_decision(8, {}) == ("spawn", 8)
+    assert bench.launch_decision(8, {"WORLD_SIZE": "8"}) == ("inprocess", 8)
+    assert bench.launch_decision(None, {"WORLD_SIZE": "4"}) == ("inprocess", 4)
+    with pytest.raises(SystemExit, match="--gpus 8 but WORLD_SIZE 2"):
+        bench.launch_decision(8, {"WORLD_SIZE": "2"})
+    with pytest.raises(SystemExit, match="--gpus 2 but WORLD_SIZE 1"):
+        bench.launch_decision(2, {"WORLD_SIZE": "1"})
+    with pytest.raises(SystemExit):
+        bench.launch_decision(0, {})
+
+
+def test_child_command_is_torchrun_on_loopback():
+    cmd = bench.child_command(4, ["--gpus", "4", "--steps", "3"], 29555)
+    assert cmd[1:3] == ["-m", "torch.distributed.run"]
+    assert "--nproc-per-node=4" in cmd and "--nnodes=1" in cmd
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert cmd[cmd.index("--master-port") + 1] == "29555"
+    assert cmd[-5].endswith("bench.py") and cmd[-4:] == ["--gpus", "4", "--steps", "3"]
+
+
+def test_spawn_relays_rank0_line(monkeypatch, capsys):
+    """spawn_ranks runs the child, passes the one JSON line to stdout and
+    everything else to stderr, and returns the child's exit code."""
+    import sys
+    line = '{"metric": "m", "value": 1.0, "n_gpus": 2}'
+    prog = f"print('noise'); print({line!r}); print('more')"
+    monkeypatch.setattr(bench, "child_command", lambda n, argv, port: [sys.executable, "-c", prog])
+    assert bench.spawn_ranks(2, []) == 0
+    out, err = capsys.readouterr()
+    assert out.strip() == line and "noise" in err and "more" in err
+    monkeypatch.setattr(bench, "child_command", lambda n, argv, port: [sys.executable, "-c", "raise SystemExit(3)"])
+    assert bench.spawn_ranks(2, []) == 3
+    monkeypatch.setattr(bench, "child_command", lambda n, argv, port: [sys.executable, "-c", "print('x')"])
+    assert bench.spawn_ranks(2, []) == 1        # rc 0 but no result line
+
+
+def test_gpus_2_starts_two_ranks_on_cpu():
+    """End to end without a GPU: `bench.py --gpus 2` starts torch.distributed.run
+    with two ranks, each rank runs in-process (WORLD_SIZE 2, so no second
+    spawn) and stops at the device check; the failure is the child's."""
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["HIP_VISIBLE_DEVICES"] = ""
+    r = subprocess.run([sys.executable, bench.__file__, "--gpus", "2", "--steps", "1"], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0
+    assert "--nproc-per-node=2" in r.stderr and "torch.distributed.run" in r.stderr
+    assert r.stderr.count("bench.py: launching") == 1                # the ranks did not re-spawn
+    assert "no GPU visible" in r.stderr
+    assert r.stdout == ""

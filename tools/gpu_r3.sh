@@ -1,0 +1,13 @@
+# Round-3 check in one GPU call: smoke, parity (fast + full-size), the N = 1
+# bench line, then the self-launched 2-rank rehearsal (bench.py --gpus 2 on
+# one card).  Every step has its own limit; the first failure ends the call.
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+rocminfo 2>/dev/null | grep -m3 -E "gfx|Marketing" > gpurun_out/info.txt || true
+timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 && echo "smoke ok" && \
+timeout -k 10 600 python -u -m pytest tests -m "gpu and not slow" -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 && echo "pytest ok" && \
+timeout -k 10 400 python -u -m pytest tests -m "gpu and slow" -x -v --timeout 200 --timeout-method thread > gpurun_out/pytest_slow.log 2>&1 && echo "slow ok" && \
+timeout -k 10 400 python bench.py --steps 10 --warmup 3 --cpu-seconds 5 > gpurun_out/bench.log 2> gpurun_out/bench.err && echo "bench ok" && \
+timeout -k 10 400 python bench.py --gpus 2 --allow-shared-devices --steps 5 --warmup 2 --no-rss --no-burst > gpurun_out/bench_n2.log 2> gpurun_out/bench_n2.err && echo "bench n2 ok"
+echo "exit=$?"
