@@ -692,6 +692,26 @@ int cgck::one_region(cgck_ctx *c, const void *src, uint32_t span, uint32_t ip_le
 	return 0;
 }
 
+// The server's stream.  A resident kernel holds its hardware queue until it
+// exits, and HIP multiplexes streams over a few hardware queues
+// (GPU_MAX_HW_QUEUES, 4 by default): a plain stream may share the server's
+// queue with another stream of the process, whose work then waits behind the
+// server until it idles out.  A stream with a CU mask gets a queue of its
+// own, so the server is given one (every CU enabled: the mask only buys the
+// dedicated queue).  $CGCK_BURST_PLAIN_STREAM (lab build) takes a plain one.
+static hipError_t burst_stream(const cgck_ctx *c, hipStream_t *st)
+{
+	if (CGCK_ENV("CGCK_BURST_PLAIN_STREAM"))
+		return hipStreamCreateWithFlags(st, hipStreamNonBlocking);
+	uint32_t mask[16];
+	const int words = (c->num_cus + 31) / 32 < 16 ? (c->num_cus + 31) / 32 : 16;
+	for (int i = 0; i < words; i++)
+		mask[i] = ~0u;
+	if (c->num_cus % 32 && words == (c->num_cus + 31) / 32)
+		mask[words - 1] = (1u << (c->num_cus % 32)) - 1;
+	return hipExtStreamCreateWithCUMask(st, (uint32_t)words, mask);
+}
+
 extern "C" int cgck_burst_open(cgck_ctx_t *c, uint32_t max_pkts, size_t max_bytes, uint32_t idle_ms)
 {
 	if (!c && !(c = thread_ctx()))
@@ -721,7 +741,7 @@ extern "C" int cgck_burst_open(cgck_ctx_t *c, uint32_t max_pkts, size_t max_byte
 	if (e == hipSuccess)
 		e = hipHostGetDevicePointer(&rd, rs, 0);
 	if (e == hipSuccess)
-		e = hipStreamCreateWithFlags(&c->bstream, hipStreamNonBlocking);
+		e = burst_stream(c, &c->bstream);
 	if (e != hipSuccess) {
 		for (void *h : {box, st, rs})
 			if (h)

@@ -31,8 +31,9 @@ def test_two_shards_two_contexts(size):
             out.free()
             par = bench.checker_leg({str(size): {"out": o}}, plan, cgck)
             res.append((plan, o, par[str(size)]))
+        every = bench.CHECK_EVERY[str(size)]
         for plan, o, (checked, bad) in res:
-            assert checked == n // 16 and bad == 0, plan
+            assert checked == -(-n // every) and bad == 0, plan
         assert not np.array_equal(res[0][1], res[1][1])    # different shards, different sums
         # a result of shard 1 checked against shard 0's generator must fail
         wrong = bench.checker_leg({str(size): {"out": res[1][1]}}, res[0][0], cgck)
