@@ -103,10 +103,7 @@ __global__ __launch_bounds__(128) void dstr_kernel(KParams p)
 		if (first + 4 * C <= n) {
 			if (lane < C) { // one 16-byte store per lane
 				const uint4 v4 = reinterpret_cast<const uint4 *>(sb)[lane];
-				const u32x4_t v = {v4.x, v4.y, v4.z, v4.w};
-				uint4 *dst = reinterpret_cast<uint4 *>(p.out + first) + lane;
-				asm volatile("s_waitcnt lgkmcnt(0)\n\tglobal_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(dst), "v"(v)
-					     : "memory");
+				bstore16<kSc1>(out_rsrc(p.out + first, 16 * C), 16 * lane, u32x4_t{v4.x, v4.y, v4.z, v4.w});
 			}
 		} else { // the batch's last, partial chunk: per-frame stores
 			for (int i = lane; i < 4 * C; i += 64)
@@ -217,8 +214,7 @@ __global__ __launch_bounds__(128) void dstr_kernel(KParams p)
 					if (p.verdict && first + i < n) // BAD_LEN, as the group kernel
 						gbl(p.verdict)[first + i] = (uint8_t)(!raw && len < (int)hd * 4 ? CGCK_BAD_LEN : 0);
 					if (first + 4 * C <= n)
-						asm volatile("s_waitcnt lgkmcnt(0)\n\tglobal_store_dword %0, %1, off sc1"
-							     ::"v"(p.out + first + i), "v"(r) : "memory");
+						bstore4<kSc1>(out_rsrc(p.out + first, 16 * C), 4 * i, r);
 					else if (first + i < n)
 						gbl(p.out)[first + i] = r;
 				}

@@ -164,11 +164,30 @@ __device__ __forceinline__ void glds16_nt(const void *gsrc, uint32_t lds_dst)
 		     : "memory");
 }
 
-// Inline-asm stores of more than 8 bytes end in "s_nop 1": the hardware needs a
-// wait state between such a store and a VALU write of its data VGPRs, and the
-// compiler, which inserts it after its own stores, cannot see an asm one (a
-// writer wave that reused the registers right away stored the next address
-// over two dwords of the data).
+// Output stores with a cache policy, as compiler-visible buffer stores
+// (raw_buffer_store with the gfx950 cache-policy operand: kSc1 = sc1, kNt =
+// nt).  The compiler's hazard recognizer then places the wait state a store
+// of more than 8 bytes needs before a VALU may overwrite its data VGPRs (an
+// inline-asm store needed a hand-written "s_nop 1": a writer wave that reused
+// the registers right away stored the next address over two dwords of the
+// data), and its own waits see the stores.  The resource covers
+// [base, base + bytes): `base` is wave-uniform; a store past `bytes` is
+// dropped by the range check instead of landing anywhere.
+constexpr int kSc1 = 16, kNt = 2, kDefaultPolicy = 0;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t out_rsrc(const void *base, uint32_t bytes)
+{
+	return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), 0, (int)bytes, 0x00020000);
+}
+template <int POLICY>
+__device__ __forceinline__ void bstore16(__amdgpu_buffer_rsrc_t r, uint32_t off, u32x4_t v)
+{
+	__builtin_amdgcn_raw_buffer_store_b128(v, r, (int)off, 0, POLICY);
+}
+template <int POLICY>
+__device__ __forceinline__ void bstore4(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t v)
+{
+	__builtin_amdgcn_raw_buffer_store_b32(v, r, (int)off, 0, POLICY);
+}
 
 // s_barrier that the optimizer cannot move memory operations across: the
 // builtin alone carries no memory semantics, so LDS loads after it may be

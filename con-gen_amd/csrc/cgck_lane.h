@@ -323,6 +323,15 @@ __device__ __forceinline__ uint64_t shfl64(uint64_t x, int src)
 	return ((uint64_t)hi << 32) | lo;
 }
 
+// x of lane `src` (wave-uniform), in SGPRs: readlane instead of a shuffle,
+// so values derived from it stay scalar (uniform loop bounds, branches)
+__device__ __forceinline__ uint64_t readlane64(uint64_t x, int src)
+{
+	const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, src);
+	const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), src);
+	return ((uint64_t)hi << 32) | lo;
+}
+
 struct DescW {
 	uint32_t lo, hi, w2;
 };

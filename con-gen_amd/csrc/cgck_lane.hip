@@ -388,7 +388,7 @@ __global__ __launch_bounds__(64) void lpd_kernel(KParams p)
 	for (int d = 0; d < D - 1; ++d)
 		issue(d);
 	const int o = lane * (int)p.stride; // packet L's byte offset in a slot
-	const bool stage = C > 1 && p.out;
+	constexpr bool stage = C > 1; // lpd_ok guarantees an output array
 	for (uint64_t j = 0; j < nsteps; ++j) {
 		issue(j + D - 1);
 		// Wait for step j's DMA.  Issued after it: the DMA of the D - 1 later
@@ -424,21 +424,12 @@ __global__ __launch_bounds__(64) void lpd_kernel(KParams p)
 			asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 			if (first + C * 64 <= p.n) {
 				const uint4 *s4 = reinterpret_cast<const uint4 *>(so);
+				const __amdgpu_buffer_rsrc_t rs = out_rsrc(p.out + first, C * 256);
+				constexpr int policy = SP == 0 ? kNt : SP == 1 ? kDefaultPolicy : kSc1;
 #pragma unroll
 				for (int i = 0; i < C / 4; ++i) {
-					typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 					const uint4 w = s4[i * 64 + lane];
-					const u32x4 v = {w.x, w.y, w.z, w.w};
-					uint4 *dst = reinterpret_cast<uint4 *>(p.out + first) + i * 64 + lane;
-					if (SP == 0)
-						asm volatile("s_waitcnt lgkmcnt(0)\n\tglobal_store_dwordx4 %0, %1, off nt\n\ts_nop 1"
-							     ::"v"(dst), "v"(v) : "memory");
-					else if (SP == 1)
-						asm volatile("s_waitcnt lgkmcnt(0)\n\tglobal_store_dwordx4 %0, %1, off\n\ts_nop 1"
-							     ::"v"(dst), "v"(v) : "memory");
-					else
-						asm volatile("s_waitcnt lgkmcnt(0)\n\tglobal_store_dwordx4 %0, %1, off sc1\n\ts_nop 1"
-							     ::"v"(dst), "v"(v) : "memory");
+					bstore16<policy>(rs, 16 * (i * 64 + lane), u32x4_t{w.x, w.y, w.z, w.w});
 				}
 			} else {
 				// the batch's last, partial chunk: per-packet stores, then drain
@@ -562,11 +553,10 @@ __global__ __launch_bounds__(128) void lpdw_kernel(KParams p)
 					v[i] = u32x4_t{w.x, w.y, w.z, w.w};
 				}
 				asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // staging free before the next barrier
+				const __amdgpu_buffer_rsrc_t rs = out_rsrc(p.out + first, C * 256);
 #pragma unroll
-				for (int i = 0; i < C / 4; ++i) {
-					uint4 *dst = reinterpret_cast<uint4 *>(p.out + first) + i * 64 + lane;
-					asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(dst), "v"(v[i]) : "memory");
-				}
+				for (int i = 0; i < C / 4; ++i)
+					bstore16<kSc1>(rs, 16 * (i * 64 + lane), v[i]);
 			} else {
 				for (int i = lane; i < C * 64; i += 64)
 					if (first + i < p.n)
@@ -619,7 +609,9 @@ __global__ __launch_bounds__(128) void lpdw_kernel(KParams p)
 
 bool lpd_ok(const KParams &p)
 {
-	return !p.desc && !p.verdict && !p.bad && !(p.flags & CGCK_STORE) && p.ip_len >= 20 && p.ip_len <= 64 &&
+	// an output array, 16-byte aligned: a chunk's outputs leave as 16-byte stores
+	return !p.desc && !p.verdict && !p.bad && !(p.flags & CGCK_STORE) && p.out &&
+	       (reinterpret_cast<uintptr_t>(p.out) & 15) == 0 && p.ip_len >= 20 && p.ip_len <= 64 &&
 	       p.stride <= 64 && p.stride * 63 + p.ip_len <= 4096 &&
 	       ((reinterpret_cast<uintptr_t>(p.base) | p.stride | p.l3_off) & 15) == 0;
 }
@@ -1360,7 +1352,10 @@ __device__ __forceinline__ LpwStep lpw_step(const KParams &p, uint64_t first, co
 	const bool ne = s.ok && s.nch > 0;
 	const uint64_t nonempty = __ballot(ne);
 	const int f = nonempty ? __ffsll((long long)nonempty) - 1 : 0; // first non-empty lane
-	const uint64_t base = shfl64(s.cs, f);
+	// the wave's values (base, span, windows) by readlane: scalar, so the
+	// window loop and the round bookkeeping (pre, pend, sage) stay uniform
+	// branches instead of exec-masked ones
+	const uint64_t base = readlane64(s.cs, f);
 	const uint64_t ds = s.cs - base, de = s.ce - base;
 	const bool far = ne && (s.cs < base || de > 0x7fffffffull); // before the first, or too far for 32 bits
 	const uint32_t rs = ne && !far ? (uint32_t)ds : 0u, re = ne && !far ? (uint32_t)de : 0u;
@@ -1373,6 +1368,7 @@ __device__ __forceinline__ LpwStep lpw_step(const KParams &p, uint64_t first, co
 	s.nwin = __any(brk) || span > 16 * kLpwWin ? 0u : (uint32_t)((span + kLpwWin - 1) / kLpwWin);
 	if (!__any(brk) && span == 0)
 		s.nwin = 1; // a step of empty packets: one window, nothing moved
+	s.nwin = __builtin_amdgcn_readfirstlane(s.nwin);
 	return s;
 }
 
@@ -1513,15 +1509,10 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(W ? 4 : 1))
 				++kiss;
 				pre = nx;
 				if (pend) {
-					typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+					const __amdgpu_buffer_rsrc_t rs = out_rsrc(p.out + pf0, C * 256);
 #pragma unroll
-					for (int i = 0; i < C / 4; ++i) {
-						const u32x4v v = reinterpret_cast<const u32x4v *>(so)[64 * i + l];
-						u32x4v *dst = reinterpret_cast<u32x4v *>(p.out + pf0) + 64 * i + l;
-						asm volatile("s_waitcnt lgkmcnt(0)\n\tglobal_store_dwordx4 %0, %1, off sc1\n\ts_nop 1"
-							     ::"v"(dst), "v"(v)
-							     : "memory");
-					}
+					for (int i = 0; i < C / 4; ++i)
+						bstore16<kSc1>(rs, 16 * (64 * i + l), reinterpret_cast<const u32x4_t *>(so)[64 * i + l]);
 					pend = false;
 					sage = 2;
 				}

@@ -56,11 +56,11 @@ def main():
             e0.synth_imix(buf.ptr, desc.ptr, n, 0xC0C0)
             for L, c in zip(libs, ctxs):
                 L.cgck_set_desc_len_hint(c, nbytes // n)
-                if w == "imixp":
-                    L.cgck_set_desc_layout(c, cgck.LAYOUT_PACKED)
-            work[w] = (lambda L, c, buf=buf, desc=desc: L.cgck_desc(c, buf.ptr, desc.ptr, n, cgck.GEN_BOTH,
-                                                                     out.ptr, None, None, None),
-                       nbytes + 16 * n)
+            layout = cgck.LAYOUT_PACKED if w == "imixp" else cgck.LAYOUT_ANY
+            pre = (lambda L, c, layout=layout: L.cgck_set_desc_layout(c, layout))
+            # the layout hint is per context: set on every launch (imix and imixp share the contexts)
+            work[w] = (lambda L, c, buf=buf, desc=desc, pre=pre: pre(L, c) or L.cgck_desc(
+                c, buf.ptr, desc.ptr, n, cgck.GEN_BOTH, out.ptr, None, None, None), nbytes + 16 * n)
             keep += [buf, desc]
         elif w == "rss":
             nt = 64 << 20

@@ -249,6 +249,128 @@ def analyze(body):
     return out, scratch
 
 
+def loops(blocks):
+    """Natural loops of the CFG: {header index: set of block indices}, from
+    the back edges (u -> h with h dominating u)."""
+    n = len(blocks)
+    idx = {b["label"]: i for i, b in enumerate(blocks)}
+    succ = [[idx[l] for l in b["succ"] if l in idx] for b in blocks]
+    pred = [[] for _ in range(n)]
+    for u in range(n):
+        for v in succ[u]:
+            pred[v].append(u)
+    reach = {0}
+    stack = [0]
+    while stack:
+        u = stack.pop()
+        for v in succ[u]:
+            if v not in reach:
+                reach.add(v)
+                stack.append(v)
+    dom = [set(reach) for _ in range(n)]
+    dom[0] = {0}
+    changed = True
+    while changed:
+        changed = False
+        for v in sorted(reach):
+            if v == 0:
+                continue
+            ps = [dom[u] for u in pred[v] if u in reach]
+            d = set.intersection(*ps) | {v} if ps else {v}
+            if d != dom[v]:
+                dom[v] = d
+                changed = True
+    out = defaultdict(set)
+    for u in reach:
+        for h in succ[u]:
+            if h in dom[u]:  # back edge u -> h
+                body = {h, u}
+                stack = [u]
+                while stack:
+                    x = stack.pop()
+                    for p_ in pred[x]:
+                        if p_ not in body and p_ in reach:
+                            body.add(p_)
+                            stack.append(p_)
+                out[h] |= body
+    return dict(out)
+
+
+def loop_segments(body):
+    """Per counted wait, the (dma, loads, stores) issued along the paths that
+    stay inside the innermost natural loop holding it, from that wait to the
+    next counted one: the steady state of the loop.  A drain (vmcnt(0)) ends a
+    path.  Returns [(N, block label, sorted set of (dma, loads, stores))]."""
+    blocks = blocks_of(body)
+    idx = {b["label"]: i for i, b in enumerate(blocks)}
+    lp = loops(blocks)
+    res = []
+    for bi, b in enumerate(blocks):
+        for k, ins in enumerate(b["ins"]):
+            if not (ins["op"] == "s_waitcnt" and ins["asm"] and (vmcnt_of(ins["text"]) or 0) > 0):
+                continue
+            inner = min((body_ for body_ in lp.values() if bi in body_), key=len, default=None)
+            if inner is None:
+                continue
+            counts = set()
+            seen = set()
+            work = [(bi, k + 1, (0, 0, 0), frozenset({("exec", "nz", 0)}))]
+            while work:
+                item = work.pop()
+                if item in seen:
+                    continue
+                seen.add(item)
+                cb, ck, cnt, facts = item
+                blk = blocks[cb]
+                stop = False
+                for ins2 in blk["ins"][ck:]:
+                    op = ins2["op"]
+                    if op == "s_waitcnt" and vmcnt_of(ins2["text"]) is not None:
+                        n2 = vmcnt_of(ins2["text"])
+                        if n2 == 0:
+                            stop = True          # a drain: the path leaves the counted regime
+                            break
+                        if ins2["asm"]:
+                            counts.add(cnt)
+                            stop = True
+                            break
+                    if VMEM.match(op):
+                        c = classify(op)
+                        cnt = tuple(min(v + 1, CAP) if i == c else v for i, v in enumerate(cnt))
+                    facts = step_known(facts, ins2)
+                if stop or max(cnt) >= CAP:   # a capped path is a per-packet store loop: no wait ahead
+                    continue
+                last = blk["ins"][-1] if blk["ins"] else None
+                succ = list(blk["succ"])
+                if last and last["op"] in ("s_cbranch_vccnz", "s_cbranch_vccz", "s_cbranch_execnz",
+                                           "s_cbranch_execz") and blk["targets"]:
+                    reg = "exec" if "exec" in last["op"] else "vcc"
+                    v = {r: vv for r, vv, _ in facts}.get(reg)
+                    taken = None if v is None else (v == "nz") == last["op"].endswith("nz")
+                    if taken is True:
+                        succ = blk["targets"]
+                    elif taken is False:
+                        succ = [x for x in succ if x not in blk["targets"]]
+                aged = frozenset((r, v, a if r == "exec" else a + 1) for r, v, a in facts
+                                 if r == "exec" or a + 1 <= FACT_AGE)
+                for lab in succ:
+                    j = idx.get(lab)
+                    if j is not None and j in inner:
+                        work.append((j, 0, cnt, aged))
+            res.append((vmcnt_of(ins["text"]), b["label"], sorted(counts)))
+    return res
+
+
+def check(asm, part):
+    """(metadata, steady segments, entry DMA counts) of one kernel: the facts
+    tests/test_isa_guard.py asserts."""
+    name, body, meta = kernel_text(asm, part)
+    waits, scratch = analyze(body)
+    entry = sorted({x[1] for _, _, _, st in waits for x in st if x[0] == "E"})
+    return {"name": name, "meta": meta, "scratch_ops": len(scratch), "steady": loop_segments(body),
+            "entry_dma": entry}
+
+
 def summary(body):
     """{N: sorted set of (origin, dma, loads, stores)} over the counted waits."""
     waits, scratch = analyze(body)
@@ -269,3 +391,5 @@ if __name__ == "__main__":
         for n, v in sorted(s.items()):
             print(f"  vmcnt({n}): {v}")
         print("  scratch ops:", len(scr))
+        for n, lab, c in loop_segments(body):
+            print(f"  steady vmcnt({n}) at {lab}: (dma, loads, stores) between waits {c}")
