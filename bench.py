@@ -256,12 +256,35 @@ def bench_imix(torch, dist, eng, cgck, n, plan, steps, warmup):
     wall_u, ev_u = timed(torch, dist, eng, cgck, step, max(2, steps // 2), min(warmup, 2))
     unhinted = {"kernel": eng.last_kernel, "kernel_ms": ev_u,
                 "frac": (nbytes + 16 * n) / (ev_u * 1e-3) / HBM_PEAK}
-    eng.set_desc_len_hint(1500)
+    ou = __import__("numpy").zeros(n, "uint32")
+    out.download(ou, stream=eng.stream)
+    eng.sync()
     buf.free()
     desc.free()
+    # The same IMIX frames in a receive ring: 2048 B slots, IPv4 at +14 (the
+    # netmap layout, netmap.c:116-126), no layout hint.  Algorithmic bytes are
+    # the frames', as for the packed set.
+    rbuf = cgck.DeviceBuffer(n * RING_SLOT)
+    rdesc = cgck.DeviceBuffer(12 * n)
+    eng.synth_imix_ring(rbuf.ptr, rdesc.ptr, n, RING_SLOT, RING_L3, plan["seed"])
+    eng.sync()
+    wall_r, ev_r = timed(torch, dist, eng, cgck,
+                         lambda: eng.desc(rbuf.ptr, rdesc.ptr, n, cgck.GEN_BOTH, out.ptr),
+                         max(2, steps // 2), min(warmup, 2))
+    ring = {"layout": f"{RING_SLOT} B slots, IPv4 at +{RING_L3}", "kernel": eng.last_kernel, "kernel_ms": ev_r,
+            "frac": (nbytes + 16 * n) / (ev_r * 1e-3) / HBM_PEAK,
+            "gpkt_s": n / (ev_r * 1e-3) / 1e9}
+    orr = __import__("numpy").zeros(n, "uint32")
+    out.download(orr, stream=eng.stream)
+    eng.sync()
+    eng.set_desc_len_hint(1500)
+    rbuf.free()
+    rdesc.free()
     out.free()
-    return wall, ev_ms, nbytes, o, kernel, unhinted
+    return wall, ev_ms, nbytes, (o, ou, orr), kernel, unhinted, ring
 
+
+RING_SLOT, RING_L3 = 2048, 14   # receive-ring layout of the IMIX frames (netmap slots)
 
 RSS_KEY = bytes.fromhex("6d5a56da255b0ec24167253d43a38fb0d0ca2bcbae7b30b477cb2da38030f20c6a42b73bbeac01fa")
 RSS_TUPLES = 64 << 20      # batched-hash tuples per GPU (805 MB: well past the 256 MB MALL)
@@ -405,9 +428,14 @@ def checker_leg(res, plan, cgck):
                                              CHECK_EVERY[key])
             par[key] = [chk, bad]
     if "imix" in res:
-        o = res["imix"]["out"]
+        o, ou, orr = res["imix"]["out"]
         bad, chk = P.check_synth_imix(len(o), plan["seed"], cgck.GEN_BOTH, o, CHECK_EVERY["imix"])
         par["imix"] = [chk, bad]
+        bad, chk = P.check_synth_imix(len(ou), plan["seed"], cgck.GEN_BOTH, ou, CHECK_EVERY["imix"])
+        par["imix_unhinted"] = [chk, bad]
+        bad, chk = P.check_synth_ring(len(orr), RING_SLOT, RING_L3, plan["seed"], cgck.GEN_BOTH, orr,
+                                      CHECK_EVERY["imix"])
+        par["imix_ring"] = [chk, bad]
     if "rss" in res:
         host, got = res["rss"]["hash_sample"]
         exp = P.toeplitz_batch(host, 4096, 12, 12, np.frombuffer(RSS_KEY, np.uint8), mask=0x7F)
@@ -600,8 +628,9 @@ def main():
         wall, ev_ms, o, k = bench_strided(torch, dist, eng, cgck, n, 64, plan, args.steps, args.warmup)
         res["64"] = {"wall": wall, "ev": ev_ms, "out": o, "kernel": k}
     if not args.no_extra and args.only in (None, "imix"):
-        wall, ev_ms, nbytes, o, k, unh = bench_imix(torch, dist, eng, cgck, n, plan, args.steps, args.warmup)
-        res["imix"] = {"wall": wall, "ev": ev_ms, "bytes": nbytes, "out": o, "kernel": k, "unhinted": unh}
+        wall, ev_ms, nbytes, o, k, unh, ring = bench_imix(torch, dist, eng, cgck, n, plan, args.steps, args.warmup)
+        res["imix"] = {"wall": wall, "ev": ev_ms, "bytes": nbytes, "out": o, "kernel": k, "unhinted": unh,
+                       "ring": ring}
     if not args.no_rss and args.only in (None, "rss"):
         res["rss"] = bench_rss(torch, dist, eng, cgck, plan, args.steps, args.warmup)
 
@@ -665,7 +694,7 @@ def main():
                                        "descriptors; BASELINE configs[3]), frames back to back: "
                                        "cgck_set_desc_layout(CGCK_LAYOUT_PACKED)",
                         "roofline_imix": roofline(n, 0, r["ev"], r["kernel"], "imix", r["bytes"] + 12 * n),
-                        "imix_without_layout_hint": r["unhinted"]})
+                        "imix_without_layout_hint": r["unhinted"], "imix_ring": r["ring"]})
         out["parity"] = parity
         if cpu:
             out["cpu_baseline"] = cpu

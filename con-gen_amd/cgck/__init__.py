@@ -67,7 +67,7 @@ EXPORTS = (
     "toeplitz_hash", "rss_hash4", "cgck_toeplitz", "cgck_dst_cache", "cgck_dst_cache_host",
     "cgck_burst_open", "cgck_burst_close", "cgck_thread_ctx", "cgck_set_error_handler",
     "cgck_rx_begin", "cgck_rx_end", "cgck_window_stats", "cgck_ctx_last_kernel", "cgck_set_desc_layout",
-    "cgck_ctx_set_kernel",
+    "cgck_ctx_set_kernel", "cgck_synth_imix_ring",
 )
 # Descriptor layout hint (cgck_set_desc_layout)
 LAYOUT_ANY = 0
@@ -124,6 +124,7 @@ def bind(path):
     L.cgck_host_unregister.argtypes = [_vp]
     L.cgck_synth_strided.argtypes = [_vp, _vp, _u64, _u64, _u32, _u64, _vp]
     L.cgck_synth_imix.argtypes = [_vp, _vp, _vp, _u64, _u64, _vp]
+    L.cgck_synth_imix_ring.argtypes = [_vp, _vp, _vp, _u64, _u64, _u32, _u64, _vp]
     L.cgck_imix_bytes.restype = _u64
     L.cgck_imix_bytes.argtypes = [_u64]
     L.cgck_dev_alloc.argtypes = [ctypes.c_size_t, ctypes.POINTER(_vp)]
@@ -407,6 +408,11 @@ class Engine:
 
     def synth_imix(self, base, desc, n, seed, stream=None):
         _check(load().cgck_synth_imix(self.ctx, base, desc, n, seed, stream), "cgck_synth_imix")
+
+    def synth_imix_ring(self, base, desc, n, stride, l3_off, seed, stream=None):
+        """IMIX frames in ring slots (cgck_synth_imix_ring): n * stride bytes at base."""
+        _check(load().cgck_synth_imix_ring(self.ctx, base, desc, n, stride, l3_off, seed, stream),
+               "cgck_synth_imix_ring")
 
     def toeplitz(self, data, n, stride, cnt, key, out, mask=0xFFFFFFFF, key_size=None, stream=None):
         """cgck_toeplitz: device data/out, host key.  Asynchronous."""

@@ -1068,6 +1068,22 @@ extern "C" int cgck_synth_imix(cgck_ctx_t *c, void *base, cgck_desc_t *desc, uin
 	return 0;
 }
 
+extern "C" int cgck_synth_imix_ring(cgck_ctx_t *c, void *base, cgck_desc_t *desc, uint64_t n, uint64_t stride,
+				    uint32_t l3_off, uint64_t seed, void *stream)
+{
+	if (!c || (n && (!base || !desc)))
+		return set_err(-EINVAL, "cgck_synth_imix_ring: bad arguments");
+	if (((uintptr_t)base & 15) || ((uintptr_t)desc & 3))
+		return set_err(-EINVAL, "cgck_synth_imix_ring: misaligned buffers");
+	if (l3_off > 0xffff || stride < (uint64_t)l3_off + 1500)
+		return set_err(-EINVAL, "cgck_synth_imix_ring: a slot must hold l3_off + 1500 bytes");
+	HIP_TRY(hipSetDevice(c->device));
+	hipStream_t st = pick(c, stream);
+	HIP_TRY(launch_synth_fill((uint8_t *)base, n * stride, seed, c->num_cus, st));
+	HIP_TRY(launch_synth_ring((uint8_t *)base, (uint32_t *)desc, n, stride, l3_off, c->num_cus, st));
+	return 0;
+}
+
 extern "C" int cgck_probe_read(cgck_ctx_t *c, const void *src, uint64_t bytes, uint32_t *sink, void *stream)
 {
 	if (!c || !src || !sink || ((uintptr_t)src & 15))

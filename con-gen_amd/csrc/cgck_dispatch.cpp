@@ -97,17 +97,19 @@ hipError_t launch_cksum(const KParams &p0, uint32_t len_hint, int num_cus, int k
 	const bool known = variant == 1 || variant == 2 || variant == 9 || variant == 10 || variant == 11 ||
 			   variant == 13 || variant == 15;
 #endif
-	// 256 B <= typical length < 1 KiB and the frames back to back (a descriptor
-	// batch under the packed hint, or a strided batch whose stride is at most
-	// its length): lpw streams the buffer (tools/sweep.py, profiles/r02/dma/lpw:
-	// dense strided 256 / 576 / 1000 B 69.6 / 73.1 / 74.7 % vs slot2's
-	// 52.1 / 56.6 / 48.4 %; 160 B 46.9 vs 59.8 %; 1500 B 75.6 vs group 79.9 %)
-	const bool packed = len_hint >= kLpwFromLen && lpw_ok(p) &&
-			    (p.desc ? (kernel & kPacked) != 0 : p.stride <= p.ip_len && p.stride > 0);
+	// 256 B <= typical length < 1 KiB: lpw streams 64-frame steps through LDS
+	// by DMA, the step's span itself when its frames lie back to back and the
+	// frames' chunk runs gathered otherwise, decided per step on the device
+	// (tools/family_ab.py, profiles/r03/: 16M IMIX packed without a hint 73.0 %
+	// vs slot2 62.8 %, in 2048 B ring slots at +14 62.0 vs 45.7 %; dense strided
+	// 256 / 576 / 1000 B 69.6 / 73.1 / 74.7 % vs slot2's 52.1 / 56.6 / 48.4 %,
+	// profiles/r02/dma/lpw; 160 B 46.9 vs 59.8 %, 1500 B 75.6 vs group 79.9 %).
+	// The layout hint (kPacked) no longer changes the choice.
+	const bool stream = len_hint >= kLpwFromLen && lpw_ok(p) && (p.desc || p.stride > 0);
 	if (variant == 0 || !known)
 		variant = !lane_ok ? 1 : lpa_ok ? (lpd_ok(p) ? 13 : 10)
 			: len_hint >= kGroupFromLen ? (!p.desc && dstr_ok(p) ? 11 : 1)
-			: len_hint <= kLppUpToLen ? 2 : packed ? 15 : 9;
+			: len_hint <= kLppUpToLen ? 2 : stream ? 15 : 9;
 	if (variant >= 2 && !lane_ok)
 		variant = 1;
 	if (variant == 10 && !lpa_ok)
@@ -121,7 +123,7 @@ hipError_t launch_cksum(const KParams &p0, uint32_t len_hint, int num_cus, int k
 	if (variant == 11 && !dstr_ok(p))
 		variant = 1;
 	if (variant == 15 && !lpw_ok(p))
-		variant = 1;
+		variant = lane_ok ? 9 : 1;
 	bool nt, contig;
 	if (kernel & kExplicit) {
 		nt = kernel & kNT;

@@ -165,5 +165,7 @@ hipError_t launch_synth_stamp(uint8_t *base, uint64_t n, uint64_t stride, uint32
 hipError_t launch_probe_read(const void *src, uint64_t bytes, uint32_t *sink, int num_cus, int variant,
 			     hipStream_t st);
 hipError_t launch_synth_imix(uint8_t *base, uint32_t *desc, uint64_t n, int num_cus, hipStream_t st);
+hipError_t launch_synth_ring(uint8_t *base, uint32_t *desc, uint64_t n, uint64_t stride, uint32_t l3_off, int num_cus,
+			     hipStream_t st);
 
 } // namespace cgck

@@ -1325,9 +1325,11 @@ struct LpwStep {
 	uint64_t a0;
 	int len, q, nch, e;
 	bool ok;
-	uint64_t cs, ce; // absolute chunk range of the lane's packet
+	uint64_t cs, ce; // the lane's packet in window coordinates: absolute chunks (chained) or list positions
+	uint64_t dl;     // gathered: (a0 >> 4) - cs, the chunk address of list position x is dl + x
 	uint64_t S, E;   // wave: span
-	uint32_t nwin;   // wave: windows (0: not chained, computed from global memory)
+	uint32_t nwin;   // wave: windows (0: computed from global memory)
+	bool gather;     // wave: the windows are the packets' chunk runs concatenated in lane order
 };
 
 template <bool DESC>
@@ -1364,32 +1366,92 @@ __device__ __forceinline__ LpwStep lpw_step(const KParams &p, uint64_t first, co
 	const bool brk = far || (ne && l > f && (rs < prev_s || rs > prev_e));
 	s.S = nonempty ? base : 0;
 	s.E = nonempty ? base + (uint64_t)__builtin_amdgcn_readlane(mE, 63) : 0;
+	s.dl = 0;
+	s.gather = false;
 	const uint64_t span = s.E - s.S;
-	s.nwin = __any(brk) || span > 16 * kLpwWin ? 0u : (uint32_t)((span + kLpwWin - 1) / kLpwWin);
-	if (!__any(brk) && span == 0)
-		s.nwin = 1; // a step of empty packets: one window, nothing moved
+	if (!__any(brk) && span <= 16 * kLpwWin) {
+		s.nwin = span ? (uint32_t)((span + kLpwWin - 1) / kLpwWin) : 1u; // (empty packets: one window, nothing moved)
+	} else {
+		// Not back to back (ring slots, gaps, reordered frames): the windows
+		// walk the list of the packets' chunk runs concatenated in lane order,
+		// packet p at list positions [P_p, P_p + nch_p) (an exclusive scan of
+		// the chunk counts), gathered by the same DMA (lpw_issue).  The
+		// per-window work is unchanged in list coordinates.
+		const uint32_t nc = ne ? (uint32_t)s.nch : 0u;
+		const uint32_t incl = wave_scan_dpp(nc);
+		const uint32_t T = (uint32_t)__builtin_amdgcn_readlane(incl, 63);
+		s.cs = incl - nc;
+		s.ce = incl;
+		s.dl = (pk.a0 >> 4) - s.cs;
+		s.S = 0;
+		s.E = T;
+		s.gather = true;
+		s.nwin = T > 16 * kLpwWin ? 0u : T ? (T + kLpwWin - 1) / kLpwWin : 1u;
+	}
 	s.nwin = __builtin_amdgcn_readfirstlane(s.nwin);
 	return s;
 }
 
 // One round: window t of step s (live) or zero lines, plus the descriptors
-// of step dstep (when dlive) into the descriptor slot.
+// of step dstep (when dlive) into the descriptor slot.  A gathered step
+// (gather) maps each list position of the window to its packet's chunk: the
+// packets starting in the window mark their position in an owner table built
+// in the target slot itself (free until this round's DMA lands; every row's
+// address is computed before the first DMA is issued), a max-scan per row of 64
+// positions fills the table forward, the row's carry is the last packet that
+// started before it (a ballot), and the chunk address is that packet's dl
+// (staged next to the table) plus the position.
 template <bool DESC>
-__device__ __forceinline__ void lpw_issue(const KParams &p, uint64_t wb, uint64_t E, bool live, uint32_t lds_slot,
+__device__ __forceinline__ void lpw_issue(const KParams &p, uint64_t wb, uint64_t E, bool live, bool gather,
+					  uint64_t cs, uint64_t ce, uint64_t dl, uint8_t *slot, uint32_t lds_slot,
 					  uint64_t dfirst, bool dlive, uint32_t lds_dslot, const uint8_t *zero)
 {
 	// window [wb, wb + 512) of a span ending at E (values, not a step
 	// reference: selecting between two steps' structs put them in scratch)
 	const int l = threadIdx.x & 63;
 	const uint32_t base = __builtin_amdgcn_readfirstlane(lds_slot); // wave-uniform: M0
+	if (gather && live) {
+		uint32_t *own = reinterpret_cast<uint32_t *>(slot);       // kLpwWin entries: owner lane + 1, 0 none
+		uint64_t *dls = reinterpret_cast<uint64_t *>(slot + 4 * kLpwWin); // 64 lanes' dl
+		// one element type for the table, and memory clobbers between the
+		// phases: the reads must not move above the zeroing or the marks (the
+		// slot holds the last window's packet bytes until it is cleared)
 #pragma unroll
-	for (int i = 0; i < kLpwDma; ++i) {
+		for (int r = 0; r < kLpwDma; ++r)
+			own[64 * r + l] = 0u;
+		asm volatile("" ::: "memory");
+		const bool ne = ce > cs;
+		if (ne && cs >= wb && cs < wb + kLpwWin)
+			own[cs - wb] = (uint32_t)l + 1;
+		dls[l] = dl;
+		asm volatile("" ::: "memory");
+		// every row's address first: row i's DMA lands on bytes [1024 i, 1024 i
+		// + 1024) of the slot, over the table the later rows read
+		const void *src[kLpwDma];
+#pragma unroll
+		for (int i = 0; i < kLpwDma; ++i) {
+			const uint64_t x = wb + 64 * i + l;
+			const uint64_t before = __ballot(ne && cs < wb + 64 * i); // packets started before this row
+			const int carry = before ? 64 - __builtin_clzll(before) : 0; // last such lane + 1
+			const uint32_t m = wave_max_scan_dpp(own[64 * i + l]);
+			const int o = (int)(m > (uint32_t)carry ? m : (uint32_t)carry) - 1;
+			const uint64_t d = dls[o > 0 ? o : 0];
+			src[i] = x < E ? reinterpret_cast<const void *>((d + x) << 4) : zero;
+		}
+		asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // the table is read: the slot may be refilled
+#pragma unroll
+		for (int i = 0; i < kLpwDma; ++i)
+			glds16_nt(src[i], base + 1024 * i);
+	} else {
+#pragma unroll
+		for (int i = 0; i < kLpwDma; ++i) {
 #if CGCK_LPW_SLOTMAJOR
-		const uint64_t c = wb + 8 * l + i; // lane l's 8 chunks land at +16 l of each KiB
+			const uint64_t c = wb + 8 * l + i; // lane l's 8 chunks land at +16 l of each KiB
 #else
-		const uint64_t c = wb + 64 * i + l;
+			const uint64_t c = wb + 64 * i + l;
 #endif
-		glds16_nt(live && c < E ? reinterpret_cast<const void *>(c << 4) : zero, base + 1024 * i);
+			glds16_nt(live && c < E ? reinterpret_cast<const void *>(c << 4) : zero, base + 1024 * i);
+		}
 	}
 	const uint64_t doff = 12 * dfirst + 16 * (uint64_t)l;
 	const bool dok = DESC && dlive && l < 48 && doff < 12 * p.n;
@@ -1492,7 +1554,8 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(W ? 4 : 1))
 			for (int u = 0; u < 8; ++u)
 				t8[u] = u32x4_t{0, 0, 0, 0};
 			if (!pre) {
-				lpw_issue<DESC>(p, cur.S, cur.E, true, lds0 + (kiss & 1) * kLpwSlot, first_of(j + 2), first_of(j + 2) < p.n,
+				lpw_issue<DESC>(p, cur.S, cur.E, true, cur.gather, cur.cs, cur.ce, cur.dl, smem + (kiss & 1) * kLpwSlot,
+						lds0 + (kiss & 1) * kLpwSlot, first_of(j + 2), first_of(j + 2) < p.n,
 						ldsd + (uint32_t)((j + 2) & 1) * 1024, zero);
 				++kiss;
 			}
@@ -1503,8 +1566,9 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(W ? 4 : 1))
 				const bool nx = !more && first_of(j + 1) < p.n && nxt.nwin > 0;
 				const uint64_t iwb = more ? cur.S + (uint64_t)(t + 1) * kLpwWin : nxt.S;
 				const uint64_t iE = more ? cur.E : nxt.E;
-				lpw_issue<DESC>(p, iwb, iE, more || nx, lds0 + (kiss & 1) * kLpwSlot,
-						first_of(j + 3), !more && first_of(j + 3) < p.n,
+				lpw_issue<DESC>(p, iwb, iE, more || nx, more ? cur.gather : nxt.gather, more ? cur.cs : nxt.cs,
+						more ? cur.ce : nxt.ce, more ? cur.dl : nxt.dl, smem + (kiss & 1) * kLpwSlot,
+						lds0 + (kiss & 1) * kLpwSlot, first_of(j + 3), !more && first_of(j + 3) < p.n,
 						ldsd + (uint32_t)((j + 3) & 1) * 1024, zero);
 				++kiss;
 				pre = nx;

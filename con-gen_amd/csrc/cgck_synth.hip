@@ -76,6 +76,32 @@ __global__ __launch_bounds__(256) void synth_imix_kernel(uint8_t *base, uint32_t
 	}
 }
 
+// The IMIX frames in ring slots: frame k (length of the 7:4:1 cycle) at
+// k * stride + l3_off, e.g. the netmap layout (2048-byte slots, IPv4 at +14).
+__global__ __launch_bounds__(256) void synth_ring_kernel(uint8_t *base, uint32_t *desc, uint64_t n, uint64_t stride,
+							 uint32_t l3_off)
+{
+	for (uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x; k < n;
+	     k += (uint64_t)gridDim.x * 256) {
+		const uint64_t off = k * stride;
+		const uint32_t len = c_imix_len[k % 12];
+		stamp(base + off + l3_off, len);
+		desc[3 * k + 0] = (uint32_t)off;
+		desc[3 * k + 1] = (uint32_t)(off >> 32);
+		desc[3 * k + 2] = (len << 16) | l3_off;
+	}
+}
+
+hipError_t launch_synth_ring(uint8_t *base, uint32_t *desc, uint64_t n, uint64_t stride, uint32_t l3_off, int num_cus,
+			     hipStream_t st)
+{
+	uint64_t want = (n + 255) / 256;
+	int blocks = (int)(want < (uint64_t)num_cus * 8 ? want : (uint64_t)num_cus * 8);
+	if (blocks < 1)
+		blocks = 1;
+	hipLaunchKernelGGL(synth_ring_kernel, dim3(blocks), dim3(256), 0, st, base, desc, n, stride, l3_off);
+	return hipGetLastError();
+}
 
 hipError_t launch_synth_fill(uint8_t *base, uint64_t nbytes, uint64_t seed, int num_cus, hipStream_t st)
 {

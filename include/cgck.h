@@ -246,6 +246,10 @@ int cgck_synth_strided(cgck_ctx_t *ctx, void *base, uint64_t n, uint64_t stride,
 int cgck_synth_imix(cgck_ctx_t *ctx, void *base, cgck_desc_t *desc, uint64_t n,
 		    uint64_t seed, void *stream);
 uint64_t cgck_imix_bytes(uint64_t n); /* bytes an n-packet IMIX batch occupies */
+/* The same IMIX frames in ring slots: frame k at k * stride + l3_off (the
+ * netmap layout: 2048-byte slots, IPv4 at +14), n * stride bytes of buffer. */
+int cgck_synth_imix_ring(cgck_ctx_t *ctx, void *base, cgck_desc_t *desc, uint64_t n, uint64_t stride,
+			 uint32_t l3_off, uint64_t seed, void *stream);
 
 /* ------------------------------------------------------------------------ */
 /* 3. Toeplitz RSS hash (subr.c:482-530, subr.h:370-371) */

@@ -85,6 +85,10 @@ class Port:
         L.oracle_check_synth_imix.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
                                               ctypes.c_void_p, ctypes.c_uint64,
                                               ctypes.POINTER(ctypes.c_uint64)]
+        L.oracle_check_synth_ring.restype = ctypes.c_uint64
+        L.oracle_check_synth_ring.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64,
+                                              ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint64,
+                                              ctypes.POINTER(ctypes.c_uint64)]
         L.oracle_fn_in_cksum.restype = ctypes.c_void_p
         L.oracle_fn_udp_cksum.restype = ctypes.c_void_p
         # Toeplitz RSS (oracle/rss_oracle.c)
@@ -177,6 +181,13 @@ class Port:
     def check_synth_imix(self, n, seed, flags, out, every=1):
         chk = ctypes.c_uint64()
         bad = self.lib.oracle_check_synth_imix(n, seed, flags, out.ctypes.data, every,
+                                               ctypes.byref(chk))
+        return bad, chk.value
+
+    def check_synth_ring(self, n, stride, l3_off, seed, flags, out, every=1):
+        """IMIX frames in ring slots (cgck_synth_imix_ring) vs the referee."""
+        chk = ctypes.c_uint64()
+        bad = self.lib.oracle_check_synth_ring(n, stride, l3_off, seed, flags, out.ctypes.data, every,
                                                ctypes.byref(chk))
         return bad, chk.value
 

@@ -93,18 +93,24 @@ def test_reversed_overlapping_and_mixed_steps(lpw, port):
     run(lpw, port, buf, mixed, cgck.GEN_BOTH)
 
 
-def test_dispatcher_picks_lpw_under_the_hint(engine, port):
-    """The default dispatch: typical length below 1 KiB + CGCK_LAYOUT_PACKED
-    -> lpw; without the hint -> slot2; both exact."""
+def test_dispatcher_picks_lpw_for_mid_lengths(engine, port):
+    """The default dispatch: typical length 256 B .. 1 KiB -> lpw with or
+    without CGCK_LAYOUT_PACKED (the kernel tells packed steps from scattered
+    ones itself), on a packed batch and on the same frames scattered; below
+    256 B -> slot2; all exact."""
     rng = np.random.default_rng(91)
     buf, desc = packed_batch(rng, 5000, MIXES["imix"])
+    sbuf, sdesc = random_batch(rng, 5000, 700)
     engine.set_desc_len_hint(354)
     try:
-        engine.set_desc_layout(cgck.LAYOUT_PACKED)
-        _, k = run(engine, port, buf, desc, cgck.GEN_BOTH)
-        assert k.startswith("lpw_kernel<"), k
-        engine.set_desc_layout(cgck.LAYOUT_ANY)
-        _, k = run(engine, port, buf, desc, cgck.GEN_BOTH)
+        for layout in (cgck.LAYOUT_PACKED, cgck.LAYOUT_ANY):
+            engine.set_desc_layout(layout)
+            _, k = run(engine, port, buf, desc, cgck.GEN_BOTH)
+            assert k.startswith("lpw_kernel<"), (layout, k)
+            _, k = run(engine, port, sbuf, sdesc, cgck.VERIFY_BSD)
+            assert k.startswith("lpw_kernel<"), (layout, k)
+        engine.set_desc_len_hint(200)
+        _, k = run(engine, port, sbuf, sdesc, cgck.GEN_BOTH)
         assert k.startswith("slot2_kernel<"), k
     finally:
         engine.set_desc_layout(cgck.LAYOUT_ANY)
@@ -146,13 +152,14 @@ def test_full_size_imix(lpw, port):
 
 
 @pytest.mark.parametrize("stride,ln,want", [(576, 576, "lpw_kernel<"), (300, 300, "lpw_kernel<"),
-                                            (1024, 576, "slot2_kernel<"), (160, 160, "slot2_kernel<"),
-                                            (1500, 1500, "cksum_kernel<")])
+                                            (1024, 576, "lpw_kernel<"), (2048, 300, "lpw_kernel<"),
+                                            (160, 160, "slot2_kernel<"), (1500, 1500, "cksum_kernel<")])
 def test_dispatcher_strided(engine, port, stride, ln, want):
-    """Strided batches need no hint: frames back to back (stride <= length)
-    from 256 B to 1 KiB stream (lpw); gapped or smaller ones gather (slot2),
-    1 KiB and up stream through LDS four frames a step (dstr), or take the
-    group kernel when they verify; all exact."""
+    """Strided batches from 256 B to 1 KiB stream through lpw, back to back
+    (stride <= length: the span) or gapped (ring slots: the frames' chunk runs
+    gathered); smaller ones gather in registers (slot2), 1 KiB and up stream
+    through LDS four frames a step (dstr), or take the group kernel when they
+    verify; all exact."""
     n = 3001
     rng = np.random.default_rng(stride + ln)
     buf = rng.integers(0, 256, n * stride + ln + 64, dtype=np.uint8)

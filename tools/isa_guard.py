@@ -26,7 +26,7 @@ from collections import defaultdict
 VMEM = re.compile(r"^(global_|buffer_|flat_|scratch_)")
 CAP = 99      # "many": counts above WIDEN jump here, so loops with VMEM reach a fixed point
 WIDEN = (None, 24, 4, 12)  # per counter (dma, loads, stores): above it the count becomes CAP
-FACT_AGE = 2
+FACT_AGE = 4
 MAX_VISITS = 2_000_000
 TRACK = (0,)  # counters followed along paths: the DMA (the other VMEM: inventory())
 
