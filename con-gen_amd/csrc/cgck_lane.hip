@@ -389,8 +389,24 @@ __global__ __launch_bounds__(64) void lpd_kernel(KParams p)
 		issue(d);
 	const int o = lane * (int)p.stride; // packet L's byte offset in a slot
 	constexpr bool stage = C > 1; // lpd_ok guarantees an output array
+	// SP >= 3 (lab A/B): a full chunk's outputs are read from the staging into
+	// registers at the chunk's end and stored right AFTER the next step's DMA
+	// issue (as lpw does), so the two following waits leave them in flight
+	// (two steps to complete instead of one); store policy SP - 3.
+	constexpr bool DEFER = SP >= 3 && C > 1;
+	constexpr int policy = SP % 3 == 0 ? kNt : SP % 3 == 1 ? kDefaultPolicy : kSc1;
+	u32x4_t held[DEFER ? C / 4 : 1];
+	bool pend = false;
+	uint64_t pfirst = 0;
 	for (uint64_t j = 0; j < nsteps; ++j) {
 		issue(j + D - 1);
+		if (DEFER && pend) {
+			const __amdgpu_buffer_rsrc_t rs = out_rsrc(p.out + pfirst, C * 256);
+#pragma unroll
+			for (int i = 0; i < (DEFER ? C / 4 : 0); ++i)
+				bstore16<policy>(rs, 16 * (i * 64 + lane), held[i]);
+			pend = false;
+		}
 		// Wait for step j's DMA.  Issued after it: the DMA of the D - 1 later
 		// steps, plus the output stores of the steps since (C == 1: one per
 		// step once the ring is full; C > 1: C / 4 of the last chunk flush,
@@ -401,7 +417,7 @@ __global__ __launch_bounds__(64) void lpd_kernel(KParams p)
 			else
 				asm volatile("s_waitcnt vmcnt(%0)" ::"i"(5 * (D - 1)) : "memory");
 		} else {
-			if (stage && j >= (uint64_t)C && (j % C) <= (uint64_t)(D - 2))
+			if (stage && j >= (uint64_t)C && (j % C) <= (uint64_t)(DEFER ? D - 1 : D - 2))
 				asm volatile("s_waitcnt vmcnt(%0)" ::"i"(4 * (D - 1) + C / 4) : "memory");
 			else
 				asm volatile("s_waitcnt vmcnt(%0)" ::"i"(4 * (D - 1)) : "memory");
@@ -422,10 +438,17 @@ __global__ __launch_bounds__(64) void lpd_kernel(KParams p)
 			// flush the chunk: C / 4 coalesced 16-byte stores per lane
 			const uint64_t first = (b + (j / C) * G) * C * 64;
 			asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-			if (first + C * 64 <= p.n) {
+			if (DEFER && first + C * 64 <= p.n && j + 1 < nsteps) {
+				const u32x4_t *s4 = reinterpret_cast<const u32x4_t *>(so);
+#pragma unroll
+				for (int i = 0; i < (DEFER ? C / 4 : 0); ++i)
+					held[i] = s4[i * 64 + lane];
+				asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // read before the next reduce restages
+				pend = true;
+				pfirst = first;
+			} else if (first + C * 64 <= p.n) {
 				const uint4 *s4 = reinterpret_cast<const uint4 *>(so);
 				const __amdgpu_buffer_rsrc_t rs = out_rsrc(p.out + first, C * 256);
-				constexpr int policy = SP == 0 ? kNt : SP == 1 ? kDefaultPolicy : kSc1;
 #pragma unroll
 				for (int i = 0; i < C / 4; ++i) {
 					const uint4 w = s4[i * 64 + lane];
@@ -684,7 +707,7 @@ hipError_t launch_lpd(const KParams &p, int num_cus, hipStream_t st)
 	static const int sp = [] { // $CGCK_LPD_SP: flush store policy 0 nt, 1 default, 2 sc1
 		const char *e = CGCK_ENV("CGCK_LPD_SP");
 		const int v = e ? atoi(e) : 2;
-		return v >= 0 && v <= 2 ? v : 2;
+		return v >= 0 && v <= 5 ? v : 2; // 3..5: the same, stored after the next step's issue
 	}();
 #define CGCK_LPD_S(DD, CC, SS)                                                                   \
 	do {                                                                                     \
@@ -715,6 +738,10 @@ hipError_t launch_lpd(const KParams &p, int num_cus, hipStream_t st)
 		else                                                                             \
 			CGCK_LPD(DD, 32);                                                        \
 	} while (0)
+	if (sp == 5 && depth == 2 && chunk == 32) { // the deferred flush, sc1 (lab A/B)
+		CGCK_LPD_S(2, 32, 5);
+		return hipGetLastError();
+	}
 	switch (depth) {
 	case 3: CGCK_LPD_D(3); break;
 	case 4: CGCK_LPD_D(4); break;

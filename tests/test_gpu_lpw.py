@@ -4,7 +4,8 @@ Bit-exact against the oracle referee (oracle/cksum_oracle.c) on packed
 batches of every length class and alignment, on batches that are NOT packed
 (gapped, reversed, overlapping: its frame-by-frame steps must stay exact
 whatever the hint says), through the dispatcher's own choice, and on the
-full-size IMIX batch (BASELINE configs[3]) against the default slot2 path."""
+full-size IMIX batch (BASELINE configs[3]) packed and in 2048 B ring slots,
+against the slot2 kernel's results."""
 import numpy as np
 import pytest
 
@@ -123,7 +124,7 @@ def test_dispatcher_picks_lpw_for_mid_lengths(engine, port):
 def test_full_size_imix(lpw, port):
     """BASELINE configs[3] (16M IMIX packets, packed by cgck_synth_imix)
     through lpw: every 64th packet against the referee, and the whole batch
-    against the default (slot2) path."""
+    against the slot2 kernel's results."""
     n = 16 << 20
     nbytes = cgck.load().cgck_imix_bytes(n)
     buf = cgck.DeviceBuffer(nbytes)
@@ -131,7 +132,7 @@ def test_full_size_imix(lpw, port):
     out = cgck.DeviceBuffer(4 * n)
     ref = cgck.DeviceBuffer(4 * n)
     lpw.synth_imix(buf.ptr, desc.ptr, n, 0xC0C1)
-    e = cgck.Engine(0)
+    e = cgck.Engine(0, kernel="slot2")   # the register-gather path as the second opinion
     e.set_desc_len_hint(nbytes // n)
     e.desc(buf.ptr, desc.ptr, n, cgck.GEN_BOTH, ref.ptr)
     assert e.last_kernel.startswith("slot2_kernel<")
@@ -175,3 +176,40 @@ def test_dispatcher_strided(engine, port, stride, ln, want):
             assert k.startswith("dstr_kernel<"), k
         else:
             assert k.startswith(want), k
+
+
+@pytest.mark.slow
+def test_full_size_imix_ring(port):
+    """The 16M IMIX frames in 2048 B ring slots at +14 (the netmap layout)
+    through the default dispatch (lpw, gathered steps): every 64th frame
+    against the referee, the whole batch against slot2."""
+    n = 16 << 20
+    nbytes = cgck.load().cgck_imix_bytes(n)
+    buf = cgck.DeviceBuffer(2048 * n)
+    desc = cgck.DeviceBuffer(12 * n)
+    out = cgck.DeviceBuffer(4 * n)
+    ref = cgck.DeviceBuffer(4 * n)
+    e = cgck.Engine(0)
+    s2 = cgck.Engine(0, kernel="slot2")
+    try:
+        e.synth_imix_ring(buf.ptr, desc.ptr, n, 2048, 14, 0xC0C2)
+        for x in (e, s2):
+            x.set_desc_len_hint(nbytes // n)
+        e.desc(buf.ptr, desc.ptr, n, cgck.GEN_BOTH, out.ptr)
+        assert e.last_kernel.startswith("lpw_kernel<"), e.last_kernel
+        e.sync()
+        s2.desc(buf.ptr, desc.ptr, n, cgck.GEN_BOTH, ref.ptr)
+        assert s2.last_kernel.startswith("slot2_kernel<")
+        o = np.zeros(n, np.uint32)
+        r = np.zeros(n, np.uint32)
+        out.download(o, stream=s2.stream)
+        ref.download(r, stream=s2.stream)
+        s2.sync()
+    finally:
+        for b in (buf, desc, out, ref):
+            b.free()
+        e.close()
+        s2.close()
+    bad, chk = port.check_synth_ring(n, 2048, 14, 0xC0C2, cgck.GEN_BOTH, o, 64)
+    assert bad == 0 and chk == n // 64
+    assert np.array_equal(o, r)

@@ -62,6 +62,16 @@ def main():
             work[w] = (lambda L, c, buf=buf, desc=desc, pre=pre: pre(L, c) or L.cgck_desc(
                 c, buf.ptr, desc.ptr, n, cgck.GEN_BOTH, out.ptr, None, None, None), nbytes + 16 * n)
             keep += [buf, desc]
+        elif w == "ring":
+            # the IMIX frames in 2048 B ring slots at +14 (cgck_synth_imix_ring)
+            nbytes = cgck.load().cgck_imix_bytes(n)
+            buf, desc = cgck.DeviceBuffer(2048 * n), cgck.DeviceBuffer(12 * n)
+            e0.synth_imix_ring(buf.ptr, desc.ptr, n, 2048, 14, 0xC0C0)
+            for L, c in zip(libs, ctxs):
+                L.cgck_set_desc_len_hint(c, nbytes // n)
+            work[w] = (lambda L, c, buf=buf, desc=desc: L.cgck_desc(
+                c, buf.ptr, desc.ptr, n, cgck.GEN_BOTH, out.ptr, None, None, None), nbytes + 16 * n)
+            keep += [buf, desc]
         elif w == "rss":
             nt = 64 << 20
             buf = cgck.DeviceBuffer(12 * nt)
