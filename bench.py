@@ -25,7 +25,10 @@ oracle referee (every 64 B packet, every 64th 1500 B / IMIX packet across
 the whole shard; the totals are summed over ranks), and at N = 1 rank 0
 times the reference's own subr.c checksum unit (oracle/_ref, when built) or
 the oracle restatement on a bounded sample of the same workload as the CPU
-baseline.  Host-resident burst rates of SURVEY §8(f) ranks 1-2 (tools/txburst,
+baseline, and runs two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE) per
+device workload as child processes after the timed region, so roofline.traffic
+is this box's HBM bytes per launch (--no-pmc: the committed summary).
+Host-resident burst rates of SURVEY §8(f) ranks 1-2 (tools/txburst,
 N = 1) are summarised under extra.burst; the full rows go to
 gpurun_out/bench_burst.json.
 """
@@ -74,6 +77,8 @@ def parse(argv=None):
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-rss", action="store_true", help="skip the Toeplitz RSS lines")
     ap.add_argument("--no-burst", action="store_true", help="skip the host-resident burst lines")
+    ap.add_argument("--no-pmc", action="store_true",
+                    help="skip the rocprofv3 --pmc traffic passes (roofline.traffic from profiles/ instead)")
     ap.add_argument("--only", choices=["1500", "64", "imix", "rss"], default=None,
                     help="time one workload only (profiling runs)")
     ap.add_argument("--allow-shared-devices", action="store_true",
@@ -576,6 +581,49 @@ def cpu_baseline_64(seconds):
 
 TRAFFIC_SOURCE = ("profiles/pmc_latest.json: FETCH_SIZE x 2 + WRITE_SIZE per launch from separate "
                   "rocprofv3 --pmc passes of this bench (tools/gpu_prof.sh), not measured in this run")
+TRAFFIC_LIVE = ("this run: rocprofv3 --pmc FETCH_SIZE, then WRITE_SIZE, each a pass of its own over "
+                "tools/one_workload.py (the same batch and kernel, 3 launches, a child process on this box "
+                "after the timed region); bytes = (2 x FETCH_SIZE + WRITE_SIZE) KB x 1024, the median per "
+                "dispatch (MI355X_MICROARCH.md: FETCH_SIZE counts half a wide streaming read on gfx950)")
+
+
+def pmc_traffic_live(kernels):
+    """HBM bytes per launch of each workload's kernel, measured on this box
+    now: two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE: together they
+    exceed the four TCC counters of one pass) over one_workload.py per
+    workload.  {workload: bytes} for the workloads whose passes succeeded."""
+    import csv
+    import glob
+    import shutil
+    import statistics
+    import subprocess
+    import tempfile
+    if not shutil.which("rocprofv3"):
+        return {}
+    env = dict(os.environ, TMPDIR="/tmp")
+    res = {}
+    for w, kernel in kernels.items():
+        got = {}
+        for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+            d = tempfile.mkdtemp(prefix="cgck_pmc_", dir="/tmp")
+            cmd = ["rocprofv3", "--pmc", ctr, "-d", d, "-o", "run", "--output-format", "csv", "--",
+                   sys.executable, os.path.join(ROOT, "tools", "one_workload.py"), w, "--launches", "3"]
+            try:
+                subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, timeout=120)
+                vals = []
+                for f in glob.glob(os.path.join(d, "**", "run_counter_collection.csv"), recursive=True):
+                    for r in csv.DictReader(open(f)):
+                        if r.get("Counter_Name") == ctr and kernel in r.get("Kernel_Name", ""):
+                            vals.append(float(r["Counter_Value"]))
+                if vals:
+                    got[ctr] = statistics.median(vals) * 1024
+            except (OSError, subprocess.SubprocessError, ValueError, KeyError):
+                pass
+            finally:
+                shutil.rmtree(d, ignore_errors=True)
+        if len(got) == 2:
+            res[w] = 2 * got["FETCH_SIZE"] + got["WRITE_SIZE"]
+    return res
 
 
 def load_traffic(key="1500", kernel=None):
@@ -594,14 +642,21 @@ def load_traffic(key="1500", kernel=None):
     return d.get(f"bytes_per_launch_{key}")
 
 
-def roofline(n, size, ev_ms, kernel, traffic_key, extra_bytes=0):
+def roofline(n, size, ev_ms, kernel, traffic_key, extra_bytes=0, live=None):
     """HBM roofline of one workload's kernel: algorithmic bytes per launch
-    (n x (L + 4) [+ descriptors]) over its HIP-event time per launch."""
+    (n x (L + 4) [+ descriptors]) over its HIP-event time per launch.
+    traffic: the PMC bytes per launch measured in this run (live), else the
+    committed summary of the same kernel."""
     algo = n * (size + 4) + extra_bytes
     ach = algo / (ev_ms * 1e-3)
+    if live and traffic_key in live:
+        traffic, src = live[traffic_key], TRAFFIC_LIVE
+    else:
+        traffic, src = load_traffic(traffic_key, kernel), TRAFFIC_SOURCE
     return {"bound": "hbm", "achieved": ach / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-            "frac": ach / HBM_PEAK, "traffic": load_traffic(traffic_key, kernel), "kernel": kernel,
-            "algorithmic_bytes_per_launch": algo, "kernel_ms_hip_events": ev_ms}
+            "frac": ach / HBM_PEAK, "traffic": traffic, "kernel": kernel,
+            "algorithmic_bytes_per_launch": algo, "kernel_ms_hip_events": ev_ms,
+            "traffic_over_algorithmic": traffic / algo if traffic else None, "traffic_source": src}
 
 
 def main():
@@ -654,6 +709,9 @@ def main():
             cpu_64 = cpu_baseline_64(min(3.0, args.cpu_seconds))
         if "rss" in res:
             cpu_r = cpu_rss(min(3.0, args.cpu_seconds))
+    live = {}
+    if dist.rank == 0 and dist.world == 1 and not args.no_pmc:
+        live = pmc_traffic_live({k: res[k]["kernel"] for k in ("1500", "64", "imix") if k in res})
     dist.barrier()
 
     if dist.rank == 0:
@@ -675,15 +733,14 @@ def main():
                                        "configs[4] at 8 GPUs)",
                            "packets_per_gpu": n, "packet_bytes": 1500, "parallelism": f"batch-split x{W}",
                            "gb_s": gpkt * 1500, "devices": [d["device"] for d in devices]},
-                "roofline": roofline(n, 1500, r["ev"], r["kernel"], "1500"),
+                "roofline": roofline(n, 1500, r["ev"], r["kernel"], "1500", live=live),
             })
-            out["roofline"]["traffic_source"] = TRAFFIC_SOURCE
         if "64" in res:
             r = res["64"]
             gpkt = n * W * K / r["wall"] / 1e9
             out.update({"value_64B": gpkt, "gb_s_64B": gpkt * 64, "ms_per_step_64B": r["wall"] / K * 1e3,
                         "config_64B": f"{n} x 64 B IPv4+TCP per GPU, dense stride 64 (BASELINE configs[1])",
-                        "roofline_64B": roofline(n, 64, r["ev"], r["kernel"], "64")})
+                        "roofline_64B": roofline(n, 64, r["ev"], r["kernel"], "64", live=live)})
         if "imix" in res:
             r = res["imix"]
             gpkt = n * W * K / r["wall"] / 1e9
@@ -693,7 +750,8 @@ def main():
                         "config_imix": f"{n} IMIX packets per GPU (64/576/1500 at 7:4:1, 12-byte "
                                        "descriptors; BASELINE configs[3]), frames back to back: "
                                        "cgck_set_desc_layout(CGCK_LAYOUT_PACKED)",
-                        "roofline_imix": roofline(n, 0, r["ev"], r["kernel"], "imix", r["bytes"] + 12 * n),
+                        "roofline_imix": roofline(n, 0, r["ev"], r["kernel"], "imix", r["bytes"] + 12 * n,
+                                                  live=live),
                         "imix_without_layout_hint": r["unhinted"], "imix_ring": r["ring"]})
         out["parity"] = parity
         if cpu:
