@@ -1773,6 +1773,221 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(W ? 4 : 1))
 	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+#if CGCK_LAB
+// lpx: lpw with TWO rounds in flight.  lpw waits for round r - 1 right after
+// issuing round r, so one 8 KiB window per wave is in flight while a window is
+// reduced (its DMA rounds alone: 76.8 % of 8 TB/s).  Here a round's slot is
+// refilled as soon as the window's bytes are in registers (dstr's trick): the
+// wave waits for round r, reads the window (chunk sums, edge chunks, header
+// chunks), issues round r + 2 into the same slot, and only then scans; the
+// prefix goes to a separate 2 KiB area.  Every step has at least one round (a
+// zero round for a step computed from global memory or past the batch), so
+// the issue cursor runs exactly two rounds ahead through cur / nxt / nn; round
+// (k, 0) carries the descriptors of step k + 2, which processing (k, 0) turns
+// into nn before the round after it can need them.  22.3 KiB of LDS: 7 waves
+// per CU, 112 KiB in flight per CU against lpw's 64.
+template <bool DESC, int C>
+__global__ __launch_bounds__(64) void lpx_kernel(KParams p)
+{
+	extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+	// 2 x 1 KiB descriptor slots and a third the rounds without descriptors
+	// write their zero line into (round (k, 0)'s descriptors of step k + 2 wait
+	// in their slot while later rounds of step k are issued)
+	uint8_t *dring = smem + 2 * kLpwSlot;
+	uint32_t *pfx = reinterpret_cast<uint32_t *>(dring + 3 * 1024); // kLpwWin prefix sums
+	uint32_t *so = pfx + kLpwWin;
+	uint8_t *sv = reinterpret_cast<uint8_t *>(so + C * 64);
+	const int l = threadIdx.x & 63;
+	const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)smem);
+	const uint32_t ldsd = lds0 + 2 * kLpwSlot;
+	const uint8_t *zero = (const uint8_t *)p.zero + (blockIdx.x & 63) * 64;
+	const uint64_t NS = (p.n + 63) / 64, NC = (NS + C - 1) / C, G = gridDim.x, b = blockIdx.x;
+	if (b >= NC)
+		return;
+	const uint64_t nsteps = (NC - b + G - 1) / G * C;
+	auto gstep = [&](uint64_t j) { return (b + (j / C) * G) * C + j % C; };
+	auto first_of = [&](uint64_t j) { return j < nsteps ? gstep(j) * 64 : p.n; };
+
+	LpwStep cur = lpw_step<DESC>(p, first_of(0), load_desc<DESC>(p, first_of(0) + l, p.n));
+	LpwStep nxt = lpw_step<DESC>(p, first_of(1), load_desc<DESC>(p, first_of(1) + l, p.n));
+	LpwStep nn = nxt; // step j + 2: from the descriptors round (j, 0) carries, at processing (j, 0)
+	uint32_t kiss = 0; // rounds issued (round k uses data slot k & 1)
+	int ia = 0;        // issue cursor: step j + ia ...
+	uint32_t iw = 0;   // ... window iw
+	auto rounds = [](uint32_t nwin) { return nwin ? nwin : 1u; };
+	// issue the round at the cursor (one call site per step struct: a selected
+	// struct or field would put the structs in scratch), then advance it
+#define CGCK_LPX_ISSUE(ST, K)                                                                            \
+	do {                                                                                             \
+		const uint64_t k_ = (K);                                                                \
+		lpw_issue<DESC>(p, ST.S + (uint64_t)iw * kLpwWin, ST.E, ST.nwin > 0 && first_of(k_) < p.n, ST.gather, \
+				ST.cs, ST.ce, ST.dl, smem + (kiss & 1) * kLpwSlot, lds0 + (kiss & 1) * kLpwSlot,      \
+				first_of(k_ + 2), iw == 0 && first_of(k_ + 2) < p.n,                           \
+				ldsd + (iw == 0 ? (uint32_t)((k_ + 2) & 1) : 2u) * 1024, zero);               \
+		++kiss;                                                                                 \
+		if (iw + 1 < rounds(ST.nwin)) {                                                          \
+			++iw;                                                                           \
+		} else {                                                                                \
+			++ia;                                                                           \
+			iw = 0;                                                                         \
+		}                                                                                       \
+	} while (0)
+	auto issue_next = [&](uint64_t j) __attribute__((always_inline)) {
+		if (ia == 0)
+			CGCK_LPX_ISSUE(cur, j);
+		else if (ia == 1)
+			CGCK_LPX_ISSUE(nxt, j + 1);
+		else
+			CGCK_LPX_ISSUE(nn, j + 2);
+	};
+	issue_next(0);
+	issue_next(0);
+	static_assert(C % 4 == 0, "C / 4 16-byte stores per lane per chunk");
+	const bool defer_ok = p.out && !p.verdict && (reinterpret_cast<uintptr_t>(p.out) & 15) == 0;
+	bool pend = false; // a chunk's outputs wait in the staging for the next round
+	int sage = 0;      // waits left that may leave the chunk store in flight
+	uint64_t pf0 = 0;
+	for (uint64_t j = 0; j < nsteps; ++j) {
+		const uint64_t first = first_of(j);
+		const bool live = first < p.n && cur.nwin > 0;
+		uint32_t acc = 0, corr = 0;
+		Hdr h{};
+		u32x4_t t8[8];
+#pragma unroll
+		for (int u = 0; u < 8; ++u)
+			t8[u] = u32x4_t{0, 0, 0, 0};
+		const uint32_t R = rounds(cur.nwin);
+		for (uint32_t t = 0; t < R; ++t) {
+			// round (j, t); issued after it: the next round, and a chunk store
+			// (after this round: two waits leave it in flight)
+			if (sage > 0) {
+				--sage;
+				asm volatile("s_waitcnt vmcnt(%0)" ::"i"(kLpwDma + 1 + C / 4) : "memory");
+			} else {
+				asm volatile("s_waitcnt vmcnt(%0)" ::"i"(kLpwDma + 1) : "memory");
+			}
+			if (t == 0)
+				nn = lpw_step<DESC>(p, first_of(j + 2), lpw_desc_lds<DESC>(dring + ((j + 2) & 1) * 1024));
+			const uint4 *win = reinterpret_cast<const uint4 *>(smem + (kiss & 1) * kLpwSlot); // round kiss - 2
+			const uint64_t wb = cur.S + (uint64_t)t * kLpwWin;
+			const uint64_t we = wb + kLpwWin;
+			uint32_t cs8[kLpwDma];
+			if (live) {
+				const bool head = cur.ok && cur.nch > 0 && cur.cs >= wb && cur.cs < we;
+				const bool tail = cur.ok && cur.nch > 0 && cur.ce - 1 >= wb && cur.ce - 1 < we;
+				const bool dw = !__any(cur.ok && ((cur.q | cur.len) & 3) != 0);
+				if (__any(head && cur.q != 0))
+					corr += head && cur.q != 0 ? lead_sum(win[(int)(cur.cs - wb)], cur.q, dw) : 0u;
+				if (__any(tail && cur.e != 16))
+					corr += tail && cur.e != 16 ? trail_sum(win[(int)(cur.ce - 1 - wb)], cur.e, dw) : 0u;
+				const bool hwin = cur.ok && cur.cs + 8 > wb && cur.cs < we;
+				if (!(p.flags & CGCK_RAW) && __any(hwin)) {
+					const u32x4_t *win4 = reinterpret_cast<const u32x4_t *>(win);
+#pragma unroll
+					for (int u = 0; u < 8; ++u) {
+						const uint64_t c = cur.cs + u;
+						const bool in = hwin && c >= wb && c < we;
+						const u32x4_t c8 = win4[in ? (int)(c - wb) : 0];
+						t8[u] = in ? c8 : t8[u];
+					}
+				}
+#pragma unroll
+				for (int r = 0; r < kLpwDma; ++r) {
+					const uint4 v = win[64 * r + l];
+					cs8[r] = wb + 64 * r + l < cur.E ? sum4(v, 0u) : 0u;
+				}
+			}
+			asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // the window is in registers: refill its slot
+			issue_next(j);
+			if (pend) {
+				const __amdgpu_buffer_rsrc_t rs = out_rsrc(p.out + pf0, C * 256);
+#pragma unroll
+				for (int i = 0; i < C / 4; ++i)
+					bstore16<kSc1>(rs, 16 * (64 * i + l), reinterpret_cast<const u32x4_t *>(so)[64 * i + l]);
+				pend = false;
+				sage = 2;
+			}
+			if (live) {
+				uint32_t carry = 0;
+#pragma unroll
+				for (int r = 0; r < kLpwDma; ++r) {
+					const uint32_t xs = wave_scan_dpp(cs8[r]);
+					pfx[64 * r + l] = xs + carry;
+					carry += __builtin_amdgcn_readlane(xs, 63);
+				}
+				const uint64_t lo = cur.cs > wb ? cur.cs : wb;
+				const uint64_t hi = cur.ce < we ? cur.ce : we;
+				if (cur.ok && hi > lo)
+					acc += pfx[(int)(hi - 1 - wb)] - (lo > wb ? pfx[(int)(lo - 1 - wb)] : 0u);
+				asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // the prefix area is rewritten next round
+			}
+		}
+		if (live) {
+			if (!(p.flags & CGCK_RAW)) {
+				uint4 w8[8];
+#pragma unroll
+				for (int u = 0; u < 8; ++u)
+					w8[u] = make_uint4(t8[u].x, t8[u].y, t8[u].z, t8[u].w);
+				h = header<8, false>(w8, reinterpret_cast<const uint4 *>(cur.a0 & ~(uint64_t)15), cur.nch, cur.q,
+						     cur.len, p.flags, cur.ok);
+			}
+		} else if (first < p.n) {
+			// no window covers the step (more than 16 windows): the lane's packet
+			// straight from global memory, after a drain (the two rounds in
+			// flight complete first; the counts after it only over-wait)
+			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+			sage = 0;
+			const uint4 *c0 = reinterpret_cast<const uint4 *>(cur.a0 & ~(uint64_t)15);
+			const int cnt = cur.ok ? cur.nch : 0;
+			for (int i = 0; __any(i < cnt); ++i) {
+				const uint4 v = ldc<false>(c0, i, cnt, p.zero);
+				acc = i < cnt ? sum4(v, acc) : acc;
+				if (i == 0 && cnt > 0 && cur.q != 0)
+					corr += lead_sum(v, cur.q, false);
+				if (i == cnt - 1 && cur.e != 16)
+					corr += trail_sum(v, cur.e, false);
+			}
+			if (!(p.flags & CGCK_RAW)) {
+				uint4 w8[8];
+#pragma unroll
+				for (int u = 0; u < 8; ++u)
+					w8[u] = ldc<false>(c0, u, cnt, p.zero);
+				h = header<8, false>(w8, c0, cur.nch, cur.q, cur.len, p.flags, cur.ok);
+			}
+		}
+		if (first < p.n) {
+			const uint32_t r = fold16(acc) + (0xffffu - fold16(corr));
+			const Res res = result(p, cur.a0, cur.len, fold16(r), h);
+			const int slot = (int)(j % C) * 64 + l;
+			so[slot] = res.out;
+			if (p.verdict)
+				sv[slot] = (uint8_t)res.verdict;
+		}
+		if ((j + 1) % C == 0 || j + 1 == nsteps) {
+			const uint64_t f0 = gstep(j - j % C) * 64;
+			asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+			const uint64_t cntp = f0 < p.n ? (p.n - f0 < (uint64_t)C * 64 ? p.n - f0 : (uint64_t)C * 64) : 0;
+			if (defer_ok && cntp == (uint64_t)C * 64 && j + 1 < nsteps) {
+				pend = true; // stored after the next round's issue
+				pf0 = f0;
+			} else {
+				for (uint64_t i = l; i < cntp; i += 64) {
+					if (p.out)
+						gbl(p.out)[f0 + i] = so[i];
+					if (p.verdict)
+						gbl(p.verdict)[f0 + i] = sv[i];
+				}
+			}
+		}
+		cur = nxt;
+		nxt = nn;
+		--ia;
+	}
+	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#undef CGCK_LPX_ISSUE
+}
+#endif
+
 bool lpw_ok(const KParams &p)
 {
 	return !p.bad && !(p.flags & (CGCK_STORE | kFlagNoLenCheck | kFlagL4Auto)) &&
@@ -1823,6 +2038,25 @@ hipError_t launch_lpw(const KParams &p, int num_cus, hipStream_t st)
 		} else {
 			CGCK_NOTE_KERNEL("lpw_kernel<false, 8, false>");
 			hipLaunchKernelGGL((lpw_kernel<false, C8, false>), g8, dim3(64), lds8, st, q);
+		}
+		return hipGetLastError();
+	}
+	// $CGCK_LPW_X=1: lpx_kernel, two rounds in flight (7 waves per CU)
+	static const bool two = CGCK_ENV("CGCK_LPW_X") && atoi(CGCK_ENV("CGCK_LPW_X")) != 0;
+	if (two) {
+		static const int wpcx = [] {
+			const char *e = CGCK_ENV("CGCK_LPX_WPC");
+			return e && atoi(e) > 0 ? atoi(e) : 7;
+		}();
+		const uint64_t capx = (uint64_t)num_cus * wpcx;
+		const dim3 gx((unsigned)(want < capx ? (want ? want : 1) : capx));
+		const size_t ldsx = 2 * kLpwSlot + 3 * 1024 + 4 * kLpwWin + C * 64 * (p.verdict ? 5 : 4);
+		if (p.desc) {
+			CGCK_NOTE_KERNEL("lpx_kernel<true, %d>", C);
+			hipLaunchKernelGGL((lpx_kernel<true, C>), gx, dim3(64), ldsx, st, q);
+		} else {
+			CGCK_NOTE_KERNEL("lpx_kernel<false, %d>", C);
+			hipLaunchKernelGGL((lpx_kernel<false, C>), gx, dim3(64), ldsx, st, q);
 		}
 		return hipGetLastError();
 	}

@@ -14,6 +14,7 @@ from test_gpu_parity import FLAG_SETS, random_batch
 from batches import MIXES, packed_batch
 
 pytestmark = pytest.mark.gpu
+LPW = ("lpw_kernel<", "lpx_kernel<")   # lpx: the lab build's two-rounds-in-flight form ($CGCK_LPW_X)
 
 
 @pytest.fixture(scope="module")
@@ -42,7 +43,7 @@ def test_packed_batches(lpw, port, mix, flags):
     n = 40 if mix == "jumbo" else 3000
     buf, desc = packed_batch(rng, n, MIXES[mix], first_off=int(rng.integers(0, 16)))
     got, kernel = run(lpw, port, buf, desc, flags)
-    assert kernel.startswith("lpw_kernel<")
+    assert kernel.startswith(LPW)
     assert np.array_equal(got, buf)
 
 
@@ -107,9 +108,9 @@ def test_dispatcher_picks_lpw_for_mid_lengths(engine, port):
         for layout in (cgck.LAYOUT_PACKED, cgck.LAYOUT_ANY):
             engine.set_desc_layout(layout)
             _, k = run(engine, port, buf, desc, cgck.GEN_BOTH)
-            assert k.startswith("lpw_kernel<"), (layout, k)
+            assert k.startswith(LPW), (layout, k)
             _, k = run(engine, port, sbuf, sdesc, cgck.VERIFY_BSD)
-            assert k.startswith("lpw_kernel<"), (layout, k)
+            assert k.startswith(LPW), (layout, k)
         engine.set_desc_len_hint(200)
         _, k = run(engine, port, sbuf, sdesc, cgck.GEN_BOTH)
         assert k.startswith("slot2_kernel<"), k
@@ -139,7 +140,7 @@ def test_full_size_imix(lpw, port):
     e.sync()
     e.close()
     lpw.desc(buf.ptr, desc.ptr, n, cgck.GEN_BOTH, out.ptr)
-    assert lpw.last_kernel.startswith("lpw_kernel<")
+    assert lpw.last_kernel.startswith(LPW)
     o = np.zeros(n, np.uint32)
     r = np.zeros(n, np.uint32)
     out.download(o, stream=lpw.stream)
@@ -152,8 +153,8 @@ def test_full_size_imix(lpw, port):
     assert np.array_equal(o, r)
 
 
-@pytest.mark.parametrize("stride,ln,want", [(576, 576, "lpw_kernel<"), (300, 300, "lpw_kernel<"),
-                                            (1024, 576, "lpw_kernel<"), (2048, 300, "lpw_kernel<"),
+@pytest.mark.parametrize("stride,ln,want", [(576, 576, LPW), (300, 300, LPW),
+                                            (1024, 576, LPW), (2048, 300, LPW),
                                             (160, 160, "slot2_kernel<"), (1500, 1500, "cksum_kernel<")])
 def test_dispatcher_strided(engine, port, stride, ln, want):
     """Strided batches from 256 B to 1 KiB stream through lpw, back to back
@@ -196,7 +197,7 @@ def test_full_size_imix_ring(port):
         for x in (e, s2):
             x.set_desc_len_hint(nbytes // n)
         e.desc(buf.ptr, desc.ptr, n, cgck.GEN_BOTH, out.ptr)
-        assert e.last_kernel.startswith("lpw_kernel<"), e.last_kernel
+        assert e.last_kernel.startswith(LPW), e.last_kernel
         e.sync()
         s2.desc(buf.ptr, desc.ptr, n, cgck.GEN_BOTH, ref.ptr)
         assert s2.last_kernel.startswith("slot2_kernel<")
