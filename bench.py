@@ -236,10 +236,11 @@ def bench_strided(torch, dist, eng, cgck, n, size, plan, steps, warmup):
 
 def bench_imix(torch, dist, eng, cgck, n, plan, steps, warmup):
     """BASELINE configs[3]: the IMIX frames lie back to back in one buffer
-    (cgck_synth_imix), so the caller says so (cgck_set_desc_layout PACKED:
-    the streaming kernel, lpw).  The same batch without the hint (the
-    gathering kernel, slot2, what a caller with scattered frames gets) is
-    timed after it on the same buffer and reported beside it."""
+    (cgck_synth_imix).  Timed with the caller's layout hint
+    (cgck_set_desc_layout PACKED), then without it on the same buffer (the
+    dispatcher's own choice: lpw detects the back-to-back steps itself), then
+    the same frames in 2048 B receive-ring slots at +14; the same steps and
+    warm-up each."""
     nbytes = cgck.load().cgck_imix_bytes(n)
     buf = cgck.DeviceBuffer(nbytes)
     desc = cgck.DeviceBuffer(12 * n)
@@ -258,7 +259,7 @@ def bench_imix(torch, dist, eng, cgck, n, plan, steps, warmup):
     out.download(o, stream=eng.stream)
     eng.sync()
     eng.set_desc_layout(cgck.LAYOUT_ANY)
-    wall_u, ev_u = timed(torch, dist, eng, cgck, step, max(2, steps // 2), min(warmup, 2))
+    wall_u, ev_u = timed(torch, dist, eng, cgck, step, steps, warmup)
     unhinted = {"kernel": eng.last_kernel, "kernel_ms": ev_u,
                 "frac": (nbytes + 16 * n) / (ev_u * 1e-3) / HBM_PEAK}
     ou = __import__("numpy").zeros(n, "uint32")
@@ -275,7 +276,7 @@ def bench_imix(torch, dist, eng, cgck, n, plan, steps, warmup):
     eng.sync()
     wall_r, ev_r = timed(torch, dist, eng, cgck,
                          lambda: eng.desc(rbuf.ptr, rdesc.ptr, n, cgck.GEN_BOTH, out.ptr),
-                         max(2, steps // 2), min(warmup, 2))
+                         steps, warmup)
     ring = {"layout": f"{RING_SLOT} B slots, IPv4 at +{RING_L3}", "kernel": eng.last_kernel, "kernel_ms": ev_r,
             "frac": (nbytes + 16 * n) / (ev_r * 1e-3) / HBM_PEAK,
             "gpkt_s": n / (ev_r * 1e-3) / 1e9}

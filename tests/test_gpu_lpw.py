@@ -82,6 +82,43 @@ def test_unpacked_batches(lpw, port, max_len):
         run(lpw, port, ring, rd, flags)
 
 
+@pytest.mark.parametrize("total", [0, 511, 512, 513, 1024, 8191, 8192, 8193, 12000])
+def test_gathered_window_edges(lpw, port, total):
+    """Scattered steps (frames in slots, not back to back) whose chunk-run
+    list totals `total` chunks: exactly one / two windows, one over, the
+    16-window limit and past it (computed frame by frame from global memory);
+    frames at odd offsets, empty frames among them, then a whole empty step,
+    then the same step again: the owner table's marks, carries and row edges."""
+    rng = np.random.default_rng(total + 11)
+    n = 64
+    # split `total` chunks over 64 frames (some empty), each frame in its own slot
+    cuts = np.sort(rng.integers(0, total + 1, n - 1)) if total else np.zeros(n - 1, np.int64)
+    nch = np.diff(np.concatenate([[0], cuts, [total]]))
+    q = rng.integers(0, 16, n)
+    lens = np.where(nch > 0, np.maximum(16 * nch - q - rng.integers(0, 16, n), 1), 0)
+    lens = np.where((nch > 0) & (lens <= 16 * (nch - 1) - q), 16 * (nch - 1) - q + 1, lens)
+    lens = np.minimum(lens, 65535)
+    slot = int(max(16 * nch.max() + 64, 128)) if total else 128
+    frames = np.concatenate([np.arange(n), np.arange(n)])          # two steps of the same frames
+    buf = rng.integers(0, 256, 3 * n * slot + 64, dtype=np.uint8)
+    desc = np.zeros(3 * n, cgck.DESC_DTYPE)
+    for i in range(3 * n):
+        k = i % n
+        if n <= i < 2 * n:                      # the middle step: empty frames
+            desc[i] = (2 * n * slot, 0, 0)
+            continue
+        base = (k + (n if i >= 2 * n else 0)) * slot
+        o = base + int(q[k])
+        if lens[k]:
+            buf[o] = 0x45
+            buf[o + 9] = 6 if lens[k] > 9 else buf[o + 9]
+        desc[i] = (base, int(q[k]), int(lens[k]))
+    del frames
+    for flags in (cgck.GEN_BOTH, cgck.RAW):
+        _, k = run(lpw, port, buf, desc, flags)
+        assert k.startswith(LPW), k
+
+
 def test_reversed_overlapping_and_mixed_steps(lpw, port):
     """Descriptors walking a packed buffer backwards, pairs over the same
     bytes, and packed and unpacked 64-frame steps interleaved in one batch."""
