@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Launch one workload a few times (for rocprofv3 --pmc passes over a single
-kernel): imix | imixp (packed layout hint) | 64 | 1500.
+kernel): imix | imixp (packed layout hint) | ring (IMIX in 2048 B slots) | 64 | 1500.
 
     python tools/one_workload.py imixp [--launches 5] [--kernel FAMILY]
 """
@@ -23,7 +23,17 @@ def main():
     e = cgck.Engine(0)
     out = cgck.DeviceBuffer(4 * n)
     ev0, ev1 = cgck.Event(), cgck.Event()
-    if a.workload in ("imix", "imixp"):
+    if a.workload == "ring":   # the IMIX frames in 2048 B ring slots at +14
+        nbytes = cgck.load().cgck_imix_bytes(n)
+        buf = cgck.DeviceBuffer(2048 * n)
+        desc = cgck.DeviceBuffer(12 * n)
+        e.synth_imix_ring(buf.ptr, desc.ptr, n, 2048, 14, 0xC0C0)
+        e.set_desc_len_hint(nbytes // n)
+        algo = nbytes + 16 * n
+
+        def fn():
+            e.desc(buf.ptr, desc.ptr, n, cgck.GEN_BOTH, out.ptr)
+    elif a.workload in ("imix", "imixp"):
         nbytes = cgck.load().cgck_imix_bytes(n)
         buf = cgck.DeviceBuffer(nbytes)
         desc = cgck.DeviceBuffer(12 * n)
