@@ -309,37 +309,70 @@ static double now_s()
 	return ts.tv_sec + ts.tv_nsec * 1e-9;
 }
 
-static int burst_launch(cgck_ctx *c)
+// (Re)launch the server's K workgroups; the first request each serves is
+// the one after start_seq.
+// Server launches in this process: a relay word left by one launch (in
+// device memory a later server may get again) never matches another's tag.
+static std::atomic<uint32_t> g_burst_epoch{0};
+
+static int burst_launch(cgck_ctx *c, uint32_t start_seq)
 {
-	__atomic_store_n(&c->bbox->alive, 1u, __ATOMIC_RELEASE);
-	hipError_t e = launch_burst_server(c->bbox_dev, c->bstage_dev, c->bscratch, (uint32_t *)c->bresp_dev,
-					   c->bresp_dev + c->bresp_ver, c->d_zero, (uint32_t)c->bstage_cap, c->bmax,
-					   c->bstream);
+	uint32_t epoch;
+	while ((epoch = g_burst_epoch.fetch_add(1, std::memory_order_relaxed) + 1) == 0)
+		;
+	for (uint32_t j = 0; j < c->bwgs; j++)
+		__atomic_store_n(&c->bbox->alive[j], (uint8_t)1, __ATOMIC_RELEASE);
+	hipError_t e = launch_burst_server(c->bbox_dev, c->bstage_dev, c->bscratch, c->bresp_dev, c->brelay,
+					   c->d_zero, (uint32_t)c->bstage_cap,
+					   c->bmax, c->bwgs, start_seq, epoch, c->bstream);
 	if (e != hipSuccess) {
-		__atomic_store_n(&c->bbox->alive, 0u, __ATOMIC_RELEASE);
+		for (uint32_t j = 0; j < c->bwgs; j++)
+			__atomic_store_n(&c->bbox->alive[j], (uint8_t)0, __ATOMIC_RELEASE);
 		return set_err(-EIO, "burst server launch: %s", hipGetErrorString(e));
 	}
 	return 0;
 }
 
-// The server is one workgroup: a request costs the poll, one wide read of
-// the request block and the outputs' write acknowledgements (~5 us of host
-// round trips, tools/pingpong) instead of a launch and a stream
-// synchronisation (~9.4 us for an empty kernel).  One CU's reads over the
-// fabric are slow in bulk, though (a 73 KiB block: +12 us), so only small
-// requests go to it: at most one pass of its lane shape (64 packets, or 256
-// of at most 80 bytes) and 96 KiB of packet bytes; registered packets are
-// copied into the block up to 32 KiB of block and read in place above.  The
-// caps are where the server stopped beating the launch path on the registered
-// RX window at 64 / 576 / 1500 B (tools/txburst, profiles/r02/burst).  TX
-// flushes (mixed 20 B / full-size entries) keep the launch path.
-// $CGCK_SERVER_PKTS / _BYTES / _COPY override the caps for A/B runs (lab build).
+static bool burst_all_alive(const cgck_ctx *c)
+{
+	for (uint32_t j = 0; j < c->bwgs; j++)
+		if (!__atomic_load_n(&c->bbox->alive[j], __ATOMIC_ACQUIRE))
+			return false;
+	return true;
+}
+
+// A workgroup has idled out (or the server is draining): stop the rest,
+// wait until every workgroup has left, relaunch them for the request after
+// start_seq.
+static int burst_restart(cgck_ctx *c, uint32_t start_seq)
+{
+	__atomic_store_n(&c->bbox->stop, 1u, __ATOMIC_RELEASE);
+	const hipError_t e = hipStreamSynchronize(c->bstream);
+	__atomic_store_n(&c->bbox->stop, 0u, __ATOMIC_RELEASE);
+	if (e != hipSuccess)
+		return set_err(-EIO, "burst server drain: %s", hipGetErrorString(e));
+	return burst_launch(c, start_seq);
+}
+
+// A request costs the poll, the round trips of the request block and the
+// packet bytes, and the outputs' write acknowledgements (~5 us for a small
+// one, tools/pingpong) instead of a launch and a stream synchronisation
+// (~9.4 us for an empty kernel).  Up to kBurstPerWG packets one workgroup
+// serves it from one wide read of the block; larger requests are split over
+// up to K workgroups, each reading its slice of the descriptors and the
+// packet bytes where they lie, so the host reads spread over CUs as a
+// launch's do.  Registered packets are copied into the block up to 32 KiB of
+// block (one read for a small request) and read in place above.  TX flushes
+// (mixed 20 B / full-size entries) keep the launch path.  The caps:
+// kServerBytes of packet bytes per request (above it the launch path's many
+// workgroups read the fabric faster).  $CGCK_SERVER_PKTS / _BYTES / _COPY
+// override the caps for A/B runs (lab build).
 static size_t env_size(const char *v, size_t dflt)
 {
 	return v && *v ? (size_t)strtoull(v, nullptr, 0) : dflt;
 }
-static const size_t kServerBytes = env_size(CGCK_ENV("CGCK_SERVER_BYTES"), 96 << 10);
-static const uint64_t kServerPkts = env_size(CGCK_ENV("CGCK_SERVER_PKTS"), 64); // 4x for packets <= 80 B
+static const size_t kServerBytes = env_size(CGCK_ENV("CGCK_SERVER_BYTES"), 4 << 20);
+static const uint64_t kServerPkts = env_size(CGCK_ENV("CGCK_SERVER_PKTS"), 1u << 20);
 static const size_t kServerCopy = env_size(CGCK_ENV("CGCK_SERVER_COPY"), 32 << 10);
 
 // Offsets in the request block of n descriptors and `staged` packet bytes
@@ -362,8 +395,9 @@ static BurstLayout burst_layout(size_t staged, uint64_t n)
 // the server?
 static bool burst_fits(const cgck_ctx *c, uint64_t n, uint32_t max_len, size_t staged, size_t data)
 {
-	return c->bbox && n <= c->bmax && n <= (max_len <= 80 ? 4 * kServerPkts : kServerPkts) &&
-	       burst_layout(staged, n).bytes <= c->bstage_cap && data <= kServerBytes;
+	(void)max_len;
+	return c->bbox && n <= c->bmax && n <= kServerPkts && burst_layout(staged, n).bytes <= c->bstage_cap &&
+	       data <= kServerBytes;
 }
 
 // Serve the request whose descriptors (and, for base_dev == nullptr, packet
@@ -380,29 +414,54 @@ static int burst_serve(cgck_ctx *c, const uint8_t *base_dev, uint64_t n, uint32_
 	r->base = (uint64_t)(uintptr_t)base_dev;
 	r->d_off = (uint32_t)L.d_off;
 	r->p_off = (uint32_t)L.p_off;
-	const uint32_t seq = ++c->bseq;
-	__atomic_store_n(&b->seq_req, seq, __ATOMIC_RELEASE);
-	if (!__atomic_load_n(&b->alive, __ATOMIC_ACQUIRE)) {
-		int rc = burst_launch(c); // idled out: a new server picks the request up
+	if (++c->bseq == 0) // seq 0 is the relay word's "nothing posted"
+		++c->bseq;
+	const uint32_t seq = c->bseq;
+	__atomic_store_n(&b->req, (uint64_t)seq | (uint64_t)n << 32, __ATOMIC_RELEASE);
+	if (!burst_all_alive(c)) {
+		int rc = burst_restart(c, seq - 1); // idled out: a new server picks the request up
 		if (rc)
 			return rc;
 	}
+	const uint32_t W = burst_wgs((uint32_t)n, c->bwgs);
 	const double t0 = now_s();
-	for (uint32_t spin = 0; __atomic_load_n(&b->seq_done, __ATOMIC_ACQUIRE) != seq; spin++) {
-		__builtin_ia32_pause();
-		if ((spin & 1023) != 1023)
+	uint32_t spin = 0;
+	for (uint32_t j = 0; j < W;) {
+		if (__atomic_load_n(&b->done[j], __ATOMIC_ACQUIRE) == seq) {
+			j++;
 			continue;
-		if (!__atomic_load_n(&b->alive, __ATOMIC_ACQUIRE) && __atomic_load_n(&b->seq_done, __ATOMIC_ACQUIRE) != seq) {
-			// exited between our post and its last poll: relaunch after it drains
-			(void)hipStreamSynchronize(c->bstream);
-			if (__atomic_load_n(&b->seq_done, __ATOMIC_ACQUIRE) == seq)
-				break;
-			int rc = burst_launch(c);
+		}
+		__builtin_ia32_pause();
+		if ((++spin & 1023) != 0)
+			continue;
+		if (!burst_all_alive(c)) {
+			// a workgroup exited between our post and its last poll: drain
+			// and relaunch (a request served twice writes the same outputs)
+			int rc = burst_restart(c, seq - 1);
 			if (rc)
 				return rc;
 		}
-		if (now_s() - t0 > 2.0)
-			return set_err(-ETIMEDOUT, "burst server: request %u not served in 2 s", seq);
+		if (now_s() - t0 > 2.0) {
+			// Drain before returning, so no workgroup touches the caller's
+			// memory after the call (each leaves within its idle bound),
+			// and say which slices never came back.
+			char miss[160];
+			int at = 0;
+			for (uint32_t k = 0; k < W && at < (int)sizeof(miss) - 12; k++)
+				if (__atomic_load_n(&b->done[k], __ATOMIC_ACQUIRE) != seq)
+					at += snprintf(miss + at, sizeof(miss) - at, " %u:%u", k,
+						       __atomic_load_n(&b->done[k], __ATOMIC_ACQUIRE));
+			miss[at] = 0;
+			__atomic_store_n(&b->stop, 1u, __ATOMIC_RELEASE);
+			(void)hipStreamSynchronize(c->bstream);
+			__atomic_store_n(&b->stop, 0u, __ATOMIC_RELEASE);
+			uint64_t relay = 0;
+			(void)hipMemcpy(&relay, c->brelay, 8, hipMemcpyDeviceToHost);
+			return set_err(-ETIMEDOUT,
+				       "burst server: request %u (n %llu, W %u) not served in 2 s; missing (wg:done)%s; "
+				       "relay %#llx",
+				       seq, (unsigned long long)n, W, miss, (unsigned long long)relay);
+		}
 	}
 	const uint32_t bad = __atomic_load_n(&b->bad_req, __ATOMIC_ACQUIRE);
 	if (bad != c->bbad) {
@@ -449,7 +508,7 @@ static void *registered_ptr(void *p, size_t bytes)
 }
 
 int cgck::desc_host(cgck_ctx *c, void *base, size_t bytes, const cgck_desc_t *desc, uint64_t n, uint32_t flags,
-		    uint32_t *out, uint8_t *verdict)
+		    uint32_t *out, uint8_t *verdict, uint32_t *meta)
 {
 	if (n == 0)
 		return 0;
@@ -507,14 +566,17 @@ int cgck::desc_host(cgck_ctx *c, void *base, size_t bytes, const cgck_desc_t *de
 			return rc;
 		if (out)
 			memcpy(out, c->bresp, 4 * n);
+		if (meta)
+			memcpy(meta, c->bresp + burst_meta_off((uint32_t)n), 4 * n);
 		if (verdict)
-			memcpy(verdict, c->bresp + c->bresp_ver, n);
+			memcpy(verdict, c->bresp + burst_ver_off((uint32_t)n), n);
 		return 0;
 	}
 	if (dev_base || pkt_bytes <= kStageBytes) {
-		// pinned staging: [packets (staged case)] | descriptors | out | verdict
+		// pinned staging: [packets (staged case)] | descriptors | out | meta | verdict
 		const size_t sbytes = dev_base ? 0 : pkt_bytes;
-		const size_t d_off = sbytes, o_off = (d_off + 12 * n + 15) & ~(size_t)15, v_off = o_off + 4 * n;
+		const size_t d_off = sbytes, o_off = (d_off + 12 * n + 15) & ~(size_t)15, m_off = o_off + 4 * n,
+			     v_off = m_off + (meta ? 4 * n : 0);
 		if ((rc = grow_host((void **)&c->h_stage, &c->h_stage_cap, v_off + n)))
 			return rc;
 		uint8_t *h = c->h_stage;
@@ -532,13 +594,16 @@ int cgck::desc_host(cgck_ctx *c, void *base, size_t bytes, const cgck_desc_t *de
 			}
 		}
 		uint32_t *o = (uint32_t *)(h + o_off);
+		uint32_t *m = meta ? (uint32_t *)(h + m_off) : nullptr;
 		uint8_t *v = h + v_off;
-		KParams p = {dev_base ? (const uint8_t *)dev_base : h, d, n, 0, 0, 0, flags, o, v, nullptr, 0, nullptr};
+		KParams p = {dev_base ? (const uint8_t *)dev_base : h, d, n, 0, 0, 0, flags, o, v, nullptr, 0, nullptr, m};
 		if ((rc = run(c, p, hint, st)))
 			return rc;
 		HIP_TRY(hipStreamSynchronize(st));
 		if (out)
 			memcpy(out, o, 4 * n);
+		if (meta)
+			memcpy(meta, m, 4 * n);
 		if (verdict)
 			memcpy(verdict, v, n);
 		if ((flags & CGCK_STORE) && !dev_base)
@@ -548,21 +613,24 @@ int cgck::desc_host(cgck_ctx *c, void *base, size_t bytes, const cgck_desc_t *de
 		return 0;
 	}
 	// a large pageable batch: DMA of [base, base + bytes) into device scratch
-	const size_t dbytes = 12 * n, obytes = 4 * n, vbytes = n;
+	const size_t dbytes = 12 * n, obytes = 4 * n, vbytes = n, mbytes = meta ? 4 * n : 0;
 	if ((rc = grow_dev((void **)&c->d_bytes, &c->d_bytes_cap, bytes)))
 		return rc;
-	if ((rc = grow_dev((void **)&c->d_aux, &c->d_aux_cap, dbytes + obytes + vbytes + 64)))
+	if ((rc = grow_dev((void **)&c->d_aux, &c->d_aux_cap, dbytes + obytes + mbytes + vbytes + 64)))
 		return rc;
 	uint8_t *d_desc = c->d_aux;
 	uint32_t *d_out = (uint32_t *)(c->d_aux + ((dbytes + 15) & ~(size_t)15));
-	uint8_t *d_ver = (uint8_t *)(d_out + n);
+	uint32_t *d_meta = meta ? d_out + n : nullptr;
+	uint8_t *d_ver = (uint8_t *)(d_out + n + (meta ? n : 0));
 	HIP_TRY(hipMemcpyAsync(c->d_bytes, base, bytes, hipMemcpyHostToDevice, st));
 	HIP_TRY(hipMemcpyAsync(d_desc, desc, dbytes, hipMemcpyHostToDevice, st));
-	KParams p = {c->d_bytes, (const cgck_desc_t *)d_desc, n, 0, 0, 0, flags, d_out, d_ver, nullptr, 0, nullptr};
+	KParams p = {c->d_bytes, (const cgck_desc_t *)d_desc, n, 0, 0, 0, flags, d_out, d_ver, nullptr, 0, nullptr, d_meta};
 	if ((rc = run(c, p, hint, st)))
 		return rc;
 	if (out)
 		HIP_TRY(hipMemcpyAsync(out, d_out, obytes, hipMemcpyDeviceToHost, st));
+	if (meta)
+		HIP_TRY(hipMemcpyAsync(meta, d_meta, mbytes, hipMemcpyDeviceToHost, st));
 	if (verdict)
 		HIP_TRY(hipMemcpyAsync(verdict, d_ver, vbytes, hipMemcpyDeviceToHost, st));
 	uint8_t *back = nullptr;
@@ -684,7 +752,7 @@ int cgck::one_region(cgck_ctx *c, const void *src, uint32_t span, uint32_t ip_le
 		return rc;
 	if (span)
 		memcpy(c->h_stage, src, span);
-	KParams p = {c->h_stage, nullptr, 1, 0, 0, ip_len, flags, c->h_out, nullptr, nullptr, 0, nullptr};
+	KParams p = {c->h_stage, nullptr, 1, 0, 0, ip_len, flags | kFlagGroup, c->h_out, nullptr, nullptr, 0, nullptr};
 	if ((rc = run(c, p, ip_len, c->stream)))
 		return rc;
 	HIP_TRY(hipStreamSynchronize(c->stream));
@@ -725,15 +793,26 @@ extern "C" int cgck_burst_open(cgck_ctx_t *c, uint32_t max_pkts, size_t max_byte
 	// server's first read fetches kBurstFirst bytes whatever the request
 	size_t cap = burst_layout(((max_bytes + 15) & ~(size_t)15) + 16 * (size_t)max_pkts, max_pkts).bytes;
 	cap = (cap < kBurstFirst ? kBurstFirst : cap + 15) & ~(size_t)15;
-	const size_t ver_off = (4 * (size_t)max_pkts + 63) & ~(size_t)63;
+	const size_t ver_off = burst_ver_off(max_pkts); // the outputs of the largest request
+	size_t resp_bytes = ver_off + max_pkts;
+	unsigned resp_flags = hipHostMallocCoherent;
+	if (const char *e = CGCK_ENV("CGCK_BRESP_MIN")) // lab A/B: allocation size of the outputs
+		resp_bytes = resp_bytes < env_size(e, 0) ? env_size(e, 0) : resp_bytes;
+	if (const char *e = CGCK_ENV("CGCK_BRESP_FLAGS")) // lab A/B: their hipHostMalloc flags
+		resp_flags = (unsigned)env_size(e, hipHostMallocCoherent);
 	void *box = nullptr, *st = nullptr, *rs = nullptr, *bd = nullptr, *sd = nullptr, *rd = nullptr, *sc = nullptr;
 	hipError_t e = hipHostMalloc(&box, sizeof(BurstBox), hipHostMallocCoherent);
 	if (e == hipSuccess)
 		e = hipHostMalloc(&st, cap, hipHostMallocCoherent);
 	if (e == hipSuccess)
-		e = hipHostMalloc(&rs, ver_off + max_pkts, hipHostMallocCoherent);
+		e = hipHostMalloc(&rs, resp_bytes, resp_flags);
 	if (e == hipSuccess)
 		e = hipMalloc(&sc, cap);
+	// the leader's relay word, uncached: every poll and store goes to memory,
+	// whichever XCD's L2 the workgroups sit behind
+	void *rl = nullptr;
+	if (e == hipSuccess)
+		e = hipExtMallocWithFlags(&rl, 64, hipDeviceMallocUncached);
 	if (e == hipSuccess)
 		e = hipHostGetDevicePointer(&bd, box, 0);
 	if (e == hipSuccess)
@@ -748,11 +827,20 @@ extern "C" int cgck_burst_open(cgck_ctx_t *c, uint32_t max_pkts, size_t max_byte
 				(void)hipHostFree(h);
 		if (sc)
 			(void)hipFree(sc);
+		if (rl)
+			(void)hipFree(rl);
 		return set_err(-EIO, "cgck_burst_open: %s", hipGetErrorString(e));
 	}
 	memset(box, 0, sizeof(BurstBox));
 	memset(st, 0, cap);
 	c->bbox = (BurstBox *)box;
+	// one workgroup per kBurstPerWG packets of the largest request, at most
+	// kBurstMaxWG (and the device's CUs)
+	c->bwgs = burst_wgs(max_pkts, kBurstMaxWG);
+	if (c->bwgs > (uint32_t)c->num_cus)
+		c->bwgs = (uint32_t)c->num_cus;
+	if (const char *e = CGCK_ENV("CGCK_SERVER_WGS")) // lab A/B: K
+		c->bwgs = atoi(e) > 0 && atoi(e) <= (int)kBurstMaxWG ? (uint32_t)atoi(e) : c->bwgs;
 	c->bbox->idle_ticks = (uint64_t)(idle_ms ? idle_ms : 200) * 100000; // 100 MHz counter
 	c->bstage = (uint8_t *)st;
 	c->bstage_cap = cap;
@@ -760,12 +848,12 @@ extern "C" int cgck_burst_open(cgck_ctx_t *c, uint32_t max_pkts, size_t max_byte
 	c->bbox_dev = (BurstBox *)bd;
 	c->bresp = (uint8_t *)rs;
 	c->bresp_dev = (uint8_t *)rd;
-	c->bresp_ver = ver_off;
 	c->bscratch = (uint8_t *)sc;
+	c->brelay = (uint64_t *)rl;
 	c->bmax = max_pkts;
 	c->bseq = 0;
 	c->bbad = 0;
-	return burst_launch(c);
+	return burst_launch(c, 0);
 }
 
 extern "C" int cgck_burst_close(cgck_ctx_t *c)
@@ -782,11 +870,13 @@ extern "C" int cgck_burst_close(cgck_ctx_t *c)
 	(void)hipHostFree(c->bstage);
 	(void)hipHostFree(c->bresp);
 	(void)hipFree(c->bscratch);
+	(void)hipFree(c->brelay);
 	c->bbox = nullptr;
 	c->bstage = nullptr;
 	c->bstage_cap = 0;
 	c->bresp = nullptr;
 	c->bscratch = nullptr;
+	c->brelay = nullptr;
 	if (e != hipSuccess)
 		return set_err(-EIO, "cgck_burst_close: %s", hipGetErrorString(e));
 	return 0;

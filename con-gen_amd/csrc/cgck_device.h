@@ -119,6 +119,33 @@ __device__ __forceinline__ int l4_field(uint32_t proto, uint32_t flags)
 	return proto == 6 ? 16 : (proto == 17 ? 6 : -1);
 }
 
+// kFlagRx: which of the stack's verify calls a frame of `avail` bytes can
+// see (cgck_internal.h), from its first header bytes.  Returns the meta word
+// and sets *cover to the bytes to sum: min(ntohs(ip_len), avail), at least
+// the header; 0 when the stack drops the frame before any checksum
+// (ip_input.c:28-44, gbtcp/inet.c:282-306: 20 <= ip_hl * 4 <= len).  The L4
+// value is asked for only when the frame holds ntohs(ip_len) bytes
+// (ip_input.c:76, gbtcp/inet.c:314) and the segment its header
+// (tcp_input.c:67, udp_usrreq.c:65, ip_icmp.c:177).
+__device__ __forceinline__ uint32_t rx_meta(uint32_t avail, uint32_t b0, uint32_t tl_hi, uint32_t tl_lo,
+					    uint32_t proto, uint32_t *cover)
+{
+	const uint32_t hl = (b0 & 15) * 4;
+	if (avail < 20 || hl < 20 || hl > avail) {
+		*cover = 0;
+		return 0;
+	}
+	const uint32_t total = tl_hi << 8 | tl_lo;
+	uint32_t cv = total < avail ? total : avail;
+	*cover = cv < hl ? hl : cv;
+	const uint32_t l4len = total >= hl ? total - hl : 0;
+	const uint32_t need = proto == 6 ? 18 : proto == 17 ? 8 : proto == 1 ? 4 : 0xffffffffu;
+	uint32_t m = kRxOkIp | (proto == 1 ? kRxIcmp : 0) | hl << 8 | l4len << 16;
+	if (total >= hl && total <= avail && l4len >= need)
+		m |= kRxOkL4;
+	return m;
+}
+
 __device__ __forceinline__ void store16(uint8_t *p, uint32_t v)
 {
 	if ((reinterpret_cast<uintptr_t>(p) & 1) == 0) {
@@ -269,20 +296,26 @@ struct Sched {
 	uint64_t it, end, step;
 };
 
-__device__ __forceinline__ Sched sched(uint64_t n_iters, bool contig)
+// Block `bid` of `nb` (a burst-server workgroup runs its share as block 0 of 1).
+__device__ __forceinline__ Sched sched(uint64_t n_iters, bool contig, uint32_t bid, uint32_t nb)
 {
 	Sched s;
 	if (contig) {
-		const uint64_t per = (n_iters + gridDim.x - 1) / gridDim.x;
-		s.it = (uint64_t)blockIdx.x * per;
+		const uint64_t per = (n_iters + nb - 1) / nb;
+		s.it = (uint64_t)bid * per;
 		s.end = s.it + per < n_iters ? s.it + per : n_iters;
 		s.step = 1;
 	} else {
-		s.it = blockIdx.x;
+		s.it = bid;
 		s.end = n_iters;
-		s.step = gridDim.x;
+		s.step = nb;
 	}
 	return s;
+}
+
+__device__ __forceinline__ Sched sched(uint64_t n_iters, bool contig)
+{
+	return sched(n_iters, contig, blockIdx.x, gridDim.x);
 }
 
 struct Pkt {

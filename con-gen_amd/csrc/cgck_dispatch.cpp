@@ -86,7 +86,7 @@ hipError_t launch_cksum(const KParams &p0, uint32_t len_hint, int num_cus, int k
 	if (p0.n == 0)
 		return hipSuccess;
 	KParams p = p0;
-	const bool lane_ok = !(p.flags & (kFlagNoLenCheck | kFlagL4Auto));
+	const bool lane_ok = !(p.flags & (kFlagNoLenCheck | kFlagL4Auto | kFlagRx | kFlagGroup));
 	int variant = kernel & 15;
 	// aligned fixed-length strided batch of 20..64-byte packets (the 64 B config)
 	const bool lpa_ok = lane_ok && !p.desc && p.ip_len >= 20 && p.ip_len <= 64 &&

@@ -106,17 +106,6 @@ struct TxEntry {
 	int16_t fo; // -1: IP header entry (field ip+10); else L4 field offset after the header
 };
 
-enum { kRxIp = 1, kRxL4 = 2 };
-
-struct RxEntry {
-	const uint8_t *ip;
-	uint32_t out;   // lo16 header checksum, hi16 L4 checksum (ICMP: no pseudo-header)
-	uint16_t hl;    // ip_hl * 4 at rx_begin
-	uint16_t l4len; // ntohs(ip_len) - hl: the length the stack passes (ip_input.c:63,98; inet.c:313)
-	uint8_t proto;
-	uint8_t ok; // kRxIp | kRxL4: which values are valid
-};
-
 struct ThreadState {
 	cgck_ctx *ctx = nullptr;
 	// TX window
@@ -125,14 +114,20 @@ struct ThreadState {
 	const uint8_t *tx_max = nullptr; // highest header address queued so far
 	bool tx_map = false;             // txidx built (the first call below tx_max)
 	PtrMap txidx; // (ip << 1 | is_l4) -> txq index
-	// RX window
+	// RX window: frame i's header at rx_base + rxd[i].frame_off +
+	// rxd[i].l3_off; rxo[i] its values (lo16 header checksum, hi16 L4
+	// checksum, ICMP without the pseudo-header) and rxm[i] which calls they
+	// answer (kFlagRx's meta word: kRxOkIp | kRxOkL4 | kRxIcmp, ip_hl * 4 in
+	// bits 8-15, ntohs(ip_len) - ip_hl * 4 in bits 16-31, zero for a frame the
+	// stack drops before any checksum), both written by the kernel
 	bool rx_open = false;
-	std::vector<RxEntry> rx;
-	size_t rx_cur = 0;    // the entry the last answered call matched
+	const uint8_t *rx_base = nullptr;
+	size_t rx_n = 0;
+	size_t rx_cur = 0;    // the frame the last answered call matched
 	bool rx_map = false;  // rxidx built (on the first call off the cursor)
-	PtrMap rxidx; // ip -> entry << 1; ip + hl (ICMP message) -> entry << 1 | 1
+	PtrMap rxidx; // ip -> frame << 1; ip + hl (ICMP message) -> frame << 1 | 1
 	std::vector<cgck_desc_t> rxd;
-	std::vector<uint32_t> rxo;
+	std::vector<uint32_t> rxo, rxm;
 	uint64_t rx_served0 = 0; // stats[0] at rx_begin
 	uint64_t stats[4] = {0, 0, 0, 0};
 };
@@ -166,22 +161,34 @@ uint32_t sync_region(const void *src, uint32_t span, uint32_t ip_len, uint32_t f
 	return out;
 }
 
-// The window entry a pointer names: (entry << 1) for an IPv4 header, (entry
-// << 1 | 1) for the ICMP message after it.  The stack walks a burst in slot
-// order and asks for each frame's header and then its segment, so the entry
-// of the previous answer or the one after it almost always matches; a map
-// of every entry is built only on the first call that matches neither.
-bool rx_find(ThreadState &t, const uint8_t *p, uint32_t *v)
+// The window frame a pointer names: (frame << 1) for an IPv4 header,
+// (frame << 1 | 1) for the ICMP message after it.  The stack walks a burst in
+// slot order and asks for each frame's header and then its segment, so the
+// frame of the previous answer or the next answerable one almost always
+// matches; a map of every frame is built only on the first call that matches
+// neither.
+inline const uint8_t *rx_ip(const ThreadState &t, size_t i)
 {
-	const size_t n = t.rx.size();
-	for (size_t i = t.rx_cur; i < t.rx_cur + 2 && i < n; i++) {
-		const RxEntry &e = t.rx[i];
-		if (e.ip == p) {
+	return t.rx_base + t.rxd[i].frame_off + t.rxd[i].l3_off;
+}
+
+__attribute__((noinline)) bool rx_find_slow(ThreadState &t, const uint8_t *p, uint32_t *v)
+{
+	const size_t n = t.rx_n;
+	const uint32_t *m = t.rxm.data();
+	// the cursor frame, then the next answerable ones (frames the stack
+	// dropped unverified have no calls: up to 8 are stepped over)
+	for (size_t i = t.rx_cur, seen = 0, lim = t.rx_cur + 10; i < n && i < lim && seen < 2; i++) {
+		if (!m[i])
+			continue;
+		seen++;
+		const uint8_t *ip = rx_ip(t, i);
+		if (ip == p) {
 			*v = (uint32_t)(i << 1);
 			t.rx_cur = i;
 			return true;
 		}
-		if (e.proto == 1 && e.ip + e.hl == p) {
+		if ((m[i] & kRxIcmp) && ip + (m[i] >> 8 & 0xff) == p) {
 			*v = (uint32_t)(i << 1 | 1);
 			t.rx_cur = i;
 			return true;
@@ -190,10 +197,12 @@ bool rx_find(ThreadState &t, const uint8_t *p, uint32_t *v)
 	if (!t.rx_map) {
 		t.rxidx.reset(2 * n);
 		for (size_t i = 0; i < n; i++) {
-			const RxEntry &e = t.rx[i];
-			t.rxidx.put((uintptr_t)e.ip, (uint32_t)(i << 1));
-			if (e.proto == 1 && (e.ok & kRxL4))
-				t.rxidx.put((uintptr_t)(e.ip + e.hl), (uint32_t)(i << 1 | 1));
+			if (!m[i])
+				continue;
+			const uint8_t *ip = rx_ip(t, i);
+			t.rxidx.put((uintptr_t)ip, (uint32_t)(i << 1));
+			if ((m[i] & (kRxIcmp | kRxOkL4)) == (kRxIcmp | kRxOkL4))
+				t.rxidx.put((uintptr_t)(ip + (m[i] >> 8 & 0xff)), (uint32_t)(i << 1 | 1));
 		}
 		t.rx_map = true;
 	}
@@ -201,6 +210,26 @@ bool rx_find(ThreadState &t, const uint8_t *p, uint32_t *v)
 		return false;
 	t.rx_cur = *v >> 1;
 	return true;
+}
+
+// The header of the cursor frame or of the next one (the stack's next call
+// is almost always one of the two) without leaving the caller; everything
+// else (ICMP messages, skipped frames, the map) in rx_find_slow.
+inline bool rx_find(ThreadState &t, const uint8_t *p, uint32_t *v)
+{
+	const size_t i = t.rx_cur;
+	if (__builtin_expect(i + 1 < t.rx_n, 1)) {
+		if (t.rxm[i] && rx_ip(t, i) == p) {
+			*v = (uint32_t)(i << 1);
+			return true;
+		}
+		if (t.rxm[i + 1] && rx_ip(t, i + 1) == p) {
+			*v = (uint32_t)((i + 1) << 1);
+			t.rx_cur = i + 1;
+			return true;
+		}
+	}
+	return rx_find_slow(t, p, v);
 }
 
 // Queue one field; a header or segment queued again replaces its entry (the
@@ -325,14 +354,14 @@ extern "C" uint16_t in_cksum(void *data, int len)
 		// ip_icmp.c:189, after the caller zeroed the field
 		uint32_t v;
 		if (rx_find(t, b, &v)) {
-			const RxEntry &e = t.rx[v >> 1];
-			if (!(v & 1) && (e.ok & kRxIp) && len == e.hl) {
+			const uint32_t m = t.rxm[v >> 1];
+			if (!(v & 1) && (m & kRxOkIp) && (uint32_t)len == (m >> 8 & 0xff)) {
 				t.stats[0]++;
-				return (uint16_t)e.out;
+				return (uint16_t)t.rxo[v >> 1];
 			}
-			if ((v & 1) && (e.ok & kRxL4) && len == e.l4len) {
+			if ((v & 1) && (m & kRxOkL4) && (uint32_t)len == m >> 16) {
 				t.stats[0]++;
-				return (uint16_t)(e.out >> 16);
+				return (uint16_t)(t.rxo[v >> 1] >> 16);
 			}
 		}
 		rx_miss = true;
@@ -366,10 +395,10 @@ extern "C" uint16_t udp_cksum(struct ip *ipp, int len)
 		// udp_cksum(ip, len) at udp_usrreq.c:89
 		uint32_t v;
 		if (rx_find(t, ip, &v) && !(v & 1)) {
-			const RxEntry &e = t.rx[v >> 1];
-			if ((e.ok & kRxL4) && e.proto != 1 && (uint32_t)len == e.l4len && hl == e.hl) {
+			const uint32_t m = t.rxm[v >> 1];
+			if ((m & (kRxOkL4 | kRxIcmp)) == kRxOkL4 && (uint32_t)len == m >> 16 && hl == (m >> 8 & 0xff)) {
 				t.stats[0]++;
-				return (uint16_t)(e.out >> 16);
+				return (uint16_t)(t.rxo[v >> 1] >> 16);
 			}
 		}
 		rx_miss = true;
@@ -409,55 +438,31 @@ extern "C" int cgck_rx_begin(void *base, size_t bytes, const cgck_desc_t *desc, 
 	cgck_ctx *c = thread_ctx();
 	if (!c)
 		return -ENODEV; // thread_ctx set the message
-	t.rx.clear();
-	t.rxd.clear();
-	const uint8_t *b = (const uint8_t *)base;
-	for (uint64_t i = 0; i < n; i++) {
-		const uint64_t at = desc[i].frame_off + desc[i].l3_off;
-		if (at + desc[i].ip_len > bytes || at < desc[i].frame_off)
-			return set_err(-EINVAL, "cgck_rx_begin: descriptor %llu reaches past the %zu bytes given",
-				       (unsigned long long)i, bytes);
-		// Which calls the stack can make on this frame.  ip_input.c:28-44 and
-		// inet.c:282-306 drop before the header checksum unless 20 <= hl <=
-		// len; the L4 checksum runs only when the frame holds ntohs(ip_len)
-		// bytes (ip_input.c:76, inet.c:314) and the segment its header
-		// (tcp_input.c:67, udp_usrreq.c:65, ip_icmp.c:177).
-		const uint32_t avail = desc[i].ip_len;
-		if (avail < 20)
-			continue;
-		const uint8_t *ip = b + at;
-		const uint32_t hl = (ip[0] & 15) * 4;
-		if (hl < 20 || hl > avail)
-			continue;
-		const uint32_t total = (uint32_t)ip[2] << 8 | ip[3];
-		const uint8_t proto = ip[9];
-		uint32_t cover = total < avail ? total : avail; // bytes the kernel reads
-		if (cover < hl)
-			cover = hl;
-		uint8_t ok = kRxIp;
-		const uint32_t l4len = total >= hl ? total - hl : 0;
-		const uint32_t need = proto == 6 ? 18 : proto == 17 ? 8 : proto == 1 ? 4 : 0xffffffffu;
-		if (total >= hl && total <= avail && l4len >= need)
-			ok |= kRxL4;
-		t.rx.push_back({ip, 0, (uint16_t)hl, (uint16_t)l4len, proto, ok});
-		cgck_desc_t d;
-		d.frame_off = desc[i].frame_off;
-		d.l3_off = desc[i].l3_off;
-		d.ip_len = (uint16_t)cover;
-		t.rxd.push_back(d);
+	// One launch (or one burst-server request) over the whole burst: the
+	// kernel sums each frame's header and L4 checksum with the fields read as
+	// zero (ICMP without the pseudo-header) and itself decides, from the
+	// frame's header, which calls the stack can make on it (kFlagRx: the
+	// drop rules of ip_input.c:28-44, 76, tcp_input.c:67, udp_usrreq.c:65,
+	// ip_icmp.c:177, gbtcp/inet.c:282-314), so no header is parsed here.
+	// desc_host checks every descriptor against [base, base + bytes).
+	t.rxd.assign(desc, desc + n);
+	t.rxo.resize(n ? n : 1);
+	t.rxm.resize(n ? n : 1);
+	if (n) {
+		const int rc = desc_host(c, base, bytes, t.rxd.data(), n,
+					 CGCK_IP | CGCK_L4 | CGCK_ZERO_FIELDS | kFlagL4Auto | kFlagRx, t.rxo.data(), nullptr,
+					 t.rxm.data());
+		if (rc) {
+			char msg[256];
+			snprintf(msg, sizeof(msg), "%s", err_text());
+			return set_err(rc, "cgck_rx_begin: %s", msg);
+		}
 	}
-	const uint64_t m = t.rx.size();
-	t.rxo.resize(m ? m : 1);
-	if (m) {
-		// header checksum + L4 checksum per frame, checksum fields read as
-		// zero; ICMP without the pseudo-header (kFlagL4Auto, group kernel)
-		const int rc = desc_host(c, base, bytes, t.rxd.data(), m,
-					 CGCK_IP | CGCK_L4 | CGCK_ZERO_FIELDS | kFlagL4Auto, t.rxo.data(), nullptr);
-		if (rc)
-			return rc;
-	}
-	for (uint64_t i = 0; i < m; i++)
-		t.rx[i].out = t.rxo[i];
+	uint64_t m = 0;
+	for (uint64_t i = 0; i < n; i++)
+		m += t.rxm[i] != 0;
+	t.rx_base = (const uint8_t *)base;
+	t.rx_n = n;
 	t.rx_cur = 0;
 	t.rx_map = false;
 	t.rx_open = true;
@@ -471,7 +476,7 @@ extern "C" int cgck_rx_end(void)
 	if (!t.rx_open)
 		return set_err(-EINVAL, "cgck_rx_end: no open RX window on this thread");
 	t.rx_open = false;
-	t.rx.clear();
+	t.rx_n = 0;
 	t.rx_map = false;
 	return (int)(t.stats[0] - t.rx_served0);
 }

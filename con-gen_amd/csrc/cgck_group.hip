@@ -26,7 +26,7 @@ namespace cgck {
 constexpr int kGrpStage = 2048;
 
 template <int G, int S, int U, bool DESC, bool NT>
-__device__ __forceinline__ void cksum_body(const KParams &p)
+__device__ __forceinline__ void cksum_body(const KParams &p, uint32_t bid, uint32_t nb)
 {
 	__shared__ uint32_t so[kGrpStage];
 	constexpr int GPB = 256 / G;        // groups per block
@@ -37,8 +37,9 @@ __device__ __forceinline__ void cksum_body(const KParams &p)
 	const uint32_t flags = p.flags;
 	const bool raw = flags & CGCK_RAW;
 	const bool need_hdr = !raw;
+	const bool rx = flags & kFlagRx; // uniform
 
-	const Sched sc = sched((p.n + PPB - 1) / PPB, p.contig);
+	const Sched sc = sched((p.n + PPB - 1) / PPB, p.contig, bid, nb);
 	const bool stage = p.contig && p.out; // block-uniform
 	uint64_t wb = sc.it * PPB;            // first packet of the open window
 	auto flush = [&](uint64_t e) {        // block-uniform call
@@ -53,7 +54,7 @@ __device__ __forceinline__ void cksum_body(const KParams &p)
 		if (stage && (blk + 1) * PPB > wb + kGrpStage)
 			flush(blk * PPB);
 		Pkt pk[U];
-		uint32_t b0[U], proto[U];
+		uint32_t b0[U], proto[U], tl[U]; // tl: ntohs(ip_len)'s bytes (kFlagRx)
 		uint4 v[U][S];
 		int nch[U];
 #pragma unroll
@@ -68,10 +69,16 @@ __device__ __forceinline__ void cksum_body(const KParams &p)
 			nch[u] = span ? (int)(((a0 + span + 15) >> 4) - (a0 >> 4)) : 0;
 			b0[u] = 0;
 			proto[u] = 0;
+			tl[u] = 0;
 			if (need_hdr && pk[u].ok && span > 0) {
 				b0[u] = *gbl_at<const uint8_t>(a0);
 				if (span > 9)
 					proto[u] = *gbl_at<const uint8_t>(a0 + 9);
+				// kFlagRx: the frame's own length field, read with the
+				// chunks (one round trip), so its coverage is decided after
+				// the loads and the surplus chunks are masked by position
+				if (rx && span >= 20)
+					tl[u] = (uint32_t)*gbl_at<const uint8_t>(a0 + 2) << 8 | *gbl_at<const uint8_t>(a0 + 3);
 			}
 			const uint4 *c0 = reinterpret_cast<const uint4 *>(a0 & ~(uint64_t)15);
 			// clamped: chunks past the packet re-read its last chunk and
@@ -83,7 +90,10 @@ __device__ __forceinline__ void cksum_body(const KParams &p)
 #pragma unroll
 		for (int u = 0; u < U; ++u) {
 			const int q = (int)(pk[u].a0 & 15);
-			const int len = (int)pk[u].len;
+			uint32_t rxm = 0, cover = pk[u].len;
+			if (rx)
+				rxm = rx_meta(pk[u].len, b0[u], tl[u] >> 8, tl[u] & 0xffu, proto[u], &cover);
+			const int len = (int)cover;
 			const int hl = (int)(b0[u] & 15) * 4;
 			const int fo = (need_hdr && (flags & (CGCK_L4)) && len >= 20 && len >= hl &&
 					l4_field(proto[u], flags) >= 0 &&
@@ -179,6 +189,8 @@ __device__ __forceinline__ void cksum_body(const KParams &p)
 				gbl(p.out)[k] = lo | (hi << 16);
 			if (p.verdict)
 				gbl(p.verdict)[k] = (uint8_t)verdict;
+			if (rx && p.meta)
+				gbl(p.meta)[k] = rxm;
 			if (p.bad) {
 				if (verdict & CGCK_BAD_IP)
 					atomicAdd(p.bad + 0, 1u);
@@ -194,24 +206,31 @@ __device__ __forceinline__ void cksum_body(const KParams &p)
 template <int G, int S, int U, bool DESC, bool NT>
 __global__ __launch_bounds__(256) void cksum_kernel(KParams p)
 {
-	cksum_body<G, S, U, DESC, NT>(p);
+	cksum_body<G, S, U, DESC, NT>(p, blockIdx.x, gridDim.x);
 }
 
 // --------------------------------------------------------------------------
-// Burst server: one resident workgroup that serves small host-resident
-// batches (RX bursts, drop-in calls) without a launch or a stream
-// synchronisation per batch.  The host writes a request block (BurstReq,
-// descriptors, packet bytes) into host-coherent staging and bumps seq_req;
-// thread 0 polls it with system-scope acquire loads.  The workgroup then
-// copies the block into device scratch with one wide read (tools/pingpong:
-// every dependent host round trip costs ~1.3 us, so the block is fetched at
-// once instead of header -> descriptor -> packet bytes), runs the group
-// kernel's body over the scratch copy (or over registered ring memory in
-// place, for larger or in-place-store requests), writes the outputs to
-// host-coherent memory and publishes seq_done with a system-scope release.
-// Every poll loop is bounded: the server exits on `stop`, or after
-// idle_ticks of the 100 MHz real-time counter without a request (the host
-// relaunches it on the next request), so no launch outlives its context.
+// Burst server: K resident workgroups that serve small and mid-size
+// host-resident batches (RX bursts, drop-in calls) without a launch or a
+// stream synchronisation per batch.  The host writes a request block
+// (BurstReq, descriptors, packet bytes) into host-coherent staging and stores
+// req = seq | n << 32; thread 0 of every workgroup polls it with relaxed
+// system-scope loads.  W = burst_wgs(n, K) workgroups serve the request:
+//  * W == 1 (up to kBurstPerWG packets: a drop-in call, a small burst):
+//    workgroup 0 copies the block into device scratch with one wide read
+//    (tools/pingpong: every dependent host round trip costs ~1.3 us, so the
+//    block is fetched at once instead of header -> descriptor -> packet
+//    bytes) and runs the group body over the copy, or over registered ring
+//    memory in place;
+//  * W > 1: workgroup j reads the header and its own slice of the
+//    descriptors (d_off is fixed, so both in one round trip) into scratch,
+//    then the packet bytes where they lie (registered memory, or the block):
+//    the burst's host reads spread over W CUs, as a launch's would.
+// Each serving workgroup writes its outputs to host-coherent memory and
+// publishes done[j] after a system-scope release.  Every poll loop is
+// bounded: a workgroup exits on `stop`, or after idle_ticks of the 100 MHz
+// real-time counter without a request (the host relaunches the server when
+// it finds a workgroup gone), so no launch outlives its context.
 // --------------------------------------------------------------------------
 
 __device__ __forceinline__ uint32_t sys_load(const uint32_t *p)
@@ -224,86 +243,201 @@ __device__ __forceinline__ uint32_t sys_relaxed(const uint32_t *p)
 	return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-__global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const uint8_t *req, uint8_t *scratch,
-							   uint32_t *out, uint8_t *verdict, const void *zero, uint32_t cap,
-							   uint32_t max_pkts)
+__device__ __forceinline__ uint64_t sys_relaxed64(const uint64_t *p)
 {
-	__shared__ uint32_t cmd; // 1 run the pending request, 2 exit
+	return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// The group body over a request's packets [lo, hi) (block 0 of 1).
+__device__ __forceinline__ void burst_body(const BurstReq &h, const uint8_t *scratch, uint32_t lo, uint32_t hi,
+					   uint32_t *out, uint32_t *meta, uint8_t *verdict, const void *zero,
+					   const uint8_t *base)
+{
+	KParams p = {base, reinterpret_cast<const cgck_desc_t *>(scratch + h.d_off) + lo,
+		     hi - lo, 0, 0, 0, h.flags, out + lo, verdict + lo, nullptr, 0, zero, meta + lo};
+	if (h.max_len <= 80)
+		cksum_body<4, 2, 4, true, false>(p, 0, 1);
+	else
+		cksum_body<16, 6, 4, true, false>(p, 0, 1);
+}
+
+// Device-memory command word of a server launch (the leader's relay to the
+// other workgroups): seq | n << 32; kBurstExit << 32 | epoch: leave.  Zeroed
+// by the host before every launch (seq 0 is never posted), and an exit word
+// counts only with this launch's epoch, so a word left over from an earlier
+// launch over the same memory can neither end nor feed this one.  The word
+// is uncached device memory (hipDeviceMallocUncached): an sc1 poll of a
+// cached line is served by the polling XCD's L2, which another XCD's store
+// does not refresh (the cached word: one wide request in a suite run was not
+// served in 2 s).
+constexpr uint32_t kBurstExit = 0xffffffffu;
+
+__device__ __forceinline__ uint64_t relay_load(const uint64_t *p)
+{
+	return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const uint8_t *req, uint8_t *scratch,
+							   uint8_t *resp, uint64_t *dcmd, const void *zero,
+							   uint32_t cap, uint32_t max_pkts, uint32_t start_seq,
+							   uint32_t epoch)
+{
+	__shared__ uint32_t cmd, cmd_n; // cmd: 1 run the pending request, 2 exit, 3 already served
 	__shared__ uint4 hdr_w[4];
 	const int t = threadIdx.x;
-	uint32_t last = 0; // thread 0: the last request served
-	if (t == 0)
-		last = sys_load(&box->seq_done);
+	const uint32_t j = blockIdx.x, K = gridDim.x;
+	uint32_t last = start_seq; // the last request seen (thread 0)
+	bool first = true;         // thread 0: no request seen since the launch
 	const uint4 *src = reinterpret_cast<const uint4 *>(req);
 	uint4 *dst = reinterpret_cast<uint4 *>(scratch);
 	for (;;) {
 		if (t == 0) {
 			const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
 			const uint64_t idle = box->idle_ticks;
-			uint32_t c = 0;
-			while (c == 0) {
-				// relaxed: an acquire load would invalidate the caches every poll
-				const uint32_t r = sys_relaxed(&box->seq_req);
-				if (sys_relaxed(&box->stop))
-					c = 2;
-				else if (r != last)
-					c = 1, last = r;
-				else if (__builtin_amdgcn_s_memrealtime() - t0 > idle)
-					c = 2;
-				else
-					__builtin_amdgcn_s_sleep(4);
+			uint32_t c = 0, n = 0;
+			if (j == 0) {
+				// The leader polls the host mailbox.  Only one workgroup
+				// does: K pollers of one host line cost every request
+				// ~13 us at K = 16 and ~27 us at K = 32 (tools/txburst
+				// dropin, one in_cksum through a server of K workgroups).
+				while (c == 0) {
+					// relaxed: an acquire load would invalidate the caches every poll
+					const uint64_t r = sys_relaxed64(&box->req);
+					if (sys_relaxed(&box->stop))
+						c = 2;
+					else if ((uint32_t)r != last)
+						c = 1, last = (uint32_t)r, n = (uint32_t)(r >> 32);
+					else if (__builtin_amdgcn_s_memrealtime() - t0 > idle)
+						c = 2;
+					else
+						__builtin_amdgcn_s_sleep(4);
+				}
+				// relay a wide request (and the exit) to the others now;
+				// a small one after it is served (it keeps their idle
+				// bound from running out)
+				if (K > 1 && (c == 2 || burst_wgs(n, K) > 1))
+					__hip_atomic_store(dcmd, c == 2 ? (uint64_t)kBurstExit << 32 | epoch
+									: (uint64_t)last | (uint64_t)n << 32,
+							   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+			} else {
+				// The others poll the leader's relay in device memory, with
+				// a bound of their own (four idle periods) in case it never
+				// comes.
+				while (c == 0) {
+					const uint64_t r = relay_load(dcmd);
+					if ((uint32_t)(r >> 32) == kBurstExit) {
+						if ((uint32_t)r == epoch)
+							c = 2;
+						else
+							__builtin_amdgcn_s_sleep(2); // an earlier launch's
+					} else if ((uint32_t)r != last && (uint32_t)r != 0)
+						c = 1, last = (uint32_t)r, n = (uint32_t)(r >> 32);
+					else if (__builtin_amdgcn_s_memrealtime() - t0 > 4 * idle)
+						c = 2;
+					else
+						__builtin_amdgcn_s_sleep(2);
+				}
 			}
+			// A relaunch after a drain re-posts the pending request; a
+			// slice the previous launch already served is not served
+			// twice (an in-place store is not idempotent without
+			// ZERO_FIELDS).
+			if (c == 1 && first && sys_relaxed(&box->done[j]) == last)
+				c = 3;
+			if (c == 1)
+				first = false;
 			cmd = c;
+			cmd_n = n;
 		}
 		__syncthreads();
 		if (cmd == 2)
 			break;
-		// One system-scope acquire (no line of an earlier request, or of an
-		// earlier burst in a registered ring, is served from the cache), then
-		// the first kBurstFirst bytes of the block in one round trip: plain
-		// 16-byte loads, so every wave's read leaves as whole-line requests.
+		const uint32_t n = cmd_n;
+		const uint32_t W = burst_wgs(n, K);
+		if (j >= W || cmd == 3) {
+			__syncthreads(); // cmd / cmd_n are rewritten by the next poll
+			continue;
+		}
+		// One system-scope acquire: no line of an earlier request, or of an
+		// earlier burst in a registered ring, is served from the cache.
 		__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-		constexpr int W = kBurstFirst / 16 / 256;
-		uint4 v[W];
+		bool ok;
+		if (W == 1) {
+			// the first kBurstFirst bytes of the block in one round trip:
+			// plain 16-byte loads, so every wave's read leaves as whole-line
+			// requests
+			constexpr int NW = kBurstFirst / 16 / 256;
+			uint4 v[NW];
 #pragma unroll
-		for (int w = 0; w < W; ++w)
-			v[w] = src[w * 256 + t];
+			for (int w = 0; w < NW; ++w)
+				v[w] = src[w * 256 + t];
 #pragma unroll
-		for (int w = 0; w < W; ++w)
-			dst[w * 256 + t] = v[w];
-		if (t < 4)
-			hdr_w[t] = v[0];
-		__syncthreads();
-		const BurstReq &h = *reinterpret_cast<const BurstReq *>(hdr_w);
-		// The block is host-written: a header or descriptor that does not fit
-		// the block the context allocated is refused (counted in bad_req, the
-		// host's call fails) instead of steering the loads below out of it.
-		bool ok = h.n <= max_pkts && h.bytes <= cap && h.d_off >= sizeof(BurstReq) &&
-			  (uint64_t)h.d_off + 12ull * h.n <= h.bytes && (h.base || h.p_off <= h.bytes);
-		const uint32_t chunks = ok ? (h.bytes + 15) / 16 : 0;
-		// the rest of a larger block, 16 loads in flight per thread (64 KiB a
-		// round trip)
-		for (uint32_t at = kBurstFirst / 16; at < chunks; at += 16 * 256) {
-			uint4 x[16];
+			for (int w = 0; w < NW; ++w)
+				dst[w * 256 + t] = v[w];
+			if (t < 4)
+				hdr_w[t] = v[0];
+			__syncthreads();
+			const BurstReq &h = *reinterpret_cast<const BurstReq *>(hdr_w);
+			// The block is host-written: a header or descriptor that does not
+			// fit the block the context allocated is refused (counted in
+			// bad_req, the host's call fails) instead of steering the loads
+			// below out of it.
+			ok = h.n == n && h.n <= max_pkts && h.bytes <= cap && h.d_off == sizeof(BurstReq) &&
+			     (uint64_t)h.d_off + 12ull * h.n <= h.bytes && (h.base || h.p_off <= h.bytes);
+			const uint32_t chunks = ok ? (h.bytes + 15) / 16 : 0;
+			// the rest of a larger block, 16 loads in flight per thread (64 KiB
+			// a round trip)
+			for (uint32_t at = kBurstFirst / 16; at < chunks; at += 16 * 256) {
+				uint4 x[16];
 #pragma unroll
-			for (int k = 0; k < 16; ++k) {
-				const uint32_t i = at + k * 256 + t;
-				x[k] = i < chunks ? src[i] : make_uint4(0, 0, 0, 0);
+				for (int k = 0; k < 16; ++k) {
+					const uint32_t i = at + k * 256 + t;
+					x[k] = i < chunks ? src[i] : make_uint4(0, 0, 0, 0);
+				}
+#pragma unroll
+				for (int k = 0; k < 16; ++k) {
+					const uint32_t i = at + k * 256 + t;
+					if (i < chunks)
+						dst[i] = x[k];
+				}
 			}
+		} else {
+			// header and this workgroup's descriptors [lo, hi) in one round
+			// trip, as dwords (a slice starts on a 4-byte boundary); the
+			// count comes from the poll, so the slice does not wait for the
+			// header
+			const uint32_t lo = (uint32_t)((uint64_t)n * j / W), hi = (uint32_t)((uint64_t)n * (j + 1) / W);
+			const uint32_t nd = (n <= max_pkts ? 3 * (hi - lo) : 0);
+			const uint32_t *sd = reinterpret_cast<const uint32_t *>(req + sizeof(BurstReq)) + 3 * lo;
+			uint32_t *dd = reinterpret_cast<uint32_t *>(scratch + sizeof(BurstReq)) + 3 * lo;
+			uint4 hv = t < 4 ? src[t] : make_uint4(0, 0, 0, 0);
+			for (uint32_t i = t; i < nd; i += 4 * 256) {
+				uint32_t x[4];
 #pragma unroll
-			for (int k = 0; k < 16; ++k) {
-				const uint32_t i = at + k * 256 + t;
-				if (i < chunks)
-					dst[i] = x[k];
+				for (int k = 0; k < 4; ++k)
+					x[k] = i + k * 256 < nd ? sd[i + k * 256] : 0u;
+#pragma unroll
+				for (int k = 0; k < 4; ++k)
+					if (i + k * 256 < nd)
+						dd[i + k * 256] = x[k];
 			}
+			if (t < 4)
+				hdr_w[t] = hv;
+			__syncthreads();
+			const BurstReq &h = *reinterpret_cast<const BurstReq *>(hdr_w);
+			ok = h.n == n && h.n <= max_pkts && h.bytes <= cap && h.d_off == sizeof(BurstReq) &&
+			     (uint64_t)h.d_off + 12ull * h.n <= h.bytes && (h.base || h.p_off <= h.bytes);
 		}
 		// scratch stores visible to the workgroup (its waves share one CU's
 		// L1: workgroup scope)
 		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
 		__syncthreads();
 		__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+		const BurstReq &h = *reinterpret_cast<const BurstReq *>(hdr_w);
+		const uint32_t lo = W == 1 ? 0u : (uint32_t)((uint64_t)n * j / W);
+		const uint32_t hi = W == 1 ? n : (uint32_t)((uint64_t)n * (j + 1) / W);
 		if (ok && !h.base) // packet bytes in the block: every descriptor inside it
-			for (uint32_t i = t; i < h.n; i += 256) {
+			for (uint32_t i = lo + t; i < hi; i += 256) {
 				const cgck_desc_t *d = reinterpret_cast<const cgck_desc_t *>(scratch + h.d_off) + i;
 				uint32_t fo_lo, fo_hi, w2;
 				__builtin_memcpy(&fo_lo, reinterpret_cast<const uint8_t *>(d), 4);
@@ -314,33 +448,41 @@ __global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const 
 			}
 		ok = __syncthreads_and(ok);
 		if (ok) {
-			const KParams p = {h.base ? reinterpret_cast<const uint8_t *>(h.base) : scratch + h.p_off,
-					   reinterpret_cast<const cgck_desc_t *>(scratch + h.d_off),
-					   h.n, 0, 0, 0, h.flags, out, verdict, nullptr, 0, zero};
-			if (h.max_len <= 80)
-				cksum_body<4, 2, 4, true, false>(p);
-			else
-				cksum_body<16, 6, 4, true, false>(p);
+			// W == 1 reads staged packet bytes from its scratch copy; wider
+			// requests read them from the block in host memory
+			const uint8_t *base = h.base ? reinterpret_cast<const uint8_t *>(h.base)
+					      : (W == 1 ? scratch : req) + h.p_off;
+			burst_body(h, scratch, lo, hi, reinterpret_cast<uint32_t *>(resp),
+				   reinterpret_cast<uint32_t *>(resp + burst_meta_off(n)), resp + burst_ver_off(n), zero,
+				   base);
 		} else if (t == 0) {
 			__hip_atomic_fetch_add(&box->bad_req, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 		}
 		// every thread's outputs (and in-place stores) written back to host
-		// memory before thread 0 publishes seq_done: a system-scope release per
+		// memory before thread 0 publishes done[j]: a system-scope release per
 		// thread (one fence per request, noise next to the ~5 us round trip)
 		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
 		__syncthreads();
-		if (t == 0)
-			__hip_atomic_store(&box->seq_done, last, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+		if (t == 0) {
+			__hip_atomic_store(&box->done[j], last, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+			if (j == 0 && K > 1 && W == 1)
+				__hip_atomic_store(dcmd, (uint64_t)last | (uint64_t)n << 32, __ATOMIC_RELAXED,
+						   __HIP_MEMORY_SCOPE_SYSTEM);
+		}
 	}
 	if (t == 0)
-		__hip_atomic_store(&box->alive, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+		__hip_atomic_store(&box->alive[j], (uint8_t)0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-hipError_t launch_burst_server(BurstBox *box, const uint8_t *req, uint8_t *scratch, uint32_t *out, uint8_t *verdict,
-			       const void *zero, uint32_t cap, uint32_t max_pkts, hipStream_t st)
+hipError_t launch_burst_server(BurstBox *box, const uint8_t *req, uint8_t *scratch, uint8_t *resp, uint64_t *dcmd,
+			       const void *zero, uint32_t cap, uint32_t max_pkts, uint32_t wgs, uint32_t start_seq,
+			       uint32_t epoch, hipStream_t st)
 {
-	hipLaunchKernelGGL(burst_server_kernel, dim3(1), dim3(256), 0, st, box, req, scratch, out, verdict, zero, cap,
-			   max_pkts);
+	hipError_t e = hipMemsetAsync(dcmd, 0, sizeof(uint64_t), st);
+	if (e != hipSuccess)
+		return e;
+	hipLaunchKernelGGL(burst_server_kernel, dim3(wgs), dim3(256), 0, st, box, req, scratch, resp, dcmd, zero, cap,
+			   max_pkts, start_seq, epoch);
 	return hipGetLastError();
 }
 

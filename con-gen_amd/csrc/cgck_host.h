@@ -48,11 +48,12 @@ struct cgck_ctx {
 	size_t bstage_cap;
 	uint8_t *bstage_dev;        // device view of bstage
 	cgck::BurstBox *bbox_dev;   // device view of bbox
-	uint8_t *bresp;             // [out u32 x bmax | verdict u8 x bmax]
+	uint8_t *bresp;             // a request's outputs, packed by its n (burst_meta_off / burst_ver_off)
 	uint8_t *bresp_dev;
-	size_t bresp_ver;           // offset of the verdicts in bresp
 	uint8_t *bscratch;          // device: the server's copy of the block (bstage_cap bytes)
+	uint64_t *brelay;           // device, uncached: the leader's relay word
 	uint32_t bmax;              // packets per request
+	uint32_t bwgs;              // workgroups of the server (K)
 	uint32_t bbad;              // bbox->bad_req as last seen
 	uint32_t bseq;
 	hipStream_t bstream; // the server's own stream (it stays resident)
@@ -79,8 +80,9 @@ int grow_dev(void **p, size_t *cap, size_t need);
 int run(cgck_ctx *c, const KParams &p, uint32_t len_hint, hipStream_t st);
 
 // cgck_desc_host without the public flag check (internal flags allowed).
+// meta: kFlagRx's per-packet words (nullptr otherwise).
 int desc_host(cgck_ctx *c, void *base, size_t bytes, const cgck_desc_t *desc, uint64_t n, uint32_t flags,
-	      uint32_t *out, uint8_t *verdict);
+	      uint32_t *out, uint8_t *verdict, uint32_t *meta = nullptr);
 
 // Staging path of one region for the drop-in symbols (burst server when open,
 // else a launch on the context stream and a synchronisation).

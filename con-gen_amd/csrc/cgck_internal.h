@@ -29,6 +29,20 @@ constexpr uint32_t kFlagNoLenCheck = 1u << 15;
 // everything else udp_cksum with the pseudo-header (tcp_input.c:75-78,
 // udp_usrreq.c:86-89).  Group kernel only.
 constexpr uint32_t kFlagL4Auto = 1u << 14;
+// Internal flag of the RX window: descriptor ip_len is the bytes the frame
+// holds after l3_off (ip_input's `len`); the group kernel itself decides, as
+// cgck_rx_begin's host walk used to, which calls the stack can make on the
+// frame (ip_input.c:28-44, 76; tcp_input.c:67; udp_usrreq.c:65;
+// ip_icmp.c:177; gbtcp/inet.c:282-314) and covers min(ntohs(ip_len), len)
+// bytes.  Per frame it writes KParams.meta: kRxOkIp | kRxOkL4 | kRxIcmp,
+// ip_hl * 4 in bits 8-15, ntohs(ip_len) - ip_hl * 4 in bits 16-31.
+constexpr uint32_t kFlagRx = 1u << 13;
+constexpr uint32_t kRxOkIp = 1, kRxOkL4 = 2, kRxIcmp = 4;
+// Internal flag: a host-resident region bound by PCIe round trips (the
+// drop-in symbols' one region): take the group kernel, whose one block reads
+// the region at once, whatever the lane kernels' preconditions say (lpd for
+// a 20-byte in_cksum read its DMA steps over the fabric: 31 vs 14 us).
+constexpr uint32_t kFlagGroup = 1u << 12;
 
 constexpr uint32_t kImixCycleBytes = 4252; // 7*64 + 4*576 + 1500
 
@@ -49,27 +63,47 @@ struct KParams {
 	uint32_t *bad;
 	uint32_t contig; // set by the launcher: contiguous block ranges
 	const void *zero; // kZeroBytes zero bytes of device memory (safe target for clamped loads)
+	uint32_t *meta;   // kFlagRx only: one word per packet (see kFlagRx)
 };
 
 // Mailbox of the burst server (cgck_group.hip), in host-coherent pinned
-// memory: the host writes a request block (BurstReq + descriptors + packet
-// bytes) into its staging and bumps seq_req (release); the server answers
-// with seq_done (release) once the outputs are visible.
+// memory.  The host writes a request block (BurstReq + descriptors + packet
+// bytes) into its staging, then `req` = seq | n << 32 in one 64-bit release
+// store (seq never 0); the server's leader workgroup polls it and relays a
+// wide request to the others through device memory, so each learns the
+// packet count, and with it its share, from its poll.  Workgroup j of the W = burst_wgs(n, K)
+// that serve a request answers with done[j] = seq (release) once its outputs
+// are visible.
+constexpr uint32_t kBurstMaxWG = 32; // workgroups of a server (K)
+constexpr uint32_t kBurstPerWG = 64; // packets per workgroup before another one joins
 struct BurstBox {
-	uint32_t seq_req;    // host -> device: number of the pending request
-	uint32_t seq_done;   // device -> host: last request served
+	uint64_t req;        // host -> device: seq | n << 32
 	uint32_t stop;       // host -> device: exit now
-	uint32_t alive;      // host sets 1 at launch; the server clears it on exit
-	uint64_t idle_ticks; // 100 MHz ticks without a request before the server exits
 	uint32_t bad_req;    // device -> host: requests refused by the server's block check
-	uint32_t pad;
+	uint64_t idle_ticks; // 100 MHz ticks without a request before the server exits
+	uint32_t pad[10];
+	uint32_t done[kBurstMaxWG]; // device -> host: the last request workgroup j served
+	uint8_t alive[kBurstMaxWG]; // host sets 1 at launch; workgroup j clears its byte on exit
+	uint8_t pad2[64 - kBurstMaxWG];
 };
+static_assert(sizeof(BurstBox) == 128 + 4 * kBurstMaxWG, "mailbox line, the done lines, the alive line");
 
-// Header of a request block (the first 64 bytes of the burst staging).  The
-// server copies the block's first kBurstFirst bytes into device scratch with
-// one wide read — every thread's loads in flight together, one host round
-// trip for a small request's header, descriptors and packet bytes — and the
-// rest of a larger block in a second pass.
+// Workgroups that serve a request of n packets on a server of K: one up to
+// kBurstPerWG packets (it reads the whole small block in one round trip),
+// then one per kBurstPerWG packets.
+__host__ __device__ constexpr uint32_t burst_wgs(uint32_t n, uint32_t K)
+{
+	return n <= kBurstPerWG ? 1u : ((n + kBurstPerWG - 1) / kBurstPerWG < K ? (n + kBurstPerWG - 1) / kBurstPerWG : K);
+}
+
+// Header of a request block (the first 64 bytes of the burst staging), then
+// the n descriptors at d_off = 64, then (base == 0) the packet bytes.  A
+// request served by one workgroup is copied into device scratch with one wide
+// read of the block's first kBurstFirst bytes — every thread's loads in
+// flight together, one host round trip for a small request's header,
+// descriptors and packet bytes — and the rest of a larger block in a second
+// pass.  Workgroup j of a wider request reads the header and its own slice of
+// the descriptors in one round trip and the packet bytes where they lie.
 struct BurstReq {
 	uint32_t n;       // packets
 	uint32_t flags;   // CGCK_* flags
@@ -83,8 +117,18 @@ struct BurstReq {
 static_assert(sizeof(BurstReq) == 64, "one header line");
 constexpr uint32_t kBurstFirst = 8192;
 
-hipError_t launch_burst_server(BurstBox *box, const uint8_t *req, uint8_t *scratch, uint32_t *out, uint8_t *verdict,
-			       const void *zero, uint32_t cap, uint32_t max_pkts, hipStream_t st);
+// Outputs of a server request of n packets, host-coherent and packed by n
+// (not by the server's capacity), so a small request's outputs share one
+// page: [out u32 x n | meta u32 x n | verdict u8 x n], each part 64-byte
+// aligned.  (With the verdicts at a capacity-sized offset, 16 KiB away, a
+// one-packet request took 36.8 us instead of 9.5: tools/txburst dropin.)
+__host__ __device__ constexpr uint32_t burst_meta_off(uint32_t n) { return (4 * n + 63) & ~63u; }
+__host__ __device__ constexpr uint32_t burst_ver_off(uint32_t n) { return 2 * burst_meta_off(n); }
+// dcmd: 8 bytes of device memory, the leader's relay word (zeroed here on
+// the launch stream before the launch); epoch: nonzero, new for every launch.
+hipError_t launch_burst_server(BurstBox *box, const uint8_t *req, uint8_t *scratch, uint8_t *resp, uint64_t *dcmd,
+			       const void *zero, uint32_t cap, uint32_t max_pkts, uint32_t wgs, uint32_t start_seq,
+			       uint32_t epoch, hipStream_t st);
 
 // Kernel selection flags (see cgck_dispatch.cpp) and the measured defaults
 // (tools/sweep.py; profiles/r01).  The group kernel streams whole lines per

@@ -397,15 +397,58 @@ def test_burst_server_desc_host(engine, port, registered):
         engine.burst_close()
 
 
+@pytest.mark.parametrize("max_len", [80, 600])
+@pytest.mark.parametrize("registered", [False, True])
+def test_burst_server_wide(engine, port, registered, max_len):
+    """Requests split over the server's workgroups (burst_wgs: one per 64
+    packets, up to 32): slice edges at 64 / 65 / 130 / 2047 / 2048 / 4096
+    packets, staged or in place, generate / fill / verify, against the
+    referee; a second server with 2 workgroups (max_pkts 128) takes uneven
+    slices of the same batches."""
+    L = cgck.load()
+    for max_pkts, sizes in ((4096, (64, 65, 130, 2047, 2048, 4096)), (128, (65, 127, 128))):
+        engine.burst_open(max_pkts=max_pkts, max_bytes=4 << 20)
+        try:
+            for npk in sizes:
+                rng = np.random.default_rng(77 + npk + max_len)
+                buf, desc = random_batch(rng, npk, max_len)
+                ring = None
+                if registered:
+                    size = (len(buf) + 4095) // 4096 * 4096
+                    raw = np.zeros(size + 4096, np.uint8)
+                    off = (-raw.ctypes.data) % 4096
+                    ring = raw[off:off + size]
+                    assert L.cgck_host_register(ring.ctypes.data, size) == 0
+                try:
+                    for flags in (cgck.GEN_BOTH, cgck.FILL_BOTH, cgck.VERIFY_BSD):
+                        ref = buf.copy()
+                        exp, ever = port.batch_desc(ref, desc.view(np.uint8), len(desc), flags)
+                        if registered:
+                            ring[:len(buf)] = buf
+                            got = ring[:len(buf)]
+                        else:
+                            got = buf.copy()
+                        out = np.zeros(len(desc), np.uint32)
+                        ver = np.zeros(len(desc), np.uint8)
+                        engine.desc_host(got, desc, flags, out, ver)
+                        assert np.array_equal(out, exp) and np.array_equal(ver, ever), (max_pkts, npk, flags)
+                        assert np.array_equal(got, ref), (max_pkts, npk, flags)
+                finally:
+                    if registered:
+                        L.cgck_host_unregister(ring.ctypes.data)
+        finally:
+            engine.burst_close()
+
+
 def test_burst_server_idle_relaunch(engine, port):
     """The server exits after idle_ms without a request and the next request
     relaunches it; close is idempotent."""
     import time
     engine.burst_open(max_pkts=256, max_bytes=1 << 20, idle_ms=20)
     try:
-        for rep in range(3):
+        for rep in range(4):
             rng = np.random.default_rng(41 + rep)
-            buf, desc = random_batch(rng, 64, 1500)
+            buf, desc = random_batch(rng, 64 if rep % 2 == 0 else 256, 1500)   # one / four workgroups
             exp, ever = port.batch_desc(buf.copy(), desc.view(np.uint8), len(desc), cgck.VERIFY_BSD)
             out, ver = np.zeros(len(desc), np.uint32), np.zeros(len(desc), np.uint8)
             engine.desc_host(buf.copy(), desc, cgck.VERIFY_BSD, out, ver)

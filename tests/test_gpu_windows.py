@@ -81,6 +81,39 @@ def test_rx_window_replay(port, clean, registered):
             L.cgck_host_unregister(ring.ctypes.data)
 
 
+@pytest.mark.parametrize("nframes", [40, 400, 2500])
+def test_rx_window_replay_server(port, nframes):
+    """The same replay with this thread's burst server open: the window's
+    burst is one server request, served by one workgroup (40 frames) or split
+    over 7 / 32 of them, staged (pageable ring) and in place (registered)."""
+    rng = np.random.default_rng(211 + nframes)
+    frames = rxcorpus.corpus(rng, referee(port), nframes, clean=False)
+    buf, desc = rxcorpus.ring(frames)
+    L = cgck.load()
+    cgck.burst_open(max_pkts=4096, max_bytes=8 << 20)
+    try:
+        for registered in (False, True):
+            ring = None
+            if registered:
+                raw, ring, size = rxcorpus.registered_copy(buf)
+                assert L.cgck_host_register(ring.ctypes.data, size) == 0
+            try:
+                for stack, ip_in, tcp_in in FLAGS[::2]:
+                    (a, ref), (b, got), m, served, d = replay_pair(port, buf, desc, stack, ip_in, tcp_in, ring)
+                    cell = (registered, stack, ip_in, tcp_in)
+                    assert np.array_equal(a[0], b[0]), (cell, np.nonzero(a[0] != b[0])[0][:8])
+                    assert np.array_equal(a[1], b[1]), (cell, a[1], b[1])
+                    assert np.array_equal(ref, got), cell
+                    calls = int(b[1][4] + b[1][5])
+                    assert served == d[0] and served + d[1] == calls, (cell, served, d, calls)
+                    assert served >= 0.9 * calls, (cell, served, calls)
+            finally:
+                if registered:
+                    L.cgck_host_unregister(ring.ctypes.data)
+    finally:
+        cgck.burst_close()
+
+
 def test_rx_window_fixture_frames(port, golden_verify):
     """The reference-made verify fixtures (tests/golden/verify.json) as one
     burst: verdicts through the window equal the fixtures' own."""

@@ -32,6 +32,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
 #include <time.h>
 
 #include "cgck.h"
@@ -86,7 +87,18 @@ int main(int argc, char **argv)
 	const int lens[] = {1500, 576, 64};
 	const int nl = (int)(sizeof(lens) / sizeof(lens[0]));
 	const int maxb = 2048, maxit = 100000;
-	uint8_t *ring = aligned_alloc(4096, (size_t)maxb * SLOT);
+	/* TXBURST_HUGE=1: the ring on transparent huge pages (2 MiB), as a DPDK
+	 * mempool or a huge-page XDP UMEM would be; otherwise 4 KiB pages */
+	uint8_t *ring;
+	if (getenv("TXBURST_HUGE") && atoi(getenv("TXBURST_HUGE"))) {
+		const size_t sz = (size_t)maxb * SLOT, al = 2u << 20;
+		uint8_t *m = mmap(NULL, sz + al, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+		ring = m == MAP_FAILED ? NULL : (uint8_t *)(((uintptr_t)m + al - 1) & ~(uintptr_t)(al - 1));
+		if (ring)
+			madvise(ring, sz, MADV_HUGEPAGE);
+	} else {
+		ring = aligned_alloc(4096, (size_t)maxb * SLOT);
+	}
 	cgck_desc_t *desc = malloc(sizeof(cgck_desc_t) * maxb);
 	uint32_t *out = malloc(4 * maxb);
 	uint8_t *ver = malloc(maxb);
@@ -96,6 +108,45 @@ int main(int argc, char **argv)
 	if (!ring || !desc || !out || !ver || !t || !tc || cgck_ctx_create(0, &ctx)) {
 		fprintf(stderr, "txburst: setup failed: %s\n", cgck_last_error());
 		return 1;
+	}
+	if (argc > 2 && !strcmp(argv[2], "dropin")) {
+		/* drop-in latency alone: launch path, server of 1 and of 32
+		 * workgroups, launch path again after they closed */
+		memset(ring, 0, SLOT);
+		uint64_t s0 = 1;
+		make_packet(ring + L3, 64, &s0);
+		/* (max_pkts, max_bytes) of the server; 0: the launch path */
+		uint32_t caps[16] = {0, 64, 64, 2048, 2048, 0};
+		size_t bytes[16] = {0, 64 << 10, 3 << 20, 64 << 10, 3 << 20, 0};
+		int nm = 6;
+		if (argc > 3) { /* txburst budget dropin max_pkts[:max_bytes] ... (0: launch path) */
+			nm = 0;
+			for (int a = 3; a < argc && nm < 16; a++, nm++) {
+				char *colon;
+				caps[nm] = (uint32_t)strtoul(argv[a], &colon, 0);
+				bytes[nm] = *colon == ':' ? (size_t)strtoull(colon + 1, NULL, 0) : (size_t)caps[nm] * 1536;
+			}
+		}
+		for (int m = 0; m < nm; m++) {
+			if (caps[m] && cgck_burst_open(NULL, caps[m], bytes[m], 0)) {
+				fprintf(stderr, "txburst: burst_open failed: %s\n", cgck_last_error());
+				return 1;
+			}
+			int it = 0;
+			double t0 = now();
+			while (it < maxit && now() - t0 < budget) {
+				double a = now();
+				volatile uint16_t v = in_cksum(ring + L3, 20);
+				(void)v;
+				t[it++] = now() - a;
+			}
+			printf("{\"mode\": \"in_cksum\", \"max_pkts\": %u, \"max_bytes\": %zu, \"iters\": %d, "
+			       "\"us_median\": %.2f}\n", caps[m], bytes[m], it, median(t, it) * 1e6);
+			fflush(stdout);
+			if (caps[m])
+				cgck_burst_close(NULL);
+		}
+		return 0;
 	}
 	for (int li = 0; li < nl; li++) {
 		const int len = lens[li];
