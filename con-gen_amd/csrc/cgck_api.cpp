@@ -311,6 +311,10 @@ static double now_s()
 
 // (Re)launch the server's K workgroups; the first request each serves is
 // the one after start_seq.
+#if CGCK_LAB
+static thread_local uint64_t t_lab_host[2]; // cgck_lab_burst_times
+#endif
+
 // Server launches in this process: a relay word left by one launch (in
 // device memory a later server may get again) never matches another's tag.
 static std::atomic<uint32_t> g_burst_epoch{0};
@@ -324,7 +328,7 @@ static int burst_launch(cgck_ctx *c, uint32_t start_seq)
 		__atomic_store_n(&c->bbox->alive[j], (uint8_t)1, __ATOMIC_RELEASE);
 	hipError_t e = launch_burst_server(c->bbox_dev, c->bstage_dev, c->bscratch, c->bresp_dev, c->brelay,
 					   c->d_zero, (uint32_t)c->bstage_cap,
-					   c->bmax, c->bwgs, start_seq, epoch, c->bstream);
+					   c->bmax, c->bwgs, c->bper, start_seq, epoch, c->bstream);
 	if (e != hipSuccess) {
 		for (uint32_t j = 0; j < c->bwgs; j++)
 			__atomic_store_n(&c->bbox->alive[j], (uint8_t)0, __ATOMIC_RELEASE);
@@ -357,7 +361,7 @@ static int burst_restart(cgck_ctx *c, uint32_t start_seq)
 // A request costs the poll, the round trips of the request block and the
 // packet bytes, and the outputs' write acknowledgements (~5 us for a small
 // one, tools/pingpong) instead of a launch and a stream synchronisation
-// (~9.4 us for an empty kernel).  Up to kBurstPerWG packets one workgroup
+// (~9.4 us for an empty kernel).  Up to kBurstOneWG packets one workgroup
 // serves it from one wide read of the block; larger requests are split over
 // up to K workgroups, each reading its slice of the descriptors and the
 // packet bytes where they lie, so the host reads spread over CUs as a
@@ -417,13 +421,16 @@ static int burst_serve(cgck_ctx *c, const uint8_t *base_dev, uint64_t n, uint32_
 	if (++c->bseq == 0) // seq 0 is the relay word's "nothing posted"
 		++c->bseq;
 	const uint32_t seq = c->bseq;
+#if CGCK_LAB
+	t_lab_host[0] = (uint64_t)(now_s() * 1e9);
+#endif
 	__atomic_store_n(&b->req, (uint64_t)seq | (uint64_t)n << 32, __ATOMIC_RELEASE);
 	if (!burst_all_alive(c)) {
 		int rc = burst_restart(c, seq - 1); // idled out: a new server picks the request up
 		if (rc)
 			return rc;
 	}
-	const uint32_t W = burst_wgs((uint32_t)n, c->bwgs);
+	const uint32_t W = burst_wgs((uint32_t)n, c->bwgs, c->bper);
 	const double t0 = now_s();
 	uint32_t spin = 0;
 	for (uint32_t j = 0; j < W;) {
@@ -463,6 +470,9 @@ static int burst_serve(cgck_ctx *c, const uint8_t *base_dev, uint64_t n, uint32_
 				       seq, (unsigned long long)n, W, miss, (unsigned long long)relay);
 		}
 	}
+#if CGCK_LAB
+	t_lab_host[1] = (uint64_t)(now_s() * 1e9);
+#endif
 	const uint32_t bad = __atomic_load_n(&b->bad_req, __ATOMIC_ACQUIRE);
 	if (bad != c->bbad) {
 		c->bbad = bad;
@@ -836,7 +846,10 @@ extern "C" int cgck_burst_open(cgck_ctx_t *c, uint32_t max_pkts, size_t max_byte
 	c->bbox = (BurstBox *)box;
 	// one workgroup per kBurstPerWG packets of the largest request, at most
 	// kBurstMaxWG (and the device's CUs)
-	c->bwgs = burst_wgs(max_pkts, kBurstMaxWG);
+	c->bper = kBurstPerWG;
+	if (const char *e = CGCK_ENV("CGCK_SERVER_PER_WG")) // lab A/B: packets per workgroup
+		c->bper = atoi(e) > 0 ? (uint32_t)atoi(e) : c->bper;
+	c->bwgs = burst_wgs(max_pkts, kBurstMaxWG, c->bper);
 	if (c->bwgs > (uint32_t)c->num_cus)
 		c->bwgs = (uint32_t)c->num_cus;
 	if (const char *e = CGCK_ENV("CGCK_SERVER_WGS")) // lab A/B: K
@@ -855,6 +868,22 @@ extern "C" int cgck_burst_open(cgck_ctx_t *c, uint32_t max_pkts, size_t max_byte
 	c->bbad = 0;
 	return burst_launch(c, 0);
 }
+
+#if CGCK_LAB
+// Lab: workgroup 0's timestamps of the last request (100 MHz ticks: seen,
+// block read, computed, published) and the host's view of that request
+// (ns: post, done seen) for tools/srvlat.c.
+extern "C" int cgck_lab_burst_times(cgck_ctx_t *c, uint64_t dev[4], uint64_t host[2])
+{
+	if (!c || !c->bbox)
+		return -EINVAL;
+	for (int i = 0; i < 4; i++)
+		dev[i] = __atomic_load_n(&c->bbox->lab_t[i], __ATOMIC_ACQUIRE);
+	host[0] = t_lab_host[0];
+	host[1] = t_lab_host[1];
+	return 0;
+}
+#endif
 
 extern "C" int cgck_burst_close(cgck_ctx_t *c)
 {

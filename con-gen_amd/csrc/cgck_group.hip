@@ -216,7 +216,7 @@ __global__ __launch_bounds__(256) void cksum_kernel(KParams p)
 // (BurstReq, descriptors, packet bytes) into host-coherent staging and stores
 // req = seq | n << 32; thread 0 of every workgroup polls it with relaxed
 // system-scope loads.  W = burst_wgs(n, K) workgroups serve the request:
-//  * W == 1 (up to kBurstPerWG packets: a drop-in call, a small burst):
+//  * W == 1 (up to kBurstOneWG packets: a drop-in call, a small burst):
 //    workgroup 0 copies the block into device scratch with one wide read
 //    (tools/pingpong: every dependent host round trip costs ~1.3 us, so the
 //    block is fetched at once instead of header -> descriptor -> packet
@@ -279,8 +279,8 @@ __device__ __forceinline__ uint64_t relay_load(const uint64_t *p)
 
 __global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const uint8_t *req, uint8_t *scratch,
 							   uint8_t *resp, uint64_t *dcmd, const void *zero,
-							   uint32_t cap, uint32_t max_pkts, uint32_t start_seq,
-							   uint32_t epoch)
+							   uint32_t cap, uint32_t max_pkts, uint32_t per_wg,
+							   uint32_t start_seq, uint32_t epoch)
 {
 	__shared__ uint32_t cmd, cmd_n; // cmd: 1 run the pending request, 2 exit, 3 already served
 	__shared__ uint4 hdr_w[4];
@@ -315,7 +315,7 @@ __global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const 
 				// relay a wide request (and the exit) to the others now;
 				// a small one after it is served (it keeps their idle
 				// bound from running out)
-				if (K > 1 && (c == 2 || burst_wgs(n, K) > 1))
+				if (K > 1 && (c == 2 || burst_wgs(n, K, per_wg) > 1))
 					__hip_atomic_store(dcmd, c == 2 ? (uint64_t)kBurstExit << 32 | epoch
 									: (uint64_t)last | (uint64_t)n << 32,
 							   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -353,11 +353,14 @@ __global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const 
 		if (cmd == 2)
 			break;
 		const uint32_t n = cmd_n;
-		const uint32_t W = burst_wgs(n, K);
+		const uint32_t W = burst_wgs(n, K, per_wg);
 		if (j >= W || cmd == 3) {
 			__syncthreads(); // cmd / cmd_n are rewritten by the next poll
 			continue;
 		}
+#if CGCK_LAB
+		uint64_t lab_t0 = __builtin_amdgcn_s_memrealtime(), lab_t1 = 0, lab_t2 = 0;
+#endif
 		// One system-scope acquire: no line of an earlier request, or of an
 		// earlier burst in a registered ring, is served from the cache.
 		__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
@@ -447,6 +450,9 @@ __global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const 
 				ok = ok && fo_hi == 0 && end + h.p_off <= h.bytes;
 			}
 		ok = __syncthreads_and(ok);
+#if CGCK_LAB
+		lab_t1 = __builtin_amdgcn_s_memrealtime();
+#endif
 		if (ok) {
 			// W == 1 reads staged packet bytes from its scratch copy; wider
 			// requests read them from the block in host memory
@@ -458,11 +464,24 @@ __global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const 
 		} else if (t == 0) {
 			__hip_atomic_fetch_add(&box->bad_req, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 		}
+#if CGCK_LAB
+		__syncthreads();
+		lab_t2 = __builtin_amdgcn_s_memrealtime();
+#endif
 		// every thread's outputs (and in-place stores) written back to host
 		// memory before thread 0 publishes done[j]: a system-scope release per
 		// thread (one fence per request, noise next to the ~5 us round trip)
 		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
 		__syncthreads();
+#if CGCK_LAB
+		if (t == 0 && j == 0) {
+			const uint64_t lab_t3 = __builtin_amdgcn_s_memrealtime();
+			__hip_atomic_store(&box->lab_t[0], lab_t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+			__hip_atomic_store(&box->lab_t[1], lab_t1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+			__hip_atomic_store(&box->lab_t[2], lab_t2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+			__hip_atomic_store(&box->lab_t[3], lab_t3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+		}
+#endif
 		if (t == 0) {
 			__hip_atomic_store(&box->done[j], last, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 			if (j == 0 && K > 1 && W == 1)
@@ -475,14 +494,14 @@ __global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const 
 }
 
 hipError_t launch_burst_server(BurstBox *box, const uint8_t *req, uint8_t *scratch, uint8_t *resp, uint64_t *dcmd,
-			       const void *zero, uint32_t cap, uint32_t max_pkts, uint32_t wgs, uint32_t start_seq,
-			       uint32_t epoch, hipStream_t st)
+			       const void *zero, uint32_t cap, uint32_t max_pkts, uint32_t wgs, uint32_t per_wg,
+			       uint32_t start_seq, uint32_t epoch, hipStream_t st)
 {
 	hipError_t e = hipMemsetAsync(dcmd, 0, sizeof(uint64_t), st);
 	if (e != hipSuccess)
 		return e;
 	hipLaunchKernelGGL(burst_server_kernel, dim3(wgs), dim3(256), 0, st, box, req, scratch, resp, dcmd, zero, cap,
-			   max_pkts, start_seq, epoch);
+			   max_pkts, per_wg, start_seq, epoch);
 	return hipGetLastError();
 }
 

@@ -54,6 +54,7 @@ struct cgck_ctx {
 	uint64_t *brelay;           // device, uncached: the leader's relay word
 	uint32_t bmax;              // packets per request
 	uint32_t bwgs;              // workgroups of the server (K)
+	uint32_t bper;              // packets per workgroup of a wide request
 	uint32_t bbad;              // bbox->bad_req as last seen
 	uint32_t bseq;
 	hipStream_t bstream; // the server's own stream (it stays resident)

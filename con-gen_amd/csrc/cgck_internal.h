@@ -75,25 +75,30 @@ struct KParams {
 // that serve a request answers with done[j] = seq (release) once its outputs
 // are visible.
 constexpr uint32_t kBurstMaxWG = 32; // workgroups of a server (K)
-constexpr uint32_t kBurstPerWG = 64; // packets per workgroup before another one joins
+constexpr uint32_t kBurstOneWG = 64; // packets one workgroup serves alone (one wide read of the block)
+constexpr uint32_t kBurstPerWG = 64; // packets per workgroup of a wider request (default)
 struct BurstBox {
 	uint64_t req;        // host -> device: seq | n << 32
 	uint32_t stop;       // host -> device: exit now
 	uint32_t bad_req;    // device -> host: requests refused by the server's block check
 	uint64_t idle_ticks; // 100 MHz ticks without a request before the server exits
-	uint32_t pad[10];
+	uint32_t pad[2];
+	uint64_t lab_t[4];   // lab build: workgroup 0's s_memrealtime at seen / read / computed / published
 	uint32_t done[kBurstMaxWG]; // device -> host: the last request workgroup j served
 	uint8_t alive[kBurstMaxWG]; // host sets 1 at launch; workgroup j clears its byte on exit
-	uint8_t pad2[64 - kBurstMaxWG];
 };
-static_assert(sizeof(BurstBox) == 128 + 4 * kBurstMaxWG, "mailbox line, the done lines, the alive line");
+static_assert(sizeof(BurstBox) == 64 + 5 * kBurstMaxWG, "mailbox line, the done lines, the alive lines");
 
-// Workgroups that serve a request of n packets on a server of K: one up to
-// kBurstPerWG packets (it reads the whole small block in one round trip),
-// then one per kBurstPerWG packets.
-__host__ __device__ constexpr uint32_t burst_wgs(uint32_t n, uint32_t K)
+// Workgroups that serve a request of n packets on a server of K with `per`
+// packets per workgroup: one up to kBurstOneWG packets (it reads the whole
+// small block in one round trip), then one per `per` packets, at most K.
+// A wide request's packet reads over the fabric are bound by the device's
+// aggregate host-read rate, not by one CU: 2048 x 64 B in place took 25.3 /
+// 31.2 / 44.4 / 43.9 us at 64 / 32 / 16 / 8 packets per workgroup
+// (tools/srvlat, profiles/r03/burst/srvlat_per_wg.log), so 64 it is.
+__host__ __device__ constexpr uint32_t burst_wgs(uint32_t n, uint32_t K, uint32_t per)
 {
-	return n <= kBurstPerWG ? 1u : ((n + kBurstPerWG - 1) / kBurstPerWG < K ? (n + kBurstPerWG - 1) / kBurstPerWG : K);
+	return n <= kBurstOneWG ? 1u : ((n + per - 1) / per < K ? (n + per - 1) / per : K);
 }
 
 // Header of a request block (the first 64 bytes of the burst staging), then
@@ -127,8 +132,8 @@ __host__ __device__ constexpr uint32_t burst_ver_off(uint32_t n) { return 2 * bu
 // dcmd: 8 bytes of device memory, the leader's relay word (zeroed here on
 // the launch stream before the launch); epoch: nonzero, new for every launch.
 hipError_t launch_burst_server(BurstBox *box, const uint8_t *req, uint8_t *scratch, uint8_t *resp, uint64_t *dcmd,
-			       const void *zero, uint32_t cap, uint32_t max_pkts, uint32_t wgs, uint32_t start_seq,
-			       uint32_t epoch, hipStream_t st);
+			       const void *zero, uint32_t cap, uint32_t max_pkts, uint32_t wgs, uint32_t per_wg,
+			       uint32_t start_seq, uint32_t epoch, hipStream_t st);
 
 // Kernel selection flags (see cgck_dispatch.cpp) and the measured defaults
 // (tools/sweep.py; profiles/r01).  The group kernel streams whole lines per
