@@ -364,18 +364,20 @@ static int burst_restart(cgck_ctx *c, uint32_t start_seq)
 // (~9.4 us for an empty kernel).  Up to kBurstOneWG packets one workgroup
 // serves it from one wide read of the block; larger requests are split over
 // up to K workgroups, each reading its slice of the descriptors and the
-// packet bytes where they lie, so the host reads spread over CUs as a
-// launch's do.  Registered packets are copied into the block up to 32 KiB of
-// block (one read for a small request) and read in place above.  TX flushes
-// (mixed 20 B / full-size entries) keep the launch path.  The caps:
-// kServerBytes of packet bytes per request (above it the launch path's many
-// workgroups read the fabric faster).  $CGCK_SERVER_PKTS / _BYTES / _COPY
-// override the caps for A/B runs (lab build).
+// packet bytes where they lie.  Registered packets are copied into the block
+// up to 32 KiB of block (one read for a small request) and read in place
+// above.  TX flushes (mixed 20 B / full-size entries) keep the launch path.
+// Which requests go to the server is the caller's choice at open:
+// cgck_burst_open's max_pkts and max_bytes (packet bytes per request).  The
+// launch path's many workgroups read the fabric faster for hundreds of
+// frames of >= 576 B (256 x 576 B: 22.8 vs 29.2 us), the server wins below
+// ~100 KiB of packet bytes (profiles/r03/burst), so max_bytes ~96 KiB routes
+// a mixed workload best; the bench opens it wide and reports both paths.
+// $CGCK_SERVER_PKTS / _COPY override the caps for A/B runs (lab build).
 static size_t env_size(const char *v, size_t dflt)
 {
 	return v && *v ? (size_t)strtoull(v, nullptr, 0) : dflt;
 }
-static const size_t kServerBytes = env_size(CGCK_ENV("CGCK_SERVER_BYTES"), 4 << 20);
 static const uint64_t kServerPkts = env_size(CGCK_ENV("CGCK_SERVER_PKTS"), 1u << 20);
 static const size_t kServerCopy = env_size(CGCK_ENV("CGCK_SERVER_COPY"), 32 << 10);
 
@@ -401,7 +403,7 @@ static bool burst_fits(const cgck_ctx *c, uint64_t n, uint32_t max_len, size_t s
 {
 	(void)max_len;
 	return c->bbox && n <= c->bmax && n <= kServerPkts && burst_layout(staged, n).bytes <= c->bstage_cap &&
-	       data <= kServerBytes;
+	       data <= c->bmax_bytes;
 }
 
 // Serve the request whose descriptors (and, for base_dev == nullptr, packet
@@ -864,6 +866,7 @@ extern "C" int cgck_burst_open(cgck_ctx_t *c, uint32_t max_pkts, size_t max_byte
 	c->bscratch = (uint8_t *)sc;
 	c->brelay = (uint64_t *)rl;
 	c->bmax = max_pkts;
+	c->bmax_bytes = max_bytes;
 	c->bseq = 0;
 	c->bbad = 0;
 	return burst_launch(c, 0);

@@ -53,6 +53,7 @@ struct cgck_ctx {
 	uint8_t *bscratch;          // device: the server's copy of the block (bstage_cap bytes)
 	uint64_t *brelay;           // device, uncached: the leader's relay word
 	uint32_t bmax;              // packets per request
+	size_t bmax_bytes;          // packet bytes per request (cgck_burst_open's max_bytes)
 	uint32_t bwgs;              // workgroups of the server (K)
 	uint32_t bper;              // packets per workgroup of a wide request
 	uint32_t bbad;              // bbox->bad_req as last seen

@@ -225,14 +225,18 @@ int cgck_tx_flush(void);
  * calls inside a TX window computed synchronously (memory not registered). */
 int cgck_window_stats(uint64_t stats[4]);
 
-/* Burst server (latency).  Keeps one workgroup
- * resident on `ctx` (NULL: this thread's drop-in context) that serves small
- * host-resident batches through a host-coherent mailbox: cgck_desc_host and
- * the synchronous drop-in calls then skip the kernel launch and the stream
- * synchronisation whenever a batch fits (at most max_pkts and 64 packets,
- * max_bytes and 64 KiB of packet bytes).  The server exits after idle_ms without a
- * request (0: 200 ms) and is relaunched by the next one; close stops it.
- * cgck_ctx_destroy and cgck_thread_release close it too. */
+/* Burst server (latency).  Keeps up to 32 workgroups
+ * (one per 64 packets of max_pkts) resident on `ctx` (NULL: this thread's
+ * drop-in context) that serve host-resident batches through a host-coherent
+ * mailbox: cgck_desc_host, the RX window and the synchronous drop-in calls
+ * then skip the kernel launch and the stream synchronisation whenever a
+ * batch fits (at most max_pkts packets and max_bytes of packet bytes; a
+ * batch of more than 64 packets is split over the workgroups).  Batches
+ * above the caps take the launch path, whose many workgroups read host
+ * memory faster for hundreds of frames of >= 576 B: max_bytes ~96 KiB routes
+ * a mixed workload best.  The server exits after idle_ms
+ * without a request (0: 200 ms) and is relaunched by the next one; close
+ * stops it.  cgck_ctx_destroy and cgck_thread_release close it too. */
 int cgck_burst_open(cgck_ctx_t *ctx, uint32_t max_pkts, size_t max_bytes, uint32_t idle_ms);
 int cgck_burst_close(cgck_ctx_t *ctx);
 
