@@ -128,6 +128,8 @@ struct ThreadState {
 	PtrMap rxidx; // ip -> frame << 1; ip + hl (ICMP message) -> frame << 1 | 1
 	std::vector<cgck_desc_t> rxd;
 	std::vector<uint32_t> rxo, rxm;
+	std::vector<cgck_desc_t> txd; // the TX flush's descriptors and values (in place)
+	std::vector<uint32_t> txo;
 	uint64_t rx_served0 = 0; // stats[0] at rx_begin
 	uint64_t stats[4] = {0, 0, 0, 0};
 };
@@ -514,46 +516,56 @@ extern "C" int cgck_tx_flush(void)
 	HIP_TRY(hipSetDevice(c->device));
 	// Every entry lies in registered memory (the window queues nothing
 	// else).  When they all lie in one range (the transport's pool) the
-	// kernel reads them where they lie; otherwise each region is staged
-	// 16-byte aligned in pinned memory.  Descriptors and outputs follow.
+	// batch is described in place, as cgck_desc_host of that range (the
+	// burst server when one is open on this context and the flush fits it,
+	// else a launch); otherwise each region is staged 16-byte aligned in
+	// pinned memory and launched.
 	RegRange reg{nullptr, nullptr, nullptr};
 	bool inplace = reg_find(q[0].ip, q[0].span, &reg);
 	for (uint64_t i = 1; inplace && i < n; i++)
 		inplace = q[i].ip >= reg.lo && q[i].ip + q[i].span <= reg.hi;
-	size_t bytes = 0; // staged bytes
-	if (!inplace)
-		for (const TxEntry &e : q)
-			bytes += (e.span + 15) & ~(size_t)15;
-	const size_t d_off = (bytes + 15) & ~(size_t)15;
-	const size_t o_off = (d_off + 12 * n + 15) & ~(size_t)15;
-	int rc;
-	if ((rc = grow_host((void **)&c->h_stage, &c->h_stage_cap, o_off + 4 * n)))
-		return rc;
-	uint8_t *h = c->h_stage;
-	cgck_desc_t *d = (cgck_desc_t *)(h + d_off);
-	uint32_t *o = (uint32_t *)(h + o_off);
-	size_t at = 0;
-	for (uint64_t i = 0; i < n; i++) {
-		if (inplace) {
-			d[i].frame_off = (uint64_t)(q[i].ip - reg.lo);
-		} else {
-			memcpy(h + at, q[i].ip, q[i].span);
-			d[i].frame_off = at;
-			at += (q[i].span + 15) & ~(size_t)15;
-		}
-		d[i].l3_off = 0;
-		d[i].ip_len = (uint16_t)q[i].span;
-	}
-	// Both kinds in one launch: IP entries ask for the header checksum, L4
+	// Both kinds in one batch: IP entries ask for the header checksum, L4
 	// entries for the segment checksum; both read their fields as zero, as
 	// the reference's callers have just stored them (ip_output.c:61,
-	// tcp_subr.c:75 / gbtcp/tcp.c:426,436).  (The burst server measured
-	// slower on TX flushes: they keep the launch.)
-	KParams p = {inplace ? reg.dev : h, d, n, 0, 0, 0, CGCK_IP | CGCK_L4 | CGCK_ZERO_FIELDS, o, nullptr,
-		     nullptr, 0, nullptr};
-	if ((rc = run(c, p, 1500, c->stream)))
-		return rc;
-	HIP_TRY(hipStreamSynchronize(c->stream));
+	// tcp_subr.c:75 / gbtcp/tcp.c:426,436).
+	const uint32_t fl = CGCK_IP | CGCK_L4 | CGCK_ZERO_FIELDS;
+	int rc;
+	uint32_t *o;
+	if (inplace) {
+		t.txd.resize(n);
+		t.txo.resize(n);
+		for (uint64_t i = 0; i < n; i++) {
+			t.txd[i].frame_off = (uint64_t)(q[i].ip - reg.lo);
+			t.txd[i].l3_off = 0;
+			t.txd[i].ip_len = (uint16_t)q[i].span;
+		}
+		if ((rc = desc_host(c, reg.lo, (size_t)(reg.hi - reg.lo), t.txd.data(), n, fl, t.txo.data(), nullptr)))
+			return rc;
+		o = t.txo.data();
+	} else {
+		size_t bytes = 0; // staged bytes
+		for (const TxEntry &e : q)
+			bytes += (e.span + 15) & ~(size_t)15;
+		const size_t d_off = (bytes + 15) & ~(size_t)15;
+		const size_t o_off = (d_off + 12 * n + 15) & ~(size_t)15;
+		if ((rc = grow_host((void **)&c->h_stage, &c->h_stage_cap, o_off + 4 * n)))
+			return rc;
+		uint8_t *h = c->h_stage;
+		cgck_desc_t *d = (cgck_desc_t *)(h + d_off);
+		o = (uint32_t *)(h + o_off);
+		size_t at = 0;
+		for (uint64_t i = 0; i < n; i++) {
+			memcpy(h + at, q[i].ip, q[i].span);
+			d[i].frame_off = at;
+			d[i].l3_off = 0;
+			d[i].ip_len = (uint16_t)q[i].span;
+			at += (q[i].span + 15) & ~(size_t)15;
+		}
+		KParams p = {h, d, n, 0, 0, 0, fl, o, nullptr, nullptr, 0, nullptr};
+		if ((rc = run(c, p, 1500, c->stream)))
+			return rc;
+		HIP_TRY(hipStreamSynchronize(c->stream));
+	}
 	for (uint64_t i = 0; i < n; i++) {
 		uint16_t v;
 		uint8_t *dst;

@@ -256,7 +256,7 @@ int main(int argc, char **argv)
 				       win_name[pass], len, R, it, us, us_calls, R / us, bad_ip, bad_l4, (R + 63) / 64);
 				fflush(stdout);
 			}
-			for (int bi = 0; bi < nb && pass == 1; bi++) { /* TX: registered ring, launch path */
+			for (int bi = 0; bi < nb && (pass == 1 || pass == 3); bi++) { /* TX: registered ring, launch / server */
 				const int R = bursts[bi];
 				int it = 0, w = 0;
 				double t0 = now();
@@ -285,7 +285,7 @@ int main(int argc, char **argv)
 				const double us = median(t, it) * 1e6;
 				printf("{\"mode\": \"%s\", \"pkt_len\": %d, \"burst\": %d, \"iters\": %d, "
 				       "\"us_median\": %.2f, \"mpkt_s\": %.3f}\n",
-				       "tx_fill_registered", len, R, it, us, R / us);
+				       pass == 3 ? "tx_fill_registered_server" : "tx_fill_registered", len, R, it, us, R / us);
 				fflush(stdout);
 			}
 			if (srv) {
