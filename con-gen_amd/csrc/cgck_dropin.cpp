@@ -129,7 +129,7 @@ struct ThreadState {
 	std::vector<cgck_desc_t> rxd;
 	std::vector<uint32_t> rxo, rxm;
 	std::vector<cgck_desc_t> txd; // the TX flush's descriptors and values (in place)
-	std::vector<uint32_t> txo;
+	std::vector<uint32_t> txo, txi; // txi: the descriptor of each queued entry
 	uint64_t rx_served0 = 0; // stats[0] at rx_begin
 	uint64_t stats[4] = {0, 0, 0, 0};
 };
@@ -531,18 +531,37 @@ extern "C" int cgck_tx_flush(void)
 	const uint32_t fl = CGCK_IP | CGCK_L4 | CGCK_ZERO_FIELDS;
 	int rc;
 	uint32_t *o;
+	// One descriptor per packet: a packet's header entry and its segment
+	// entry (queued one after the other by the finalisers, ip_output.c:61-64
+	// after tcp_output.c:416-418) share it — it covers the segment, and the
+	// kernel returns both the header checksum (over ip_hl * 4 bytes, which
+	// the queue checked equals the header call's length) and the segment's
+	// L4 checksum from one read of the frame.
+	t.txi.resize(n);
 	if (inplace) {
 		t.txd.resize(n);
-		t.txo.resize(n);
+		uint64_t m = 0;
 		for (uint64_t i = 0; i < n; i++) {
-			t.txd[i].frame_off = (uint64_t)(q[i].ip - reg.lo);
-			t.txd[i].l3_off = 0;
-			t.txd[i].ip_len = (uint16_t)q[i].span;
+			if (i > 0 && q[i].ip == q[i - 1].ip && (q[i].fo < 0) != (q[i - 1].fo < 0) && t.txi[i - 1] == m - 1 &&
+			    (i < 2 || t.txi[i - 2] != m - 1)) {
+				t.txi[i] = (uint32_t)(m - 1);
+				if (q[i].span > t.txd[m - 1].ip_len)
+					t.txd[m - 1].ip_len = (uint16_t)q[i].span;
+				continue;
+			}
+			t.txi[i] = (uint32_t)m;
+			t.txd[m].frame_off = (uint64_t)(q[i].ip - reg.lo);
+			t.txd[m].l3_off = 0;
+			t.txd[m].ip_len = (uint16_t)q[i].span;
+			m++;
 		}
-		if ((rc = desc_host(c, reg.lo, (size_t)(reg.hi - reg.lo), t.txd.data(), n, fl, t.txo.data(), nullptr)))
+		t.txo.resize(m);
+		if ((rc = desc_host(c, reg.lo, (size_t)(reg.hi - reg.lo), t.txd.data(), m, fl, t.txo.data(), nullptr)))
 			return rc;
 		o = t.txo.data();
 	} else {
+		for (uint64_t i = 0; i < n; i++)
+			t.txi[i] = (uint32_t)i;
 		size_t bytes = 0; // staged bytes
 		for (const TxEntry &e : q)
 			bytes += (e.span + 15) & ~(size_t)15;
@@ -569,11 +588,12 @@ extern "C" int cgck_tx_flush(void)
 	for (uint64_t i = 0; i < n; i++) {
 		uint16_t v;
 		uint8_t *dst;
+		const uint32_t r = o[t.txi[i]];
 		if (q[i].fo < 0) {
-			v = (uint16_t)o[i];
+			v = (uint16_t)r;
 			dst = q[i].ip + 10;
 		} else {
-			v = (uint16_t)(o[i] >> 16);
+			v = (uint16_t)(r >> 16);
 			dst = q[i].ip + q[i].hl + q[i].fo;
 		}
 		memcpy(dst, &v, 2);

@@ -61,6 +61,9 @@ struct cgck_ctx {
 	hipStream_t bstream; // the server's own stream (it stays resident)
 };
 
+// Library-internal: hidden, so calls between the library's own files are
+// direct (no PLT hop on the drop-in symbols' per-call path, e.g. reg_find).
+#pragma GCC visibility push(hidden)
 namespace cgck {
 
 // Thread-local error text (cgck_last_error); returns `code`.
@@ -112,3 +115,4 @@ int rss_note_use(cgck_ctx *c, hipStream_t st);
 constexpr uint32_t kRssMaxCnt = 65536;
 
 } // namespace cgck
+#pragma GCC visibility pop
