@@ -315,6 +315,16 @@ static double now_s()
 static thread_local uint64_t t_lab_host[2]; // cgck_lab_burst_times
 #endif
 
+// Lab A/B bits of the server kernel ($CGCK_SERVER_OPTS; 0 in the product).
+static uint32_t server_opts()
+{
+	static const uint32_t v = [] {
+		const char *e = CGCK_ENV("CGCK_SERVER_OPTS");
+		return e && *e ? (uint32_t)strtoul(e, nullptr, 0) : 0u;
+	}();
+	return v;
+}
+
 // Server launches in this process: a relay word left by one launch (in
 // device memory a later server may get again) never matches another's tag.
 static std::atomic<uint32_t> g_burst_epoch{0};
@@ -328,7 +338,7 @@ static int burst_launch(cgck_ctx *c, uint32_t start_seq)
 		__atomic_store_n(&c->bbox->alive[j], (uint8_t)1, __ATOMIC_RELEASE);
 	hipError_t e = launch_burst_server(c->bbox_dev, c->bstage_dev, c->bscratch, c->bresp_dev, c->brelay,
 					   c->d_zero, (uint32_t)c->bstage_cap,
-					   c->bmax, c->bwgs, c->bper, start_seq, epoch, c->bstream);
+					   c->bmax, c->bwgs, c->bper, start_seq, epoch, server_opts(), c->bstream);
 	if (e != hipSuccess) {
 		for (uint32_t j = 0; j < c->bwgs; j++)
 			__atomic_store_n(&c->bbox->alive[j], (uint8_t)0, __ATOMIC_RELEASE);

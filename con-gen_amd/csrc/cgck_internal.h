@@ -130,10 +130,11 @@ constexpr uint32_t kBurstFirst = 8192;
 __host__ __device__ constexpr uint32_t burst_meta_off(uint32_t n) { return (4 * n + 63) & ~63u; }
 __host__ __device__ constexpr uint32_t burst_ver_off(uint32_t n) { return 2 * burst_meta_off(n); }
 // dcmd: 8 bytes of device memory, the leader's relay word (zeroed here on
-// the launch stream before the launch); epoch: nonzero, new for every launch.
+// the launch stream before the launch); epoch: nonzero, new for every launch;
+// opts: lab A/B bits (0 in the product).
 hipError_t launch_burst_server(BurstBox *box, const uint8_t *req, uint8_t *scratch, uint8_t *resp, uint64_t *dcmd,
 			       const void *zero, uint32_t cap, uint32_t max_pkts, uint32_t wgs, uint32_t per_wg,
-			       uint32_t start_seq, uint32_t epoch, hipStream_t st);
+			       uint32_t start_seq, uint32_t epoch, uint32_t opts, hipStream_t st);
 
 // Kernel selection flags (see cgck_dispatch.cpp) and the measured defaults
 // (tools/sweep.py; profiles/r01).  The group kernel streams whole lines per

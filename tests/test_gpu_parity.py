@@ -400,11 +400,11 @@ def test_burst_server_desc_host(engine, port, registered):
 @pytest.mark.parametrize("max_len", [80, 600])
 @pytest.mark.parametrize("registered", [False, True])
 def test_burst_server_wide(engine, port, registered, max_len):
-    """Requests split over the server's workgroups (burst_wgs: one per 64
-    packets, up to 32): slice edges at 64 / 65 / 130 / 2047 / 2048 / 4096
-    packets, staged or in place, generate / fill / verify, against the
-    referee; a second server with 2 workgroups (max_pkts 128) takes uneven
-    slices of the same batches."""
+    """Requests split over the server's workgroups (burst_wgs: one up to 64
+    packets, then one per 64, up to 32): slice edges at 64 / 65 / 130 / 2047 /
+    2048 / 4096 packets, staged or in place, generate / fill / verify,
+    against the referee; a second server of 2 workgroups (max_pkts 128)
+    takes uneven slices of 65 / 127 / 128 packets."""
     L = cgck.load()
     for max_pkts, sizes in ((4096, (64, 65, 130, 2047, 2048, 4096)), (128, (65, 127, 128))):
         engine.burst_open(max_pkts=max_pkts, max_bytes=4 << 20)
