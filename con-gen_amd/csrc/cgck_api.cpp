@@ -884,14 +884,16 @@ extern "C" int cgck_burst_open(cgck_ctx_t *c, uint32_t max_pkts, size_t max_byte
 
 #if CGCK_LAB
 // Lab: workgroup 0's timestamps of the last request (100 MHz ticks: seen,
-// block read, computed, published) and the host's view of that request
-// (ns: post, done seen) for tools/srvlat.c.
-extern "C" int cgck_lab_burst_times(cgck_ctx_t *c, uint64_t dev[4], uint64_t host[2])
+// block read, computed, published; then the compute phase in shader clocks)
+// and the host's view of that request (ns: post, done seen) for
+// tools/srvlat.c.
+extern "C" int cgck_lab_burst_times(cgck_ctx_t *c, uint64_t dev[5], uint64_t host[2])
 {
 	if (!c || !c->bbox)
 		return -EINVAL;
 	for (int i = 0; i < 4; i++)
 		dev[i] = __atomic_load_n(&c->bbox->lab_t[i], __ATOMIC_ACQUIRE);
+	dev[4] = __atomic_load_n(&c->bbox->lab_cyc, __ATOMIC_ACQUIRE);
 	host[0] = t_lab_host[0];
 	host[1] = t_lab_host[1];
 	return 0;

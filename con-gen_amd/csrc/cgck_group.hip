@@ -456,6 +456,7 @@ __global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const 
 		ok = __syncthreads_and(ok);
 #if CGCK_LAB
 		lab_t1 = __builtin_amdgcn_s_memrealtime();
+		const uint64_t lab_c1 = __builtin_amdgcn_s_memtime();
 #endif
 		if (ok) {
 			// W == 1 reads staged packet bytes from its scratch copy; wider
@@ -477,6 +478,7 @@ __global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const 
 #if CGCK_LAB
 		__syncthreads();
 		lab_t2 = __builtin_amdgcn_s_memrealtime();
+		const uint64_t lab_c2 = __builtin_amdgcn_s_memtime();
 #endif
 		// every thread's outputs (and in-place stores) written back to host
 		// memory before thread 0 publishes done[j]: a system-scope release per
@@ -490,6 +492,7 @@ __global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const 
 			__hip_atomic_store(&box->lab_t[1], lab_t1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 			__hip_atomic_store(&box->lab_t[2], lab_t2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 			__hip_atomic_store(&box->lab_t[3], lab_t3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+			__hip_atomic_store(&box->lab_cyc, lab_c2 - lab_c1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 		}
 #endif
 		if (t == 0) {

@@ -82,7 +82,7 @@ struct BurstBox {
 	uint32_t stop;       // host -> device: exit now
 	uint32_t bad_req;    // device -> host: requests refused by the server's block check
 	uint64_t idle_ticks; // 100 MHz ticks without a request before the server exits
-	uint32_t pad[2];
+	uint64_t lab_cyc;    // lab build: workgroup 0's shader clocks (s_memtime) over the compute phase
 	uint64_t lab_t[4];   // lab build: workgroup 0's s_memrealtime at seen / read / computed / published
 	uint32_t done[kBurstMaxWG]; // device -> host: the last request workgroup j served
 	uint8_t alive[kBurstMaxWG]; // host sets 1 at launch; workgroup j clears its byte on exit

@@ -12,7 +12,7 @@
 
 #include "cgck.h"
 
-int cgck_lab_burst_times(cgck_ctx_t *c, uint64_t dev[4], uint64_t host[2]);
+int cgck_lab_burst_times(cgck_ctx_t *c, uint64_t dev[5], uint64_t host[2]);
 
 #define SLOT 2048
 #define L3 14
@@ -44,8 +44,8 @@ int main(int argc, char **argv)
 	cgck_desc_t *desc = malloc(sizeof(cgck_desc_t) * maxb);
 	uint32_t *out = malloc(4 * maxb);
 	uint8_t *ver = malloc(maxb);
-	double *tt = malloc(sizeof(double) * it), *ph[5];
-	for (int k = 0; k < 5; k++)
+	double *tt = malloc(sizeof(double) * it), *ph[6];
+	for (int k = 0; k < 6; k++)
 		ph[k] = malloc(sizeof(double) * it);
 	cgck_ctx_t *ctx;
 	if (!ring || cgck_ctx_create(0, &ctx))
@@ -80,18 +80,19 @@ int main(int argc, char **argv)
 				return 1;
 			}
 			tt[i] = (now() - a) * 1e6;
-			uint64_t d[4], h[2];
+			uint64_t d[5], h[2];
 			cgck_lab_burst_times(ctx, d, h);
 			ph[0][i] = (d[1] - d[0]) / 100.0; /* seen -> block read + checked */
 			ph[1][i] = (d[2] - d[1]) / 100.0; /* -> computed (outputs issued) */
 			ph[2][i] = (d[3] - d[2]) / 100.0; /* -> release fence done */
 			ph[3][i] = (h[1] - h[0]) / 1000.0; /* host post -> done seen */
 			ph[4][i] = tt[i] - ph[3][i];       /* host work outside the wait */
+			ph[5][i] = d[2] > d[1] ? d[4] / ((d[2] - d[1]) * 10.0) : 0; /* shader clock in GHz */
 		}
 		printf("{\"pkt_len\": %d, \"burst\": %d, \"us_call\": %.2f, \"us_wait\": %.2f, \"us_host_rest\": %.2f, "
-		       "\"us_read\": %.2f, \"us_compute\": %.2f, \"us_release\": %.2f}\n",
+		       "\"us_read\": %.2f, \"us_compute\": %.2f, \"us_release\": %.2f, \"ghz_compute\": %.2f}\n",
 		       len, R, med(tt, it), med(ph[3], it), med(ph[4], it), med(ph[0], it), med(ph[1], it),
-		       med(ph[2], it));
+		       med(ph[2], it), med(ph[5], it));
 		fflush(stdout);
 	}
 	cgck_burst_close(ctx);
