@@ -273,19 +273,23 @@ int main(int argc, char **argv)
 						v = in_cksum(ip, 20);          /* ip->ip_sum = ip_cksum(ip) */
 						memcpy(ip + 10, &v, 2);
 					}
+					const double a1 = now();
 					const int r = cgck_tx_flush();
 					if (r != 2 * R) {
 						fprintf(stderr, "txburst: flush wrote %d of %d: %s\n", r, 2 * R,
 							cgck_last_error());
 						return 1;
 					}
-					if (w++ >= 20)
+					if (w++ >= 20) {
+						tc[it] = now() - a1;
 						t[it++] = now() - a;
+					}
 				}
-				const double us = median(t, it) * 1e6;
+				const double us = median(t, it) * 1e6, us_flush = median(tc, it) * 1e6;
 				printf("{\"mode\": \"%s\", \"pkt_len\": %d, \"burst\": %d, \"iters\": %d, "
-				       "\"us_median\": %.2f, \"mpkt_s\": %.3f}\n",
-				       pass == 3 ? "tx_fill_registered_server" : "tx_fill_registered", len, R, it, us, R / us);
+				       "\"us_median\": %.2f, \"us_flush\": %.2f, \"mpkt_s\": %.3f}\n",
+				       pass == 3 ? "tx_fill_registered_server" : "tx_fill_registered", len, R, it, us, us_flush,
+				       R / us);
 				fflush(stdout);
 			}
 			if (srv) {
