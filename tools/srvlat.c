@@ -3,7 +3,8 @@
  * slots (IPv4 at +14), with workgroup 0's device timestamps
  * (cgck_lab_burst_times: seen, block read, computed, published; 100 MHz)
  * against the host's post and done times.  Prints, per burst size, the
- * median of each phase in microseconds.  Not product code. */
+ * median of each phase in microseconds.  `srvlat LEN raw` sends CGCK_RAW
+ * requests instead of the BSD verify flags.  Not product code. */
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -67,7 +68,10 @@ int main(int argc, char **argv)
 		fprintf(stderr, "srvlat: setup: %s\n", cgck_last_error());
 		return 1;
 	}
-	const uint32_t vf = CGCK_IP | CGCK_L4 | CGCK_VERIFY | CGCK_V_IP_ZERO_IS_FFFF | CGCK_V_UDP_ZERO_SKIP;
+	/* argv[2]: "raw" for CGCK_RAW requests (no header work), else the BSD verify flags */
+	const uint32_t vf = argc > 2 && !strcmp(argv[2], "raw")
+				    ? CGCK_RAW
+				    : CGCK_IP | CGCK_L4 | CGCK_VERIFY | CGCK_V_IP_ZERO_IS_FFFF | CGCK_V_UDP_ZERO_SKIP;
 	const int bursts[] = {1, 32, 64, 65, 256, 2048};
 	for (unsigned bi = 0; bi < sizeof(bursts) / sizeof(bursts[0]); bi++) {
 		const int R = bursts[bi];
