@@ -65,6 +65,40 @@ __device__ __forceinline__ void zero_bytes(uint4 &w, int co, int r0, int r1)
 	w.w &= ~dmask(co, 3, r0, r1);
 }
 
+// The same byte-range masks from one 16-bit mask per chunk (the group body's
+// header zone, eat<>): bit b set when byte b of the chunk at packet-relative
+// co lies in [r0, r1).  A dword's byte mask is its nibble spread by one
+// multiply (bit j -> byte j), about half the VALU of four dmask() (tools/srvlat:
+// the header zone was half of a one-packet server request).
+__device__ __forceinline__ uint32_t cmask16(int co, int r0, int r1)
+{
+	const int s = min(max(r0 - co, 0), 16), e = min(max(r1 - co, 0), 16);
+	return e > s ? ((1u << e) - 1u) & ~((1u << s) - 1u) : 0u;
+}
+
+__device__ __forceinline__ uint32_t nibmask(uint32_t m, int i)
+{
+	const uint32_t n = (m >> (4 * i)) & 15u;
+	return ((n * 0x00204081u) & 0x01010101u) * 0xffu;
+}
+
+__device__ __forceinline__ uint32_t msum16(const uint4 &w, uint32_t m, uint32_t acc)
+{
+	acc = hsum(w.x & nibmask(m, 0), acc);
+	acc = hsum(w.y & nibmask(m, 1), acc);
+	acc = hsum(w.z & nibmask(m, 2), acc);
+	acc = hsum(w.w & nibmask(m, 3), acc);
+	return acc;
+}
+
+__device__ __forceinline__ void zero16(uint4 &w, uint32_t m)
+{
+	w.x &= ~nibmask(m, 0);
+	w.y &= ~nibmask(m, 1);
+	w.z &= ~nibmask(m, 2);
+	w.w &= ~nibmask(m, 3);
+}
+
 // Group reduction over G lanes (G in {4, 8, 16, 32, 64}); every lane of the
 // group ends with the group's sum.  quad_perm and row mirrors are DPP; the
 // 32/64 steps use cross-row swizzles.
@@ -383,20 +417,20 @@ __device__ __forceinline__ void eat(Part &pt, uint4 w, int k, int q, int len, in
 	if (HDR && co < q + 80) {
 		// Header zone: stored fields, optional zeroing, header sums.
 		if (flags & (CGCK_VERIFY | CGCK_ZERO_FIELDS)) {
-			uint32_t f = msum(w, co, q + 10, q + 12, 0);
-			uint32_t g = fo >= 0 ? msum(w, co, q + hl + fo, q + hl + fo + 2, 0) : 0u;
+			const uint32_t mf = cmask16(co, q + 10, q + 12);
+			const uint32_t mg = fo >= 0 ? cmask16(co, q + hl + fo, q + hl + fo + 2) : 0u;
+			const uint32_t f = msum16(w, mf, 0);
+			const uint32_t g = msum16(w, mg, 0);
 			pt.fld += f | (g << 16);
-			zero_bytes(w, co, q + 10, q + 12);
-			if (fo >= 0)
-				zero_bytes(w, co, q + hl + fo, q + hl + fo + 2);
+			zero16(w, mf | mg);
 		}
-		pt.ip = msum(w, co, q, q + hl, pt.ip);
-		pt.ps = msum(w, co, q + 12, q + 20, pt.ps);
+		pt.ip = msum16(w, cmask16(co, q, q + hl), pt.ip);
+		pt.ps = msum16(w, cmask16(co, q + 12, q + 20), pt.ps);
 	}
 	if (co >= q && co + 16 <= q + len)
 		pt.tot = sum4(w, pt.tot);
 	else
-		pt.tot = msum(w, co, q, q + len, pt.tot);
+		pt.tot = msum16(w, cmask16(co, q, q + len), pt.tot);
 }
 
 } // namespace cgck
