@@ -117,6 +117,25 @@ def test_burst_crossover():
     assert bench.burst_crossover({"error": "x"}, cpu) is None
 
 
+def test_burst_rows_take_the_faster_path():
+    """The summary rows and the TX crossover take the faster of the launch
+    path and the burst server for each cell."""
+    B = bench.BURSTS
+    rows = []
+    for ln in bench.BURST_LENS:
+        for b in B:
+            for mode, launch, server in (("rx_window_registered", 5.0, 3.0), ("rx_verify_registered", 2.0, 4.0),
+                                         ("tx_fill_registered", 6.0, 1.5)):
+                rows.append({"mode": mode, "pkt_len": ln, "burst": b, "us_median": launch})
+                rows.append({"mode": mode + "_server", "pkt_len": ln, "burst": b, "us_median": server})
+    cpu = {"rows": [{"pkt_len": ln, "burst": b, "us_per_burst": 1.8} for ln in bench.BURST_LENS for b in B]}
+    for r in bench.burst_summary(rows, cpu):
+        assert r[2:] == [3.0, 2.0, 1.5, 1.8], r
+    x = bench.burst_crossover(rows, cpu)
+    assert all(x[str(ln)]["tx_window"] == B[0] for ln in bench.BURST_LENS)   # the server's 1.5 < 1.8
+    assert all(x[str(ln)]["rx_window"] is None for ln in bench.BURST_LENS)   # 3.0 > 1.8 everywhere
+
+
 def test_single_rank_is_noop():
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
         os.environ.pop(k, None)
