@@ -363,34 +363,40 @@ def bench_burst():
     return [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
 
 
-BURST_COLS = ["pkt_len", "burst", "rx_window_reg_us", "rx_verify_reg_us", "tx_fill_reg_us", "cpu_ref_us"]
+BURST_COLS = ["pkt_len", "burst", "rx_window_launch_us", "rx_window_server_us", "rx_window_pipelined_us",
+              "tx_fill_launch_us", "tx_fill_server_us", "tx_fill_pipelined_us", "cpu_ref_us"]
+# (column, txburst mode): each column is ONE routing, as measured (no per-cell
+# minimum over routings): the launch path (no server open), the burst server
+# opened wide (every burst of the cell goes to it), and the server with one
+# burst in flight (host-thread-visible us per burst: post + wait + the
+# stack's calls + end, the stack's other work overlapping the GPU)
+BURST_MODES = (("rx_window_launch_us", "rx_window_registered"),
+               ("rx_window_server_us", "rx_window_registered_server"),
+               ("rx_window_pipelined_us", "rx_window_pipelined_registered_server"),
+               ("tx_fill_launch_us", "tx_fill_registered"),
+               ("tx_fill_server_us", "tx_fill_registered_server"),
+               ("tx_fill_pipelined_us", "tx_fill_pipelined_registered_server"))
 
 
 def burst_summary(rows, cpu):
-    """At most 10 rows for the JSON line (columns BURST_COLS): per packet size
-    and burst, the RX window, the one-call RX verify and the TX window on a
-    registered ring, each the faster of the launch path and the burst server,
-    against the reference CPU loop over the same burst (us per burst)."""
+    """At most 9 rows for the JSON line (columns BURST_COLS): per packet size
+    and burst, the RX window and the TX window on a registered ring through
+    each routing as measured, against the reference CPU loop over the same
+    burst (us per burst)."""
     if not isinstance(rows, list):
         return rows
     by = {(r["mode"], r["pkt_len"], r["burst"]): r["us_median"] for r in rows}
     cpu_by = {(r["pkt_len"], r["burst"]): round(r["us_per_burst"], 2) for r in (cpu or {}).get("rows", [])}
-
-    def best(mode, ln, b):
-        v = [by[(m, ln, b)] for m in (mode, mode + "_server") if (m, ln, b) in by]
-        return min(v) if v else None
-    return [[ln, b, best("rx_window_registered", ln, b), best("rx_verify_registered", ln, b),
-             best("tx_fill_registered", ln, b), cpu_by.get((ln, b))]
+    return [[ln, b] + [by.get((m, ln, b)) for _, m in BURST_MODES] + [cpu_by.get((ln, b))]
             for ln in sorted(BURST_LENS) for b in (32, 256, 2048)]
 
 
 def burst_crossover(rows, cpu):
-    """Per packet length, the smallest measured burst from which the RX window
-    (launch path or burst server, registered ring) and the TX window beat the
-    reference CPU loop over the same burst on one core, and stay ahead at every
-    larger measured burst; None when the GPU never wins up to max(BURSTS).
-    INTEGRATION.md quotes these as the threshold below which a window should
-    not be opened."""
+    """Per packet length and routing, the smallest measured burst from which
+    that routing beats the reference CPU loop over the same burst on one core,
+    and stays ahead at every larger measured burst; None when it never wins up
+    to max(BURSTS).  INTEGRATION.md quotes these as the threshold below which
+    a window should not be opened."""
     if not isinstance(rows, list) or not cpu:
         return None
     by = {(r["mode"], r["pkt_len"], r["burst"]): r["us_median"] for r in rows}
@@ -398,19 +404,15 @@ def burst_crossover(rows, cpu):
     res = {}
     for ln in sorted(BURST_LENS):
         cell = {}
-        for what, modes in (("rx_window", ("rx_window_registered", "rx_window_registered_server")),
-                            ("tx_window", ("tx_fill_registered", "tx_fill_registered_server"))):
-            wins = []
-            for b in BURSTS:
-                g = [by[(m, ln, b)] for m in modes if (m, ln, b) in by]
-                c = cpu_by.get((ln, b))
-                wins.append(bool(g) and c is not None and min(g) < c)
+        for col, mode in BURST_MODES:
+            wins = [(mode, ln, b) in by and cpu_by.get((ln, b)) is not None and by[(mode, ln, b)] < cpu_by[(ln, b)]
+                    for b in BURSTS]
             first = None
             for i in range(len(BURSTS) - 1, -1, -1):
                 if not wins[i]:
                     break
                 first = BURSTS[i]
-            cell[what] = first
+            cell[col[:-3]] = first
         res[str(ln)] = cell
     return res
 
@@ -589,7 +591,11 @@ TRAFFIC_SOURCE = ("profiles/pmc_latest.json: FETCH_SIZE x 2 + WRITE_SIZE per lau
 TRAFFIC_LIVE = ("this run: rocprofv3 --pmc FETCH_SIZE, then WRITE_SIZE, each a pass of its own over "
                 "tools/one_workload.py (the same batch and kernel, 3 launches, a child process on this box "
                 "after the timed region); bytes = (2 x FETCH_SIZE + WRITE_SIZE) KB x 1024, the median per "
-                "dispatch (MI355X_MICROARCH.md: FETCH_SIZE counts half a wide streaming read on gfx950)")
+                "dispatch.  The x 2: on gfx950 FETCH_SIZE = TCC_EA0_RDREQ x 64 B while each request of a "
+                "wide streaming read moves 128 B (/opt/skills/guides/MI355X_MICROARCH.md, HBM/rocprofv3 "
+                "section; in this repo profiles/r02/state64/README.md: TCC_EA0_RDREQ per 1 GiB 64 B-batch "
+                "dispatch = 8.39M = the batch's bytes / 128, and the doubled FETCH_SIZE of each workload "
+                "matches its algorithmic read bytes to 0.01-1 %, profiles/pmc_latest.json)")
 
 
 def pmc_traffic_live(kernels):
@@ -788,8 +794,9 @@ def main():
             except OSError:
                 path = None
             extra["burst"] = {"what": "us per burst, 2048 B ring slots registered with cgck_host_register, "
-                                      "from C (tools/txburst.c): RX window, one-call RX verify, TX window, "
-                                      "each the faster of the launch path and the burst server; "
+                                      "from C (tools/txburst.c): RX window and TX window through the launch "
+                                      "path, the burst server, and the server with one burst in flight "
+                                      "(host-thread-visible us, the stack's other work overlapping); "
                                       "cpu_ref = the reference in_cksum+udp_cksum per packet, 1 core",
                               "cols": BURST_COLS, "rows": burst_summary(burst, cpu_b),
                               "crossover_burst": burst_crossover(burst, cpu_b),

@@ -67,7 +67,8 @@ EXPORTS = (
     "toeplitz_hash", "rss_hash4", "cgck_toeplitz", "cgck_dst_cache", "cgck_dst_cache_host",
     "cgck_burst_open", "cgck_burst_close", "cgck_thread_ctx", "cgck_set_error_handler",
     "cgck_rx_begin", "cgck_rx_end", "cgck_window_stats", "cgck_ctx_last_kernel", "cgck_set_desc_layout",
-    "cgck_ctx_set_kernel", "cgck_synth_imix_ring",
+    "cgck_ctx_set_kernel", "cgck_synth_imix_ring", "cgck_burst_request", "cgck_host_device_ptr",
+    "cgck_rx_post", "cgck_rx_begin_posted", "cgck_tx_post", "cgck_tx_complete",
 )
 # Descriptor layout hint (cgck_set_desc_layout)
 LAYOUT_ANY = 0
@@ -148,10 +149,15 @@ def bind(path):
                                       ctypes.POINTER(_u32)]
     L.cgck_burst_open.argtypes = [_vp, _u32, ctypes.c_size_t, _u32]
     L.cgck_burst_close.argtypes = [_vp]
+    if hasattr(L, "cgck_burst_request"):   # ABI additions of round 4 (an older build loads without them)
+        L.cgck_burst_request.argtypes = [_vp, _vp, _u64, _vp, _u64, _u32, _vp, _vp]
+        L.cgck_host_device_ptr.argtypes = [_vp, ctypes.c_size_t, ctypes.POINTER(_vp)]
     L.cgck_thread_ctx.restype = _vp
     L.cgck_set_error_handler.restype = None
     L.cgck_set_error_handler.argtypes = [ERROR_FN, _vp]
     L.cgck_rx_begin.argtypes = [_vp, ctypes.c_size_t, _vp, _u64]
+    if hasattr(L, "cgck_rx_post"):
+        L.cgck_rx_post.argtypes = [_vp, ctypes.c_size_t, _vp, _u64]
     L.cgck_window_stats.argtypes = [ctypes.POINTER(_u64)]
     L.cgck_ctx_last_kernel.restype = ctypes.c_char_p
     L.cgck_ctx_last_kernel.argtypes = [_vp]
@@ -229,6 +235,19 @@ def burst_close():
     _check(load().cgck_burst_close(None), "cgck_burst_close")
 
 
+def last_error():
+    """cgck_last_error(): this thread's last error text."""
+    return load().cgck_last_error().decode()
+
+
+def host_device_ptr(arr, nbytes=None):
+    """cgck_host_device_ptr: the device view of a registered numpy buffer."""
+    p = _vp()
+    _check(load().cgck_host_device_ptr(arr.ctypes.data, arr.nbytes if nbytes is None else nbytes,
+                                       ctypes.byref(p)), "cgck_host_device_ptr")
+    return p.value
+
+
 def fn_pointers():
     """(in_cksum, udp_cksum) addresses in libcgck.so, for C harnesses that
     call the drop-in symbols (oracle.Port.replay_rx, oracle_cpu_bench)."""
@@ -249,6 +268,20 @@ def rx_begin(base, desc):
 def rx_end():
     """cgck_rx_end: returns how many drop-in calls the window answered."""
     return _check(load().cgck_rx_end(), "cgck_rx_end")
+
+
+def rx_post(base, desc):
+    """cgck_rx_post: post a burst (numpy ring + descriptors); returns the
+    frames posted.  The ring and the descriptors' frames must stay unchanged
+    until its window (rx_begin_posted .. rx_end) closes."""
+    assert desc.dtype == DESC_DTYPE
+    return _check(load().cgck_rx_post(base.ctypes.data, base.nbytes, desc.ctypes.data, len(desc)),
+                  "cgck_rx_post")
+
+
+def rx_begin_posted():
+    """cgck_rx_begin_posted: open the window over the oldest posted burst."""
+    return _check(load().cgck_rx_begin_posted(), "cgck_rx_begin_posted")
 
 
 def window_stats():
@@ -275,6 +308,16 @@ def tx_begin():
 
 def tx_flush():
     return _check(load().cgck_tx_flush(), "cgck_tx_flush")
+
+
+def tx_post():
+    """cgck_tx_post: post the window's fill; returns the fields queued."""
+    return _check(load().cgck_tx_post(), "cgck_tx_post")
+
+
+def tx_complete():
+    """cgck_tx_complete: wait for the oldest posted fill and write its fields."""
+    return _check(load().cgck_tx_complete(), "cgck_tx_complete")
 
 
 def thread_release():
@@ -374,6 +417,15 @@ class Engine:
 
     def burst_close(self):
         _check(load().cgck_burst_close(self.ctx), "cgck_burst_close")
+
+    def burst_request(self, dev_base, range_bytes, desc, flags, out=None, verdict=None):
+        """cgck_burst_request: one request to the open server over device-visible
+        memory [dev_base, +range_bytes); the server checks the descriptors.
+        Returns the library's return code (0, -EIO refused, -ENOSPC)."""
+        assert desc.dtype == DESC_DTYPE
+        return load().cgck_burst_request(self.ctx, dev_base, range_bytes, desc.ctypes.data, len(desc), flags,
+                                         None if out is None else out.ctypes.data,
+                                         None if verdict is None else verdict.ctypes.data)
 
     def set_desc_len_hint(self, n):
         _check(load().cgck_set_desc_len_hint(self.ctx, n), "cgck_set_desc_len_hint")

@@ -329,6 +329,31 @@ static uint32_t server_opts()
 // device memory a later server may get again) never matches another's tag.
 static std::atomic<uint32_t> g_burst_epoch{0};
 
+// No server kernel runs while a host mapping changes: every request, launch
+// and close holds g_map_mu shared; cgck_host_register / _unregister hold it
+// exclusively and drain every open server first (the next request relaunches
+// it).  g_srv lists the contexts with an open server.
+namespace {
+std::shared_mutex g_map_mu;
+std::mutex g_srv_mu;
+std::vector<cgck_ctx *> g_srv;
+} // namespace
+
+// Stop every open server and wait until its workgroups have left (caller
+// holds g_map_mu exclusively, so no request is in flight).
+static void burst_quiesce_all()
+{
+	std::lock_guard<std::mutex> lk(g_srv_mu);
+	for (cgck_ctx *c : g_srv) {
+		if (!c->bbox)
+			continue;
+		(void)hipSetDevice(c->device);
+		__atomic_store_n(&c->bbox->stop, 1u, __ATOMIC_RELEASE);
+		(void)hipStreamSynchronize(c->bstream);
+		__atomic_store_n(&c->bbox->stop, 0u, __ATOMIC_RELEASE);
+	}
+}
+
 static int burst_launch(cgck_ctx *c, uint32_t start_seq)
 {
 	uint32_t epoch;
@@ -356,16 +381,16 @@ static bool burst_all_alive(const cgck_ctx *c)
 }
 
 // A workgroup has idled out (or the server is draining): stop the rest,
-// wait until every workgroup has left, relaunch them for the request after
-// start_seq.
-static int burst_restart(cgck_ctx *c, uint32_t start_seq)
+// wait until every workgroup has left, relaunch them for the requests after
+// the last one completed (the pending ones are still in their slots).
+static int burst_restart(cgck_ctx *c)
 {
 	__atomic_store_n(&c->bbox->stop, 1u, __ATOMIC_RELEASE);
 	const hipError_t e = hipStreamSynchronize(c->bstream);
 	__atomic_store_n(&c->bbox->stop, 0u, __ATOMIC_RELEASE);
 	if (e != hipSuccess)
 		return set_err(-EIO, "burst server drain: %s", hipGetErrorString(e));
-	return burst_launch(c, start_seq);
+	return burst_launch(c, c->bdone);
 }
 
 // A request costs the poll, the round trips of the request block and the
@@ -376,14 +401,22 @@ static int burst_restart(cgck_ctx *c, uint32_t start_seq)
 // up to K workgroups, each reading its slice of the descriptors and the
 // packet bytes where they lie.  Registered packets are copied into the block
 // up to 32 KiB of block (one read for a small request) and read in place
-// above.  TX flushes (mixed 20 B / full-size entries) keep the launch path.
-// Which requests go to the server is the caller's choice at open:
-// cgck_burst_open's max_pkts and max_bytes (packet bytes per request).  The
-// launch path's many workgroups read the fabric faster for hundreds of
-// frames of >= 576 B (256 x 576 B: 22.8 vs 29.2 us), the server wins below
-// ~100 KiB of packet bytes (profiles/r03/burst), so max_bytes ~96 KiB routes
-// a mixed workload best; the bench opens it wide and reports both paths.
+// above; in-place requests carry their range, which the server checks every
+// descriptor against.  The TX window's flush goes through cgck_desc_host of
+// its ring range, so it takes the server whenever it fits.  Which requests go
+// to the server is the caller's choice at open: cgck_burst_open's max_pkts
+// and max_bytes (packet bytes per request).  The launch path's many
+// workgroups read the fabric faster for hundreds of frames of >= 576 B (256 x
+// 576 B: 22.8 vs 29.2 us), the server wins below ~100 KiB of packet bytes
+// (profiles/r03/burst), so max_bytes ~96 KiB routes a mixed workload best.
 // $CGCK_SERVER_PKTS / _COPY override the caps for A/B runs (lab build).
+//
+// Two requests may be outstanding (two slots, cgck_internal.h): a posted
+// request is collected (burst_wait, then its outputs read from its slot)
+// before its slot is posted to again.  The synchronous callers post and
+// collect at once; the pipelined windows (cgck_rx_post, cgck_tx_post) leave
+// one request posted while the stack works, and a later post that needs its
+// slot collects it first (burst_slot_free).
 static size_t env_size(const char *v, size_t dflt)
 {
 	return v && *v ? (size_t)strtoull(v, nullptr, 0) : dflt;
@@ -416,37 +449,24 @@ static bool burst_fits(const cgck_ctx *c, uint64_t n, uint32_t max_len, size_t s
 	       data <= c->bmax_bytes;
 }
 
-// Serve the request whose descriptors (and, for base_dev == nullptr, packet
-// bytes) are in the block, and wait for it.  Outputs land in c->bresp.
-static int burst_serve(cgck_ctx *c, const uint8_t *base_dev, uint64_t n, uint32_t flags, uint32_t max_len,
-		       const BurstLayout &L)
+static uint8_t *burst_block(const cgck_ctx *c, uint32_t seq) { return c->bstage + (size_t)(seq & 1) * c->bstage_cap; }
+
+static const uint8_t *burst_resp(const cgck_ctx *c, uint32_t seq)
 {
+	return c->bresp + (size_t)(seq & 1) * burst_resp_slot(c->bmax);
+}
+
+// Wait until request seq (n packets) is served.  Requests complete in order,
+// so a workgroup's done word at or past seq means its slice is in.
+static int burst_wait(cgck_ctx *c, uint32_t seq, uint32_t n, uint64_t range)
+{
+	std::shared_lock<std::shared_mutex> map_lk(g_map_mu);
 	BurstBox *b = c->bbox;
-	BurstReq *r = (BurstReq *)c->bstage;
-	r->n = (uint32_t)n;
-	r->flags = flags;
-	r->max_len = max_len;
-	r->bytes = (uint32_t)L.bytes;
-	r->base = (uint64_t)(uintptr_t)base_dev;
-	r->d_off = (uint32_t)L.d_off;
-	r->p_off = (uint32_t)L.p_off;
-	if (++c->bseq == 0) // seq 0 is the relay word's "nothing posted"
-		++c->bseq;
-	const uint32_t seq = c->bseq;
-#if CGCK_LAB
-	t_lab_host[0] = (uint64_t)(now_s() * 1e9);
-#endif
-	__atomic_store_n(&b->req, (uint64_t)seq | (uint64_t)n << 32, __ATOMIC_RELEASE);
-	if (!burst_all_alive(c)) {
-		int rc = burst_restart(c, seq - 1); // idled out: a new server picks the request up
-		if (rc)
-			return rc;
-	}
-	const uint32_t W = burst_wgs((uint32_t)n, c->bwgs, c->bper);
+	const uint32_t W = burst_wgs(n, c->bwgs, c->bper);
 	const double t0 = now_s();
 	uint32_t spin = 0;
 	for (uint32_t j = 0; j < W;) {
-		if (__atomic_load_n(&b->done[j], __ATOMIC_ACQUIRE) == seq) {
+		if ((int32_t)(__atomic_load_n(&b->done[j], __ATOMIC_ACQUIRE) - seq) >= 0) {
 			j++;
 			continue;
 		}
@@ -454,9 +474,10 @@ static int burst_serve(cgck_ctx *c, const uint8_t *base_dev, uint64_t n, uint32_
 		if ((++spin & 1023) != 0)
 			continue;
 		if (!burst_all_alive(c)) {
-			// a workgroup exited between our post and its last poll: drain
-			// and relaunch (a request served twice writes the same outputs)
-			int rc = burst_restart(c, seq - 1);
+			// a workgroup exited between the post and its last poll: drain
+			// and relaunch for the pending requests (slices already served
+			// are not served again: the server's recheck)
+			int rc = burst_restart(c);
 			if (rc)
 				return rc;
 		}
@@ -467,31 +488,111 @@ static int burst_serve(cgck_ctx *c, const uint8_t *base_dev, uint64_t n, uint32_
 			char miss[160];
 			int at = 0;
 			for (uint32_t k = 0; k < W && at < (int)sizeof(miss) - 12; k++)
-				if (__atomic_load_n(&b->done[k], __ATOMIC_ACQUIRE) != seq)
+				if ((int32_t)(__atomic_load_n(&b->done[k], __ATOMIC_ACQUIRE) - seq) < 0)
 					at += snprintf(miss + at, sizeof(miss) - at, " %u:%u", k,
 						       __atomic_load_n(&b->done[k], __ATOMIC_ACQUIRE));
 			miss[at] = 0;
 			__atomic_store_n(&b->stop, 1u, __ATOMIC_RELEASE);
 			(void)hipStreamSynchronize(c->bstream);
 			__atomic_store_n(&b->stop, 0u, __ATOMIC_RELEASE);
-			uint64_t relay = 0;
-			(void)hipMemcpy(&relay, c->brelay, 8, hipMemcpyDeviceToHost);
+			uint64_t relay[3] = {0, 0, 0};
+			(void)hipMemcpy(relay, c->brelay, sizeof(relay), hipMemcpyDeviceToHost);
+			c->bdone = seq; // abandoned: the next launch starts after it
 			return set_err(-ETIMEDOUT,
-				       "burst server: request %u (n %llu, W %u) not served in 2 s; missing (wg:done)%s; "
-				       "relay %#llx",
-				       seq, (unsigned long long)n, W, miss, (unsigned long long)relay);
+				       "burst server: request %u (n %u, W %u) not served in 2 s; missing (wg:done)%s; "
+				       "relay %#llx %#llx %#llx",
+				       seq, n, W, miss, (unsigned long long)relay[0], (unsigned long long)relay[1],
+				       (unsigned long long)relay[2]);
 		}
 	}
 #if CGCK_LAB
 	t_lab_host[1] = (uint64_t)(now_s() * 1e9);
 #endif
-	const uint32_t bad = __atomic_load_n(&b->bad_req, __ATOMIC_ACQUIRE);
-	if (bad != c->bbad) {
-		c->bbad = bad;
-		return set_err(-EIO, "burst server: request %u refused (block header or descriptors outside the block)",
-			       seq);
+	c->bdone = seq;
+	if (__atomic_load_n(&b->refused[seq & 1], __ATOMIC_ACQUIRE) == seq)
+		return set_err(-EIO,
+			       "burst server: request %u refused (block header, or a descriptor outside the block or "
+			       "past the %llu-byte range)",
+			       seq, (unsigned long long)range);
+	return 0;
+}
+
+// Collect a posted request: wait for it and copy its outputs where its
+// poster asked; frees its slot.
+int cgck::burst_collect(cgck_ctx *c, BurstPending *p)
+{
+	if (!p->seq)
+		return p->rc;
+	const uint32_t seq = p->seq;
+	p->seq = 0;
+	if (c->bslot[seq & 1] == p)
+		c->bslot[seq & 1] = nullptr;
+	int rc = burst_wait(c, seq, p->n, p->range);
+	if (rc == 0) {
+		const uint8_t *o = burst_resp(c, seq);
+		if (p->out)
+			memcpy(p->out, o, 4 * (size_t)p->n);
+		if (p->meta)
+			memcpy(p->meta, o + burst_meta_off(p->n), 4 * (size_t)p->n);
+		if (p->verdict)
+			memcpy(p->verdict, o + burst_ver_off(p->n), p->n);
+	}
+	p->rc = rc;
+	return rc;
+}
+
+// The block of the next request, with its slot free: a posted request still
+// holding that slot is collected first.
+static int burst_slot_free(cgck_ctx *c, uint8_t **block)
+{
+	const uint32_t seq = burst_next(c->bseq);
+	if (BurstPending *p = c->bslot[seq & 1]) {
+		const int rc = burst_collect(c, p); // its poster reads p->rc
+		(void)rc;
+	}
+	*block = burst_block(c, seq);
+	return 0;
+}
+
+// Post the request whose descriptors (and, for base_dev == nullptr, packet
+// bytes) are in the next block; returns its seq.
+static int burst_post(cgck_ctx *c, const uint8_t *base_dev, uint64_t range, uint64_t n, uint32_t flags,
+		      uint32_t max_len, const BurstLayout &L, uint32_t *seq_out)
+{
+	std::shared_lock<std::shared_mutex> map_lk(g_map_mu);
+	BurstBox *b = c->bbox;
+	const uint32_t seq = burst_next(c->bseq);
+	BurstReq *r = (BurstReq *)burst_block(c, seq);
+	r->n = (uint32_t)n;
+	r->flags = flags;
+	r->max_len = max_len;
+	r->bytes = (uint32_t)L.bytes;
+	r->base = (uint64_t)(uintptr_t)base_dev;
+	r->range = base_dev ? range : 0;
+	r->d_off = (uint32_t)L.d_off;
+	r->p_off = (uint32_t)L.p_off;
+	c->bseq = seq;
+#if CGCK_LAB
+	t_lab_host[0] = (uint64_t)(now_s() * 1e9);
+#endif
+	__atomic_store_n(&b->req[seq & 1], (uint64_t)seq | (uint64_t)n << 32, __ATOMIC_RELEASE);
+	*seq_out = seq;
+	if (!burst_all_alive(c)) {
+		int rc = burst_restart(c); // idled out: a new server picks the pending requests up
+		if (rc)
+			return rc;
 	}
 	return 0;
+}
+
+// Post and collect at once: outputs at burst_resp(c, *seq_out).
+static int burst_serve(cgck_ctx *c, const uint8_t *base_dev, uint64_t range, uint64_t n, uint32_t flags,
+		       uint32_t max_len, const BurstLayout &L, uint32_t *seq_out)
+{
+	int rc = burst_post(c, base_dev, range, n, flags, max_len, L, seq_out);
+	if (rc)
+		return rc;
+	return burst_wait(c, *seq_out, (uint32_t)n, range);
 }
 
 // --------------------------------------------------------------------------
@@ -529,8 +630,12 @@ static void *registered_ptr(void *p, size_t bytes)
 	return a.devicePointer;
 }
 
-int cgck::desc_host(cgck_ctx *c, void *base, size_t bytes, const cgck_desc_t *desc, uint64_t n, uint32_t flags,
-		    uint32_t *out, uint8_t *verdict, uint32_t *meta)
+// desc_host, or (pend != nullptr) its posted form: when the request goes to
+// the burst server it is left posted and *pend records where its outputs go
+// (1 is returned; burst_collect finishes it), otherwise it is computed at
+// once (0).
+static int desc_host_impl(cgck_ctx *c, void *base, size_t bytes, const cgck_desc_t *desc, uint64_t n, uint32_t flags,
+			  uint32_t *out, uint8_t *verdict, uint32_t *meta, BurstPending *pend)
 {
 	if (n == 0)
 		return 0;
@@ -569,7 +674,9 @@ int cgck::desc_host(cgck_ctx *c, void *base, size_t bytes, const cgck_desc_t *de
 	if ((in_place || !store) && burst_fits(c, n, max_len, in_place ? 0 : pkt_bytes, pkt_bytes)) {
 		// the resident server: no launch, no stream sync
 		const BurstLayout L = burst_layout(in_place ? 0 : pkt_bytes, n);
-		uint8_t *h = c->bstage;
+		uint8_t *h;
+		if ((rc = burst_slot_free(c, &h)))
+			return rc;
 		cgck_desc_t *d = (cgck_desc_t *)(h + L.d_off);
 		if (in_place) {
 			memcpy(d, desc, 12 * n);
@@ -584,15 +691,23 @@ int cgck::desc_host(cgck_ctx *c, void *base, size_t bytes, const cgck_desc_t *de
 				at += ((size_t)desc[i].ip_len + 15) & ~(size_t)15;
 			}
 		}
-		if ((rc = burst_serve(c, in_place ? (const uint8_t *)dev_base : nullptr, n, flags, max_len, L)))
+		uint32_t seq;
+		if ((rc = burst_post(c, in_place ? (const uint8_t *)dev_base : nullptr, bytes, n, flags, max_len, L, &seq)))
 			return rc;
-		if (out)
-			memcpy(out, c->bresp, 4 * n);
-		if (meta)
-			memcpy(meta, c->bresp + burst_meta_off((uint32_t)n), 4 * n);
-		if (verdict)
-			memcpy(verdict, c->bresp + burst_ver_off((uint32_t)n), n);
-		return 0;
+		BurstPending now;
+		BurstPending *q = pend ? pend : &now;
+		q->seq = seq;
+		q->n = (uint32_t)n;
+		q->range = bytes;
+		q->out = out;
+		q->meta = meta;
+		q->verdict = verdict;
+		q->rc = 0;
+		if (pend) {
+			c->bslot[seq & 1] = pend;
+			return 1;
+		}
+		return burst_collect(c, &now);
 	}
 	if (dev_base || pkt_bytes <= kStageBytes) {
 		// pinned staging: [packets (staged case)] | descriptors | out | meta | verdict
@@ -674,6 +789,20 @@ int cgck::desc_host(cgck_ctx *c, void *base, size_t bytes, const cgck_desc_t *de
 	return 0;
 }
 
+int cgck::desc_host(cgck_ctx *c, void *base, size_t bytes, const cgck_desc_t *desc, uint64_t n, uint32_t flags,
+		    uint32_t *out, uint8_t *verdict, uint32_t *meta)
+{
+	return desc_host_impl(c, base, bytes, desc, n, flags, out, verdict, meta, nullptr);
+}
+
+int cgck::desc_host_post(cgck_ctx *c, void *base, size_t bytes, const cgck_desc_t *desc, uint64_t n, uint32_t flags,
+			 uint32_t *out, uint8_t *verdict, uint32_t *meta, BurstPending *pend)
+{
+	pend->seq = 0;
+	pend->rc = 0;
+	return desc_host_impl(c, base, bytes, desc, n, flags, out, verdict, meta, pend);
+}
+
 extern "C" int cgck_desc_host(cgck_ctx_t *c, void *base, size_t bytes, const cgck_desc_t *desc,
 			      uint64_t n, uint32_t flags, uint32_t *out, uint8_t *verdict)
 {
@@ -683,6 +812,44 @@ extern "C" int cgck_desc_host(cgck_ctx_t *c, void *base, size_t bytes, const cgc
 	if (rc)
 		return rc;
 	return desc_host(c, base, bytes, desc, n, flags, out, verdict);
+}
+
+// One request to the context's burst server over device-visible memory the
+// caller already holds (a registered ring's device view): no host-side check
+// of the descriptors — the server checks each against `range` on the device
+// before any load or store, and refuses the request (-EIO) otherwise.
+extern "C" int cgck_burst_request(cgck_ctx_t *c, const void *dev_base, uint64_t range, const cgck_desc_t *desc,
+				  uint64_t n, uint32_t flags, uint32_t *out, uint8_t *verdict)
+{
+	if (!c && !(c = thread_ctx()))
+		return -ENODEV; // thread_ctx set the message
+	int rc = check_flags(flags);
+	if (rc)
+		return rc;
+	if (!dev_base || !range || (n && !desc))
+		return set_err(-EINVAL, "cgck_burst_request: NULL base, zero range or NULL descriptors");
+	if (n == 0)
+		return 0;
+	uint32_t max_len = 0;
+	for (uint64_t i = 0; i < n; i++)
+		max_len = desc[i].ip_len > max_len ? desc[i].ip_len : max_len;
+	if (!burst_fits(c, n, max_len, 0, 0))
+		return set_err(-ENOSPC, "cgck_burst_request: no burst server open on the context, or %llu packets "
+					"exceed its capacity", (unsigned long long)n);
+	const BurstLayout L = burst_layout(0, n);
+	uint8_t *h;
+	if ((rc = burst_slot_free(c, &h)))
+		return rc;
+	memcpy(h + L.d_off, desc, 12 * n);
+	uint32_t seq;
+	if ((rc = burst_serve(c, (const uint8_t *)dev_base, range, n, flags, max_len, L, &seq)))
+		return rc;
+	const uint8_t *o = burst_resp(c, seq);
+	if (out)
+		memcpy(out, o, 4 * n);
+	if (verdict)
+		memcpy(verdict, o + burst_ver_off((uint32_t)n), n);
+	return 0;
 }
 
 // Ranges registered through cgck_host_register, so the deferred TX window
@@ -719,6 +886,8 @@ bool cgck::reg_find(const void *p, size_t bytes, RegRange *r)
 
 extern "C" int cgck_host_register(void *ptr, size_t bytes)
 {
+	std::unique_lock<std::shared_mutex> map_lk(g_map_mu);
+	burst_quiesce_all();
 	HIP_TRY(hipHostRegister(ptr, bytes, hipHostRegisterDefault));
 	void *dev = nullptr;
 	if (hipHostGetDevicePointer(&dev, ptr, 0) != hipSuccess || !dev) {
@@ -731,8 +900,22 @@ extern "C" int cgck_host_register(void *ptr, size_t bytes)
 	return 0;
 }
 
+extern "C" int cgck_host_device_ptr(const void *ptr, size_t bytes, void **dev)
+{
+	if (!dev)
+		return set_err(-EINVAL, "cgck_host_device_ptr: dev is NULL");
+	*dev = nullptr;
+	RegRange rr;
+	if (!ptr || !reg_find(ptr, bytes, &rr))
+		return set_err(-ENOENT, "cgck_host_device_ptr: [%p, +%zu) is not inside a registered range", ptr, bytes);
+	*dev = rr.dev + ((const uint8_t *)ptr - rr.lo);
+	return 0;
+}
+
 extern "C" int cgck_host_unregister(void *ptr)
 {
+	std::unique_lock<std::shared_mutex> map_lk(g_map_mu);
+	burst_quiesce_all();
 	{
 		std::unique_lock<std::shared_mutex> lk(g_reg_mu);
 		for (size_t i = 0; i < g_reg.size(); i++)
@@ -758,15 +941,19 @@ int cgck::one_region(cgck_ctx *c, const void *src, uint32_t span, uint32_t ip_le
 	if (ip_len <= 0xffff && !(flags & CGCK_STORE) && burst_fits(c, 1, ip_len, span, span)) {
 		// the resident server: one descriptor, no launch, no stream sync
 		const BurstLayout L = burst_layout(span, 1);
+		uint8_t *h;
+		if ((rc = burst_slot_free(c, &h)))
+			return rc;
 		if (span)
-			memcpy(c->bstage + L.p_off, src, span);
-		cgck_desc_t *d = (cgck_desc_t *)(c->bstage + L.d_off);
+			memcpy(h + L.p_off, src, span);
+		cgck_desc_t *d = (cgck_desc_t *)(h + L.d_off);
 		d->frame_off = 0;
 		d->l3_off = 0;
 		d->ip_len = (uint16_t)ip_len;
-		if ((rc = burst_serve(c, nullptr, 1, flags, ip_len, L)))
+		uint32_t seq;
+		if ((rc = burst_serve(c, nullptr, 0, 1, flags, ip_len, L, &seq)))
 			return rc;
-		*out = *(const uint32_t *)c->bresp;
+		*out = *(const uint32_t *)burst_resp(c, seq);
 		return 0;
 	}
 	if ((rc = grow_host((void **)&c->h_stage, &c->h_stage_cap, span + 16)) ||
@@ -815,8 +1002,8 @@ extern "C" int cgck_burst_open(cgck_ctx_t *c, uint32_t max_pkts, size_t max_byte
 	// server's first read fetches kBurstFirst bytes whatever the request
 	size_t cap = burst_layout(((max_bytes + 15) & ~(size_t)15) + 16 * (size_t)max_pkts, max_pkts).bytes;
 	cap = (cap < kBurstFirst ? kBurstFirst : cap + 15) & ~(size_t)15;
-	const size_t ver_off = burst_ver_off(max_pkts); // the outputs of the largest request
-	size_t resp_bytes = ver_off + max_pkts;
+	// two slots of outputs, each for the largest request
+	size_t resp_bytes = 2 * (size_t)burst_resp_slot(max_pkts);
 	unsigned resp_flags = hipHostMallocCoherent;
 	if (const char *e = CGCK_ENV("CGCK_BRESP_MIN")) // lab A/B: allocation size of the outputs
 		resp_bytes = resp_bytes < env_size(e, 0) ? env_size(e, 0) : resp_bytes;
@@ -825,13 +1012,13 @@ extern "C" int cgck_burst_open(cgck_ctx_t *c, uint32_t max_pkts, size_t max_byte
 	void *box = nullptr, *st = nullptr, *rs = nullptr, *bd = nullptr, *sd = nullptr, *rd = nullptr, *sc = nullptr;
 	hipError_t e = hipHostMalloc(&box, sizeof(BurstBox), hipHostMallocCoherent);
 	if (e == hipSuccess)
-		e = hipHostMalloc(&st, cap, hipHostMallocCoherent);
+		e = hipHostMalloc(&st, 2 * cap, hipHostMallocCoherent); // two request slots
 	if (e == hipSuccess)
 		e = hipHostMalloc(&rs, resp_bytes, resp_flags);
 	if (e == hipSuccess)
 		e = hipMalloc(&sc, cap);
-	// the leader's relay word, uncached: every poll and store goes to memory,
-	// whichever XCD's L2 the workgroups sit behind
+	// the leader's relay (one per slot, then the exit word), uncached: every poll and store
+	// goes to memory, whichever XCD's L2 the workgroups sit behind
 	void *rl = nullptr;
 	if (e == hipSuccess)
 		e = hipExtMallocWithFlags(&rl, 64, hipDeviceMallocUncached);
@@ -854,7 +1041,7 @@ extern "C" int cgck_burst_open(cgck_ctx_t *c, uint32_t max_pkts, size_t max_byte
 		return set_err(-EIO, "cgck_burst_open: %s", hipGetErrorString(e));
 	}
 	memset(box, 0, sizeof(BurstBox));
-	memset(st, 0, cap);
+	memset(st, 0, 2 * cap);
 	c->bbox = (BurstBox *)box;
 	// one workgroup per kBurstPerWG packets of the largest request, at most
 	// kBurstMaxWG (and the device's CUs)
@@ -878,7 +1065,14 @@ extern "C" int cgck_burst_open(cgck_ctx_t *c, uint32_t max_pkts, size_t max_byte
 	c->bmax = max_pkts;
 	c->bmax_bytes = max_bytes;
 	c->bseq = 0;
+	c->bdone = 0;
 	c->bbad = 0;
+	c->bslot[0] = c->bslot[1] = nullptr;
+	std::shared_lock<std::shared_mutex> map_lk(g_map_mu);
+	{
+		std::lock_guard<std::mutex> lk(g_srv_mu);
+		g_srv.push_back(c);
+	}
 	return burst_launch(c, 0);
 }
 
@@ -906,6 +1100,20 @@ extern "C" int cgck_burst_close(cgck_ctx_t *c)
 		c = thread_ctx_if_any(); // this thread's drop-in context, if it exists
 	if (!c || !c->bbox)
 		return 0;
+	// posted requests complete first: their outputs land where their posters
+	// asked (a window still open reads them)
+	for (BurstPending *p : {c->bslot[0], c->bslot[1]})
+		if (p)
+			(void)burst_collect(c, p);
+	std::shared_lock<std::shared_mutex> map_lk(g_map_mu);
+	{
+		std::lock_guard<std::mutex> lk(g_srv_mu);
+		for (size_t i = 0; i < g_srv.size(); i++)
+			if (g_srv[i] == c) {
+				g_srv.erase(g_srv.begin() + i);
+				break;
+			}
+	}
 	(void)hipSetDevice(c->device);
 	__atomic_store_n(&c->bbox->stop, 1u, __ATOMIC_RELEASE);
 	hipError_t e = hipStreamSynchronize(c->bstream); // the server sees `stop` within one poll

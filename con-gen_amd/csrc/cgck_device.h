@@ -379,6 +379,29 @@ __device__ __forceinline__ Pkt get_pkt(const KParams &p, uint64_t k)
 	return r;
 }
 
+// The same over descriptors staged in the workgroup's LDS (the burst server's
+// slice path): p.desc is a generic pointer into LDS, read as ds_read.
+typedef __attribute__((address_space(3))) const uint32_t lds_u32;
+__device__ __forceinline__ Pkt get_pkt_lds(const KParams &p, uint64_t k)
+{
+	Pkt r;
+	r.ok = k < p.n;
+	const uint32_t kk = r.ok ? (uint32_t)k : 0u;
+	lds_u32 *d = (lds_u32 *)(const uint32_t *)p.desc + 3 * kk;
+	const uint32_t lo = d[0], hi = d[1], w2 = d[2];
+	r.a0 = reinterpret_cast<uint64_t>(p.base) + (((uint64_t)hi << 32) | lo) + (w2 & 0xffffu);
+	r.len = r.ok ? w2 >> 16 : 0u;
+	return r;
+}
+
+// Is descriptor {lo, hi, w2} (frame_off, l3_off | ip_len << 16) inside a
+// range of `limit` bytes: frame_off + l3_off + ip_len <= limit, no wrap.
+__device__ __forceinline__ bool desc_inside(uint32_t lo, uint32_t hi, uint32_t w2, uint64_t limit)
+{
+	const uint64_t fo = ((uint64_t)hi << 32) | lo;
+	return fo <= limit && (w2 & 0xffffu) + (w2 >> 16) <= limit - fo;
+}
+
 // (m & a) | (~m & b): one v_bfi_b32.  The mask is made opaque to the
 // optimizer so selects between array elements are never rewritten into a
 // dynamically indexed (scratch) load.

@@ -106,6 +106,25 @@ struct TxEntry {
 	int16_t fo; // -1: IP header entry (field ip+10); else L4 field offset after the header
 };
 
+// One receive burst: its descriptors and the kernel's values and meta words
+// (kFlagRx), and, when it was left posted on the burst server, the request.
+struct RxBurst {
+	const uint8_t *base = nullptr;
+	uint64_t n = 0;
+	std::vector<cgck_desc_t> d;
+	std::vector<uint32_t> o, m;
+	BurstPending pend{};
+};
+
+// One TX flush: the queued fields, the descriptors of the in-place batch (or
+// the staged copies' values), and the posted request (cgck_tx_post).
+struct TxFill {
+	std::vector<TxEntry> q;
+	std::vector<cgck_desc_t> d;
+	std::vector<uint32_t> o, idx; // idx: the value (descriptor) of each queued entry
+	BurstPending pend{};
+};
+
 struct ThreadState {
 	cgck_ctx *ctx = nullptr;
 	// TX window
@@ -114,22 +133,28 @@ struct ThreadState {
 	const uint8_t *tx_max = nullptr; // highest header address queued so far
 	bool tx_map = false;             // txidx built (the first call below tx_max)
 	PtrMap txidx; // (ip << 1 | is_l4) -> txq index
+	TxFill txs;       // cgck_tx_flush's batch
+	TxFill txp[2];    // posted fills (cgck_tx_post), oldest at txp_head
+	unsigned txp_head = 0, txp_count = 0;
 	// RX window: frame i's header at rx_base + rxd[i].frame_off +
 	// rxd[i].l3_off; rxo[i] its values (lo16 header checksum, hi16 L4
 	// checksum, ICMP without the pseudo-header) and rxm[i] which calls they
 	// answer (kFlagRx's meta word: kRxOkIp | kRxOkL4 | kRxIcmp, ip_hl * 4 in
 	// bits 8-15, ntohs(ip_len) - ip_hl * 4 in bits 16-31, zero for a frame the
-	// stack drops before any checksum), both written by the kernel
+	// stack drops before any checksum), both written by the kernel; they point
+	// into the burst the window answers from
 	bool rx_open = false;
+	bool rx_posted = false; // the window is over the oldest posted burst
 	const uint8_t *rx_base = nullptr;
 	size_t rx_n = 0;
 	size_t rx_cur = 0;    // the frame the last answered call matched
 	bool rx_map = false;  // rxidx built (on the first call off the cursor)
 	PtrMap rxidx; // ip -> frame << 1; ip + hl (ICMP message) -> frame << 1 | 1
-	std::vector<cgck_desc_t> rxd;
-	std::vector<uint32_t> rxo, rxm;
-	std::vector<cgck_desc_t> txd; // the TX flush's descriptors and values (in place)
-	std::vector<uint32_t> txo, txi; // txi: the descriptor of each queued entry
+	const cgck_desc_t *rxd = nullptr;
+	const uint32_t *rxo = nullptr, *rxm = nullptr;
+	RxBurst rxs;      // cgck_rx_begin's burst
+	RxBurst rxp[2];   // posted bursts (cgck_rx_post), oldest at rxp_head
+	unsigned rxp_head = 0, rxp_count = 0;
 	uint64_t rx_served0 = 0; // stats[0] at rx_begin
 	uint64_t stats[4] = {0, 0, 0, 0};
 };
@@ -177,7 +202,7 @@ inline const uint8_t *rx_ip(const ThreadState &t, size_t i)
 __attribute__((noinline)) bool rx_find_slow(ThreadState &t, const uint8_t *p, uint32_t *v)
 {
 	const size_t n = t.rx_n;
-	const uint32_t *m = t.rxm.data();
+	const uint32_t *m = t.rxm;
 	// the cursor frame, then the next answerable ones (frames the stack
 	// dropped unverified have no calls: up to 8 are stepped over)
 	for (size_t i = t.rx_cur, seen = 0, lim = t.rx_cur + 10; i < n && i < lim && seen < 2; i++) {
@@ -428,15 +453,59 @@ extern "C" uint16_t udp_cksum(struct ip *ipp, int len)
 // RX window
 // --------------------------------------------------------------------------
 
+namespace {
+
+constexpr uint32_t kRxFlags = CGCK_IP | CGCK_L4 | CGCK_ZERO_FIELDS | kFlagL4Auto | kFlagRx;
+
+// Fill a burst's descriptor copy and output arrays for n frames.
+void rx_fill(RxBurst &r, const void *base, const cgck_desc_t *desc, uint64_t n)
+{
+	r.base = (const uint8_t *)base;
+	r.n = n;
+	r.d.assign(desc, desc + n);
+	r.o.resize(n ? n : 1);
+	r.m.resize(n ? n : 1);
+}
+
+// Open the window over a computed burst; returns the frames it answers for.
+int rx_open_on(ThreadState &t, const RxBurst &r, bool posted)
+{
+	uint64_t m = 0;
+	for (uint64_t i = 0; i < r.n; i++)
+		m += r.m[i] != 0;
+	t.rxd = r.d.data();
+	t.rxo = r.o.data();
+	t.rxm = r.m.data();
+	t.rx_base = r.base;
+	t.rx_n = r.n;
+	t.rx_cur = 0;
+	t.rx_map = false;
+	t.rx_open = true;
+	t.rx_posted = posted;
+	t.rx_served0 = t.stats[0];
+	return (int)m;
+}
+
+int rx_check(ThreadState &t, const void *base, const cgck_desc_t *desc, uint64_t n, const char *who)
+{
+	(void)t;
+	if (n && (!base || !desc))
+		return set_err(-EINVAL, "%s: NULL base or descriptors", who);
+	if (n > 0xffffffffull / 2)
+		return set_err(-EINVAL, "%s: burst of %llu frames", who, (unsigned long long)n);
+	return 0;
+}
+
+} // namespace
+
 extern "C" int cgck_rx_begin(void *base, size_t bytes, const cgck_desc_t *desc, uint64_t n)
 {
 	ThreadState &t = tstate();
 	if (t.rx_open)
 		return set_err(-EBUSY, "cgck_rx_begin: an RX window is already open on this thread");
-	if (n && (!base || !desc))
-		return set_err(-EINVAL, "cgck_rx_begin: NULL base or descriptors");
-	if (n > 0xffffffffull / 2)
-		return set_err(-EINVAL, "cgck_rx_begin: burst of %llu frames", (unsigned long long)n);
+	int rc = rx_check(t, base, desc, n, "cgck_rx_begin");
+	if (rc)
+		return rc;
 	cgck_ctx *c = thread_ctx();
 	if (!c)
 		return -ENODEV; // thread_ctx set the message
@@ -447,29 +516,60 @@ extern "C" int cgck_rx_begin(void *base, size_t bytes, const cgck_desc_t *desc, 
 	// drop rules of ip_input.c:28-44, 76, tcp_input.c:67, udp_usrreq.c:65,
 	// ip_icmp.c:177, gbtcp/inet.c:282-314), so no header is parsed here.
 	// desc_host checks every descriptor against [base, base + bytes).
-	t.rxd.assign(desc, desc + n);
-	t.rxo.resize(n ? n : 1);
-	t.rxm.resize(n ? n : 1);
-	if (n) {
-		const int rc = desc_host(c, base, bytes, t.rxd.data(), n,
-					 CGCK_IP | CGCK_L4 | CGCK_ZERO_FIELDS | kFlagL4Auto | kFlagRx, t.rxo.data(), nullptr,
-					 t.rxm.data());
-		if (rc) {
-			char msg[256];
-			snprintf(msg, sizeof(msg), "%s", err_text());
-			return set_err(rc, "cgck_rx_begin: %s", msg);
-		}
+	rx_fill(t.rxs, base, desc, n);
+	if (n && (rc = desc_host(c, base, bytes, t.rxs.d.data(), n, kRxFlags, t.rxs.o.data(), nullptr,
+				 t.rxs.m.data()))) {
+		char msg[256];
+		snprintf(msg, sizeof(msg), "%s", err_text());
+		return set_err(rc, "cgck_rx_begin: %s", msg);
 	}
-	uint64_t m = 0;
-	for (uint64_t i = 0; i < n; i++)
-		m += t.rxm[i] != 0;
-	t.rx_base = (const uint8_t *)base;
-	t.rx_n = n;
-	t.rx_cur = 0;
-	t.rx_map = false;
-	t.rx_open = true;
-	t.rx_served0 = t.stats[0];
-	return (int)m;
+	return rx_open_on(t, t.rxs, false);
+}
+
+// Pipelined form: post burst k and return; the window over it opens at a
+// later cgck_rx_begin_posted, while the stack has worked on burst k - 1.
+extern "C" int cgck_rx_post(void *base, size_t bytes, const cgck_desc_t *desc, uint64_t n)
+{
+	ThreadState &t = tstate();
+	if (t.rxp_count == 2)
+		return set_err(-EBUSY, "cgck_rx_post: two bursts already posted and not yet opened");
+	int rc = rx_check(t, base, desc, n, "cgck_rx_post");
+	if (rc)
+		return rc;
+	cgck_ctx *c = thread_ctx();
+	if (!c)
+		return -ENODEV;
+	RxBurst &r = t.rxp[(t.rxp_head + t.rxp_count) & 1];
+	rx_fill(r, base, desc, n);
+	r.pend.seq = 0;
+	r.pend.rc = 0;
+	if (n && (rc = desc_host_post(c, base, bytes, r.d.data(), n, kRxFlags, r.o.data(), nullptr, r.m.data(),
+				      &r.pend)) < 0) {
+		char msg[256];
+		snprintf(msg, sizeof(msg), "%s", err_text());
+		return set_err(rc, "cgck_rx_post: %s", msg);
+	}
+	t.rxp_count++;
+	return (int)n;
+}
+
+extern "C" int cgck_rx_begin_posted(void)
+{
+	ThreadState &t = tstate();
+	if (t.rx_open)
+		return set_err(-EBUSY, "cgck_rx_begin_posted: an RX window is already open on this thread");
+	if (t.rxp_count == 0)
+		return set_err(-ENOENT, "cgck_rx_begin_posted: no burst posted");
+	RxBurst &r = t.rxp[t.rxp_head];
+	int rc = r.pend.seq ? burst_collect(t.ctx, &r.pend) : r.pend.rc;
+	if (rc) {
+		t.rxp_head ^= 1;
+		t.rxp_count--;
+		char msg[256];
+		snprintf(msg, sizeof(msg), "%s", err_text());
+		return set_err(rc, "cgck_rx_begin_posted: %s", msg);
+	}
+	return rx_open_on(t, r, true);
 }
 
 extern "C" int cgck_rx_end(void)
@@ -480,6 +580,11 @@ extern "C" int cgck_rx_end(void)
 	t.rx_open = false;
 	t.rx_n = 0;
 	t.rx_map = false;
+	if (t.rx_posted) {
+		t.rx_posted = false;
+		t.rxp_head ^= 1;
+		t.rxp_count--;
+	}
 	return (int)(t.stats[0] - t.rx_served0);
 }
 
@@ -499,96 +604,97 @@ extern "C" int cgck_tx_begin(void)
 	return 0;
 }
 
-extern "C" int cgck_tx_flush(void)
+namespace {
+
+// Both kinds in one batch: IP entries ask for the header checksum, L4
+// entries for the segment checksum; both read their fields as zero, as the
+// reference's callers have just stored them (ip_output.c:61, tcp_subr.c:75 /
+// gbtcp/tcp.c:426,436).
+constexpr uint32_t kTxFlags = CGCK_IP | CGCK_L4 | CGCK_ZERO_FIELDS;
+
+// Compute the values of f.q: when every entry lies in one registered range
+// (the transport's pool) the batch is described in place, as cgck_desc_host
+// of that range — the burst server when one is open on this context and the
+// flush fits it (left posted when pend is given: returns 1), else a launch;
+// otherwise each region is staged 16-byte aligned in pinned memory and
+// launched (computed at once: 0).  f.idx[i] is entry i's value in f.o.
+int tx_compute(cgck_ctx *c, TxFill &f, bool post)
 {
-	ThreadState &t = tstate();
-	if (!t.tx_open)
-		return set_err(-EINVAL, "cgck_tx_flush: no open window on this thread");
-	t.tx_open = false;
-	std::vector<TxEntry> &q = t.txq; // stays queued until the flush is done
-	t.tx_map = false;
+	const std::vector<TxEntry> &q = f.q;
 	const uint64_t n = q.size();
-	if (n == 0)
-		return 0;
-	cgck_ctx *c = thread_ctx();
-	if (!c)
-		return -ENODEV;
 	HIP_TRY(hipSetDevice(c->device));
-	// Every entry lies in registered memory (the window queues nothing
-	// else).  When they all lie in one range (the transport's pool) the
-	// batch is described in place, as cgck_desc_host of that range (the
-	// burst server when one is open on this context and the flush fits it,
-	// else a launch); otherwise each region is staged 16-byte aligned in
-	// pinned memory and launched.
 	RegRange reg{nullptr, nullptr, nullptr};
 	bool inplace = reg_find(q[0].ip, q[0].span, &reg);
 	for (uint64_t i = 1; inplace && i < n; i++)
 		inplace = q[i].ip >= reg.lo && q[i].ip + q[i].span <= reg.hi;
-	// Both kinds in one batch: IP entries ask for the header checksum, L4
-	// entries for the segment checksum; both read their fields as zero, as
-	// the reference's callers have just stored them (ip_output.c:61,
-	// tcp_subr.c:75 / gbtcp/tcp.c:426,436).
-	const uint32_t fl = CGCK_IP | CGCK_L4 | CGCK_ZERO_FIELDS;
 	int rc;
-	uint32_t *o;
 	// One descriptor per packet: a packet's header entry and its segment
 	// entry (queued one after the other by the finalisers, ip_output.c:61-64
 	// after tcp_output.c:416-418) share it — it covers the segment, and the
 	// kernel returns both the header checksum (over ip_hl * 4 bytes, which
 	// the queue checked equals the header call's length) and the segment's
 	// L4 checksum from one read of the frame.
-	t.txi.resize(n);
+	f.idx.resize(n);
 	if (inplace) {
-		t.txd.resize(n);
+		f.d.resize(n);
 		uint64_t m = 0;
 		for (uint64_t i = 0; i < n; i++) {
-			if (i > 0 && q[i].ip == q[i - 1].ip && (q[i].fo < 0) != (q[i - 1].fo < 0) && t.txi[i - 1] == m - 1 &&
-			    (i < 2 || t.txi[i - 2] != m - 1)) {
-				t.txi[i] = (uint32_t)(m - 1);
-				if (q[i].span > t.txd[m - 1].ip_len)
-					t.txd[m - 1].ip_len = (uint16_t)q[i].span;
+			if (i > 0 && q[i].ip == q[i - 1].ip && (q[i].fo < 0) != (q[i - 1].fo < 0) && f.idx[i - 1] == m - 1 &&
+			    (i < 2 || f.idx[i - 2] != m - 1)) {
+				f.idx[i] = (uint32_t)(m - 1);
+				if (q[i].span > f.d[m - 1].ip_len)
+					f.d[m - 1].ip_len = (uint16_t)q[i].span;
 				continue;
 			}
-			t.txi[i] = (uint32_t)m;
-			t.txd[m].frame_off = (uint64_t)(q[i].ip - reg.lo);
-			t.txd[m].l3_off = 0;
-			t.txd[m].ip_len = (uint16_t)q[i].span;
+			f.idx[i] = (uint32_t)m;
+			f.d[m].frame_off = (uint64_t)(q[i].ip - reg.lo);
+			f.d[m].l3_off = 0;
+			f.d[m].ip_len = (uint16_t)q[i].span;
 			m++;
 		}
-		t.txo.resize(m);
-		if ((rc = desc_host(c, reg.lo, (size_t)(reg.hi - reg.lo), t.txd.data(), m, fl, t.txo.data(), nullptr)))
-			return rc;
-		o = t.txo.data();
-	} else {
-		for (uint64_t i = 0; i < n; i++)
-			t.txi[i] = (uint32_t)i;
-		size_t bytes = 0; // staged bytes
-		for (const TxEntry &e : q)
-			bytes += (e.span + 15) & ~(size_t)15;
-		const size_t d_off = (bytes + 15) & ~(size_t)15;
-		const size_t o_off = (d_off + 12 * n + 15) & ~(size_t)15;
-		if ((rc = grow_host((void **)&c->h_stage, &c->h_stage_cap, o_off + 4 * n)))
-			return rc;
-		uint8_t *h = c->h_stage;
-		cgck_desc_t *d = (cgck_desc_t *)(h + d_off);
-		o = (uint32_t *)(h + o_off);
-		size_t at = 0;
-		for (uint64_t i = 0; i < n; i++) {
-			memcpy(h + at, q[i].ip, q[i].span);
-			d[i].frame_off = at;
-			d[i].l3_off = 0;
-			d[i].ip_len = (uint16_t)q[i].span;
-			at += (q[i].span + 15) & ~(size_t)15;
-		}
-		KParams p = {h, d, n, 0, 0, 0, fl, o, nullptr, nullptr, 0, nullptr};
-		if ((rc = run(c, p, 1500, c->stream)))
-			return rc;
-		HIP_TRY(hipStreamSynchronize(c->stream));
+		f.o.resize(m);
+		if (post)
+			return desc_host_post(c, reg.lo, (size_t)(reg.hi - reg.lo), f.d.data(), m, kTxFlags, f.o.data(),
+					      nullptr, nullptr, &f.pend);
+		return desc_host(c, reg.lo, (size_t)(reg.hi - reg.lo), f.d.data(), m, kTxFlags, f.o.data(), nullptr);
 	}
+	for (uint64_t i = 0; i < n; i++)
+		f.idx[i] = (uint32_t)i;
+	size_t bytes = 0; // staged bytes
+	for (const TxEntry &e : q)
+		bytes += (e.span + 15) & ~(size_t)15;
+	const size_t d_off = (bytes + 15) & ~(size_t)15;
+	const size_t o_off = (d_off + 12 * n + 15) & ~(size_t)15;
+	if ((rc = grow_host((void **)&c->h_stage, &c->h_stage_cap, o_off + 4 * n)))
+		return rc;
+	uint8_t *h = c->h_stage;
+	cgck_desc_t *d = (cgck_desc_t *)(h + d_off);
+	uint32_t *o = (uint32_t *)(h + o_off);
+	size_t at = 0;
+	for (uint64_t i = 0; i < n; i++) {
+		memcpy(h + at, q[i].ip, q[i].span);
+		d[i].frame_off = at;
+		d[i].l3_off = 0;
+		d[i].ip_len = (uint16_t)q[i].span;
+		at += (q[i].span + 15) & ~(size_t)15;
+	}
+	KParams p = {h, d, n, 0, 0, 0, kTxFlags, o, nullptr, nullptr, 0, nullptr};
+	if ((rc = run(c, p, 1500, c->stream)))
+		return rc;
+	HIP_TRY(hipStreamSynchronize(c->stream));
+	f.o.assign(o, o + n);
+	return 0;
+}
+
+// Write every queued field from the computed values; returns their count.
+int tx_write(TxFill &f)
+{
+	const std::vector<TxEntry> &q = f.q;
+	const uint64_t n = q.size();
 	for (uint64_t i = 0; i < n; i++) {
 		uint16_t v;
 		uint8_t *dst;
-		const uint32_t r = o[t.txi[i]];
+		const uint32_t r = f.o[f.idx[i]];
 		if (q[i].fo < 0) {
 			v = (uint16_t)r;
 			dst = q[i].ip + 10;
@@ -598,8 +704,86 @@ extern "C" int cgck_tx_flush(void)
 		}
 		memcpy(dst, &v, 2);
 	}
-	q.clear();
+	f.q.clear();
 	return (int)n;
+}
+
+// Close the window and move its queue into f.
+void tx_take(ThreadState &t, TxFill &f)
+{
+	t.tx_open = false;
+	t.tx_map = false;
+	f.q.swap(t.txq);
+	t.txq.clear();
+}
+
+} // namespace
+
+extern "C" int cgck_tx_flush(void)
+{
+	ThreadState &t = tstate();
+	if (!t.tx_open)
+		return set_err(-EINVAL, "cgck_tx_flush: no open window on this thread");
+	tx_take(t, t.txs);
+	if (t.txs.q.empty())
+		return 0;
+	cgck_ctx *c = thread_ctx();
+	if (!c)
+		return -ENODEV;
+	int rc = tx_compute(c, t.txs, false);
+	if (rc < 0) {
+		t.txs.q.clear();
+		return rc;
+	}
+	return tx_write(t.txs);
+}
+
+// Pipelined form: post the window's fill and return; cgck_tx_complete
+// (before the transport hands these slots to the NIC) waits for it and
+// writes the fields.
+extern "C" int cgck_tx_post(void)
+{
+	ThreadState &t = tstate();
+	if (!t.tx_open)
+		return set_err(-EINVAL, "cgck_tx_post: no open window on this thread");
+	if (t.txp_count == 2) {
+		t.tx_open = false;
+		t.txq.clear();
+		return set_err(-EBUSY, "cgck_tx_post: two fills already posted and not yet completed");
+	}
+	TxFill &f = t.txp[(t.txp_head + t.txp_count) & 1];
+	tx_take(t, f);
+	f.pend.seq = 0;
+	f.pend.rc = 0;
+	const int n = (int)f.q.size();
+	if (n) {
+		cgck_ctx *c = thread_ctx();
+		if (!c)
+			return -ENODEV;
+		int rc = tx_compute(c, f, true);
+		if (rc < 0) {
+			f.q.clear();
+			return rc;
+		}
+	}
+	t.txp_count++;
+	return n;
+}
+
+extern "C" int cgck_tx_complete(void)
+{
+	ThreadState &t = tstate();
+	if (t.txp_count == 0)
+		return 0;
+	TxFill &f = t.txp[t.txp_head];
+	t.txp_head ^= 1;
+	t.txp_count--;
+	const int rc = f.pend.seq ? burst_collect(t.ctx, &f.pend) : f.pend.rc;
+	if (rc < 0) {
+		f.q.clear();
+		return rc;
+	}
+	return tx_write(f);
 }
 
 // --------------------------------------------------------------------------

@@ -25,7 +25,8 @@ namespace cgck {
 // 82.7 % with none).
 constexpr int kGrpStage = 2048;
 
-template <int G, int S, int U, bool DESC, bool NT>
+// LDSD: p.desc points at descriptors staged in LDS (the burst server's slices).
+template <int G, int S, int U, bool DESC, bool NT, bool LDSD = false>
 __device__ __forceinline__ void cksum_body(const KParams &p, uint32_t bid, uint32_t nb)
 {
 	__shared__ uint32_t so[kGrpStage];
@@ -59,7 +60,10 @@ __device__ __forceinline__ void cksum_body(const KParams &p, uint32_t bid, uint3
 		int nch[U];
 #pragma unroll
 		for (int u = 0; u < U; ++u) {
-			pk[u] = get_pkt<DESC>(p, blk * PPB + (uint64_t)u * GPB + gib);
+			if constexpr (LDSD)
+				pk[u] = get_pkt_lds(p, blk * PPB + (uint64_t)u * GPB + gib);
+			else
+				pk[u] = get_pkt<DESC>(p, blk * PPB + (uint64_t)u * GPB + gib);
 			const uint64_t a0 = pk[u].a0;
 			// Bytes read: the region, or (drop-in udp_cksum, host-guaranteed)
 			// at least the 20 header bytes the pseudo-header needs.
@@ -214,8 +218,9 @@ __global__ __launch_bounds__(256) void cksum_kernel(KParams p)
 // host-resident batches (RX bursts, drop-in calls) without a launch or a
 // stream synchronisation per batch.  The host writes a request block
 // (BurstReq, descriptors, packet bytes) into host-coherent staging and stores
-// req = seq | n << 32; thread 0 of every workgroup polls it with relaxed
-// system-scope loads.  W = burst_wgs(n, K) workgroups serve the request:
+// req = seq | n << 32; thread 0 of workgroup 0 polls it with relaxed
+// system-scope loads and relays it to the others.  W = burst_wgs(n, K)
+// workgroups serve the request:
 //  * W == 1 (up to kBurstOneWG packets: a drop-in call, a small burst):
 //    workgroup 0 copies the block into device scratch with one wide read
 //    (tools/pingpong: every dependent host round trip costs ~1.3 us, so the
@@ -223,14 +228,30 @@ __global__ __launch_bounds__(256) void cksum_kernel(KParams p)
 //    bytes) and runs the group body over the copy, or over registered ring
 //    memory in place;
 //  * W > 1: workgroup j reads the header and its own slice of the
-//    descriptors (d_off is fixed, so both in one round trip) into scratch,
+//    descriptors (d_off is fixed, so both in one round trip) into its LDS,
 //    then the packet bytes where they lie (registered memory, or the block):
-//    the burst's host reads spread over W CUs, as a launch's would.
+//    the burst's host reads spread over W CUs, as a launch's would.  No byte
+//    of a slice passes through cached device memory.
+// Before any packet load or store every serving workgroup checks the header
+// and each of its descriptors: inside the block (staged bytes) or inside the
+// request's `range` (registered memory read in place); a refused request
+// counts in bad_req and its host call fails with -EIO.
 // Each serving workgroup writes its outputs to host-coherent memory and
 // publishes done[j] after a system-scope release.  Every poll loop is
 // bounded: a workgroup exits on `stop`, or after idle_ticks of the 100 MHz
 // real-time counter without a request (the host relaunches the server when
 // it finds a workgroup gone), so no launch outlives its context.
+//
+// Ordering of the request block: the host's block stores precede its `req`
+// store (x86 TSO, a release store); the block, the mailbox and the packet
+// bytes are system memory, which the GPU maps uncached (MTYPE UC: no L2 or L1
+// copy), so every read of them is a PCIe read served coherently by the host.
+// A worker's block reads are issued after its relay load returned, the relay
+// was stored after the leader's mailbox load returned the new seq, and that
+// load was served after the host's block stores were visible: each read is
+// causally after the block was written.  The system-scope acquire each
+// workgroup executes before its reads drops its CU's L1 and its XCD's L2
+// copies of the device scratch the whole-block path rewrites.
 // --------------------------------------------------------------------------
 
 __device__ __forceinline__ uint32_t sys_load(const uint32_t *p)
@@ -248,29 +269,50 @@ __device__ __forceinline__ uint64_t sys_relaxed64(const uint64_t *p)
 	return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// The group body over a request's packets [lo, hi) (block 0 of 1).
-__device__ __forceinline__ void burst_body(const BurstReq &h, const uint8_t *scratch, uint32_t lo, uint32_t hi,
+// The group body over a request's packets [lo, hi) (block 0 of 1); desc is
+// packet lo's descriptor (in LDS when LDSD).
+template <bool LDSD>
+__device__ __forceinline__ void burst_body(const BurstReq &h, const uint32_t *desc, uint32_t lo, uint32_t hi,
 					   uint32_t *out, uint32_t *meta, uint8_t *verdict, const void *zero,
 					   const uint8_t *base)
 {
-	KParams p = {base, reinterpret_cast<const cgck_desc_t *>(scratch + h.d_off) + lo,
-		     hi - lo, 0, 0, 0, h.flags, out ? out + lo : nullptr, verdict ? verdict + lo : nullptr, nullptr, 0, zero,
-		     meta + lo};
+	KParams p = {base, reinterpret_cast<const cgck_desc_t *>(desc), hi - lo, 0, 0, 0, h.flags,
+		     out ? out + lo : nullptr, verdict ? verdict + lo : nullptr, nullptr, 0, zero, meta + lo};
 	if (h.max_len <= 80)
-		cksum_body<4, 2, 4, true, false>(p, 0, 1);
+		cksum_body<4, 2, 4, true, false, LDSD>(p, 0, 1);
 	else
-		cksum_body<16, 6, 4, true, false>(p, 0, 1);
+		cksum_body<16, 6, 4, true, false, LDSD>(p, 0, 1);
 }
 
-// Device-memory command word of a server launch (the leader's relay to the
-// other workgroups): seq | n << 32; kBurstExit << 32 | epoch: leave.  Zeroed
-// by the host before every launch (seq 0 is never posted), and an exit word
-// counts only with this launch's epoch, so a word left over from an earlier
-// launch over the same memory can neither end nor feed this one.  The word
-// is uncached device memory (hipDeviceMallocUncached): an sc1 poll of a
-// cached line is served by the polling XCD's L2, which another XCD's store
-// does not refresh (the cached word: one wide request in a suite run was not
-// served in 2 s).
+// A request header the server can serve: the count it was told, inside the
+// context's capacity and block, descriptors where the host puts them, staged
+// bytes inside the block.
+__device__ __forceinline__ bool burst_hdr_ok(const BurstReq &h, uint32_t n, uint32_t max_pkts, uint32_t cap)
+{
+	return h.n == n && h.n <= max_pkts && h.bytes <= cap && h.d_off == sizeof(BurstReq) &&
+	       (uint64_t)h.d_off + 12ull * h.n <= h.bytes && (h.base ? h.range != 0 : h.p_off <= h.bytes);
+}
+
+// Bytes a descriptor may reach from the packet base: the request's range in
+// place, the staged bytes of the block otherwise (burst_hdr_ok held).
+__device__ __forceinline__ uint64_t burst_limit(const BurstReq &h)
+{
+	return h.base ? h.range : (uint64_t)(h.bytes - h.p_off);
+}
+
+// Descriptors of one slice pass staged in LDS (12 KiB): a slice of more
+// packets runs in passes.
+constexpr uint32_t kSliceLds = 1024;
+
+// Device-memory command words of a server launch (the leader's relay to the
+// other workgroups): dcmd[seq & 1] = seq | n << 32 for every request, in
+// order (a wide one before the leader serves its slice, a one-workgroup one
+// after); dcmd[2] = kBurstExit << 32 | epoch: leave.  Zeroed by the host
+// before every launch (seq 0 is never posted), and an exit word counts only
+// with this launch's epoch.  The words are uncached device memory
+// (hipDeviceMallocUncached): an sc1 poll of a cached line is served by the
+// polling XCD's L2, which another XCD's store does not refresh (the cached
+// word: one wide request in a suite run was not served in 2 s).
 constexpr uint32_t kBurstExit = 0xffffffffu;
 
 __device__ __forceinline__ uint64_t relay_load(const uint64_t *p)
@@ -278,119 +320,136 @@ __device__ __forceinline__ uint64_t relay_load(const uint64_t *p)
 	return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-__global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const uint8_t *req, uint8_t *scratch,
-							   uint8_t *resp, uint64_t *dcmd, const void *zero,
+__device__ __forceinline__ void relay_store(uint64_t *p, uint64_t v)
+{
+	__hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const uint8_t *req0, uint8_t *scratch,
+							   uint8_t *resp0, uint64_t *dcmd, const void *zero,
 							   uint32_t cap, uint32_t max_pkts, uint32_t per_wg,
 							   uint32_t start_seq, uint32_t epoch, uint32_t opts)
 {
-	__shared__ uint32_t cmd, cmd_n; // cmd: 1 run the pending request, 2 exit, 3 already served
+	// cmd: 1 serve the request, 2 exit, 3 already served by an earlier launch
+	__shared__ uint32_t cmd, cmd_n, cmd_seq;
 	__shared__ uint4 hdr_w[4];
+	__shared__ uint32_t sdesc[3 * kSliceLds];
 	const int t = threadIdx.x;
 	const uint32_t j = blockIdx.x, K = gridDim.x;
+	const uint32_t rslot = burst_resp_slot(max_pkts);
 	uint32_t last = start_seq; // the last request seen (thread 0)
-	bool first = true;         // thread 0: no request seen since the launch
-	const uint4 *src = reinterpret_cast<const uint4 *>(req);
-	uint4 *dst = reinterpret_cast<uint4 *>(scratch);
+	// thread 0: requests left whose done[j] is checked first — after a relaunch
+	// the (up to two) pending requests may have been served in part already
+	uint32_t recheck = 2;
 	for (;;) {
 		if (t == 0) {
 			const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
 			const uint64_t idle = box->idle_ticks;
 			uint32_t c = 0, n = 0;
 			if (j == 0) {
-				// The leader polls the host mailbox.  Only one workgroup
-				// does: K pollers of one host line cost every request
-				// ~13 us at K = 16 and ~27 us at K = 32 (tools/txburst
-				// dropin, one in_cksum through a server of K workgroups).
+				// The leader polls the host mailbox slot of the next seq.
+				// Only one workgroup does: K pollers of one host line cost
+				// every request ~13 us at K = 16 and ~27 us at K = 32
+				// (tools/txburst dropin, one in_cksum through a server of K
+				// workgroups).  The leader serves every request, so the host
+				// cannot post past the one it waits for.
+				const uint32_t want = burst_next(last);
 				while (c == 0) {
 					// relaxed: an acquire load would invalidate the caches every poll
-					const uint64_t r = sys_relaxed64(&box->req);
+					const uint64_t r = sys_relaxed64(&box->req[want & 1]);
 					if (sys_relaxed(&box->stop))
 						c = 2;
-					else if ((uint32_t)r != last)
-						c = 1, last = (uint32_t)r, n = (uint32_t)(r >> 32);
+					else if ((uint32_t)r == want)
+						c = 1, last = want, n = (uint32_t)(r >> 32);
 					else if (__builtin_amdgcn_s_memrealtime() - t0 > idle)
 						c = 2;
 					else
 						__builtin_amdgcn_s_sleep(4);
 				}
-				// relay a wide request (and the exit) to the others now;
-				// a small one after it is served (it keeps their idle
-				// bound from running out)
-				if (K > 1 && (c == 2 || burst_wgs(n, K, per_wg) > 1))
-					__hip_atomic_store(dcmd, c == 2 ? (uint64_t)kBurstExit << 32 | epoch
-									: (uint64_t)last | (uint64_t)n << 32,
-							   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+				// relay a wide request (and the exit) to the others now; a
+				// small one after it is served (it keeps their idle bound
+				// from running out)
+				if (K > 1 && c == 2)
+					relay_store(dcmd + 2, (uint64_t)kBurstExit << 32 | epoch);
+				else if (K > 1 && burst_wgs(n, K, per_wg) > 1)
+					relay_store(dcmd + (last & 1), (uint64_t)last | (uint64_t)n << 32);
 			} else {
 				// The others poll the leader's relay in device memory, with
 				// a bound of their own (four idle periods) in case it never
-				// comes.
+				// comes.  A slot already holding a later request of its
+				// parity means the host collected the one wanted, so this
+				// workgroup was not part of it: step over it.
 				while (c == 0) {
-					const uint64_t r = relay_load(dcmd);
-					if ((uint32_t)(r >> 32) == kBurstExit) {
-						if ((uint32_t)r == epoch)
-							c = 2;
-						else
-							__builtin_amdgcn_s_sleep(2); // an earlier launch's
-					} else if ((uint32_t)r != last && (uint32_t)r != 0)
-						c = 1, last = (uint32_t)r, n = (uint32_t)(r >> 32);
+					const uint32_t want = burst_next(last);
+					const uint64_t e = relay_load(dcmd + 2);
+					const uint64_t r = relay_load(dcmd + (want & 1));
+					if ((uint32_t)(e >> 32) == kBurstExit && (uint32_t)e == epoch)
+						c = 2;
+					else if ((uint32_t)r == want)
+						c = 1, last = want, n = (uint32_t)(r >> 32);
+					else if ((uint32_t)r != 0 && (int32_t)((uint32_t)r - want) > 0)
+						last = want; // not ours: on to the next seq
 					else if (__builtin_amdgcn_s_memrealtime() - t0 > 4 * idle)
 						c = 2;
 					else
 						__builtin_amdgcn_s_sleep(2);
 				}
 			}
-			// A relaunch after a drain re-posts the pending request; a
-			// slice the previous launch already served is not served
-			// twice (an in-place store is not idempotent without
-			// ZERO_FIELDS).
-			if (c == 1 && first && sys_relaxed(&box->done[j]) == last)
-				c = 3;
-			if (c == 1)
-				first = false;
+			// A relaunch after a drain re-posts the pending requests; a
+			// slice the previous launch already served is not served twice
+			// (an in-place store is not idempotent without ZERO_FIELDS).
+			if (c == 1 && recheck) {
+				--recheck;
+				if ((int32_t)(sys_relaxed(&box->done[j]) - last) >= 0)
+					c = 3;
+			}
 			cmd = c;
 			cmd_n = n;
+			cmd_seq = last;
 		}
 		__syncthreads();
 		if (cmd == 2)
 			break;
-		const uint32_t n = cmd_n;
+		const uint32_t n = cmd_n, seq = cmd_seq;
 		const uint32_t W = burst_wgs(n, K, per_wg);
 		if (j >= W || cmd == 3) {
+			if (t == 0 && j == 0 && K > 1 && W == 1)
+				relay_store(dcmd + (seq & 1), (uint64_t)seq | (uint64_t)n << 32);
 			__syncthreads(); // cmd / cmd_n are rewritten by the next poll
 			continue;
 		}
+		const uint8_t *req = req0 + (size_t)(seq & 1) * cap;
+		uint8_t *resp = resp0 + (size_t)(seq & 1) * rslot;
+		const uint4 *src = reinterpret_cast<const uint4 *>(req);
+		uint4 *dst = reinterpret_cast<uint4 *>(scratch);
 #if CGCK_LAB
 		uint64_t lab_t0 = __builtin_amdgcn_s_memrealtime(), lab_t1 = 0, lab_t2 = 0;
+		uint64_t lab_c1 = 0;
 #endif
-		// One system-scope acquire: no line of an earlier request, or of an
-		// earlier burst in a registered ring, is served from the cache.
+		// One system-scope acquire: no line of the scratch copy of an
+		// earlier request is served from this CU's L1 or this XCD's L2.
 		__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
 		bool ok;
+		// opts bits 1 / 2 (lab A/B, results then partial): no verdict stores
+		// / no stores at all
+		uint8_t *ver = (opts & 6) ? nullptr : resp + burst_ver_off(n);
+		uint32_t *o32 = (opts & 4) ? nullptr : reinterpret_cast<uint32_t *>(resp);
+		uint32_t *meta = reinterpret_cast<uint32_t *>(resp + burst_meta_off(n));
+		const BurstReq &h = *reinterpret_cast<const BurstReq *>(hdr_w);
 		// opts bit 0 (lab A/B): a one-workgroup request takes the slice path
 		// too (header and descriptors only, packets read where they lie)
-		const bool whole = W == 1 && !(opts & 1);
-		if (whole) {
+		if (W == 1 && !(opts & 1)) {
 			// the first kBurstFirst bytes of the block in one round trip:
 			// plain 16-byte loads, so every wave's read leaves as whole-line
 			// requests
-			constexpr int NW = kBurstFirst / 16 / 256;
-			uint4 v[NW];
-#pragma unroll
-			for (int w = 0; w < NW; ++w)
-				v[w] = src[w * 256 + t];
-#pragma unroll
-			for (int w = 0; w < NW; ++w)
-				dst[w * 256 + t] = v[w];
+			static_assert(kBurstFirst == 2 * 16 * 256, "two 16-byte loads per thread");
+			const uint4 v0 = src[t], v1 = src[256 + t];
+			dst[t] = v0;
+			dst[256 + t] = v1;
 			if (t < 4)
-				hdr_w[t] = v[0];
+				hdr_w[t] = v0;
 			__syncthreads();
-			const BurstReq &h = *reinterpret_cast<const BurstReq *>(hdr_w);
-			// The block is host-written: a header or descriptor that does not
-			// fit the block the context allocated is refused (counted in
-			// bad_req, the host's call fails) instead of steering the loads
-			// below out of it.
-			ok = h.n == n && h.n <= max_pkts && h.bytes <= cap && h.d_off == sizeof(BurstReq) &&
-			     (uint64_t)h.d_off + 12ull * h.n <= h.bytes && (h.base || h.p_off <= h.bytes);
+			ok = burst_hdr_ok(h, n, max_pkts, cap);
 			const uint32_t chunks = ok ? (h.bytes + 15) / 16 : 0;
 			// the rest of a larger block, 16 loads in flight per thread (64 KiB
 			// a round trip)
@@ -408,71 +467,77 @@ __global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const 
 						dst[i] = x[k];
 				}
 			}
-		} else {
-			// header and this workgroup's descriptors [lo, hi) in one round
-			// trip, as dwords (a slice starts on a 4-byte boundary); the
-			// count comes from the poll, so the slice does not wait for the
-			// header
-			const uint32_t lo = (uint32_t)((uint64_t)n * j / W), hi = (uint32_t)((uint64_t)n * (j + 1) / W);
-			const uint32_t nd = (n <= max_pkts ? 3 * (hi - lo) : 0);
-			const uint32_t *sd = reinterpret_cast<const uint32_t *>(req + sizeof(BurstReq)) + 3 * lo;
-			uint32_t *dd = reinterpret_cast<uint32_t *>(scratch + sizeof(BurstReq)) + 3 * lo;
-			uint4 hv = t < 4 ? src[t] : make_uint4(0, 0, 0, 0);
-			for (uint32_t i = t; i < nd; i += 4 * 256) {
-				uint32_t x[4];
-#pragma unroll
-				for (int k = 0; k < 4; ++k)
-					x[k] = i + k * 256 < nd ? sd[i + k * 256] : 0u;
-#pragma unroll
-				for (int k = 0; k < 4; ++k)
-					if (i + k * 256 < nd)
-						dd[i + k * 256] = x[k];
-			}
-			if (t < 4)
-				hdr_w[t] = hv;
+			// scratch stores visible to the workgroup (its waves share one
+			// CU's L1: workgroup scope)
+			__builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
 			__syncthreads();
-			const BurstReq &h = *reinterpret_cast<const BurstReq *>(hdr_w);
-			ok = h.n == n && h.n <= max_pkts && h.bytes <= cap && h.d_off == sizeof(BurstReq) &&
-			     (uint64_t)h.d_off + 12ull * h.n <= h.bytes && (h.base || h.p_off <= h.bytes);
-		}
-		// scratch stores visible to the workgroup (its waves share one CU's
-		// L1: workgroup scope)
-		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-		__syncthreads();
-		__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-		const BurstReq &h = *reinterpret_cast<const BurstReq *>(hdr_w);
-		const uint32_t lo = W == 1 ? 0u : (uint32_t)((uint64_t)n * j / W);
-		const uint32_t hi = W == 1 ? n : (uint32_t)((uint64_t)n * (j + 1) / W);
-		if (ok && !h.base) // packet bytes in the block: every descriptor inside it
-			for (uint32_t i = lo + t; i < hi; i += 256) {
-				const cgck_desc_t *d = reinterpret_cast<const cgck_desc_t *>(scratch + h.d_off) + i;
-				uint32_t fo_lo, fo_hi, w2;
-				__builtin_memcpy(&fo_lo, reinterpret_cast<const uint8_t *>(d), 4);
-				__builtin_memcpy(&fo_hi, reinterpret_cast<const uint8_t *>(d) + 4, 4);
-				__builtin_memcpy(&w2, reinterpret_cast<const uint8_t *>(d) + 8, 4);
-				const uint64_t end = ((uint64_t)fo_hi << 32 | fo_lo) + (w2 & 0xffffu) + (w2 >> 16);
-				ok = ok && fo_hi == 0 && end + h.p_off <= h.bytes;
+			__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+			const uint32_t *sd = reinterpret_cast<const uint32_t *>(scratch + sizeof(BurstReq));
+			if (ok) {
+				const uint64_t limit = burst_limit(h);
+				for (uint32_t i = t; i < n; i += 256)
+					ok = ok && desc_inside(gbl(sd)[3 * i], gbl(sd)[3 * i + 1], gbl(sd)[3 * i + 2], limit);
 			}
-		ok = __syncthreads_and(ok);
+			ok = __syncthreads_and(ok);
 #if CGCK_LAB
-		lab_t1 = __builtin_amdgcn_s_memrealtime();
-		const uint64_t lab_c1 = __builtin_amdgcn_s_memtime();
+			lab_t1 = __builtin_amdgcn_s_memrealtime();
+			lab_c1 = __builtin_amdgcn_s_memtime();
 #endif
-		if (ok) {
-			// W == 1 reads staged packet bytes from its scratch copy; wider
-			// requests read them from the block in host memory
-			const uint8_t *base = h.base ? reinterpret_cast<const uint8_t *>(h.base)
-					      : (whole ? scratch : req) + h.p_off;
-			// opts bits 1 / 2 (lab A/B, results then partial): no verdict stores
-			// / no stores at all
-			uint8_t *ver = (opts & 6) ? nullptr : resp + burst_ver_off(n);
-			uint32_t *o32 = (opts & 4) ? nullptr : reinterpret_cast<uint32_t *>(resp);
-			burst_body(h, scratch, lo, hi, o32, reinterpret_cast<uint32_t *>(resp + burst_meta_off(n)), ver,
-				   zero, base);
-			if (opts & 8) // lab: the body a second time (is a pass cold-start bound?)
-				burst_body(h, scratch, lo, hi, o32, reinterpret_cast<uint32_t *>(resp + burst_meta_off(n)),
-					   ver, zero, base);
-		} else if (t == 0) {
+			if (ok) {
+				// staged packet bytes are read from the scratch copy
+				const uint8_t *base = h.base ? reinterpret_cast<const uint8_t *>(h.base) : scratch + h.p_off;
+				burst_body<false>(h, sd, 0, n, o32, meta, ver, zero, base);
+				if (opts & 8) // lab: the body a second time (is a pass cold-start bound?)
+					burst_body<false>(h, sd, 0, n, o32, meta, ver, zero, base);
+			}
+		} else {
+			// Slice [lo, hi) in passes of up to kSliceLds descriptors: the
+			// header (first pass) and the pass's descriptors in one round
+			// trip, as dwords (a slice starts on a 4-byte boundary), into
+			// LDS; the count comes from the poll, so the slice does not
+			// wait for the header.
+			const uint32_t lo = (uint32_t)((uint64_t)n * j / W), hi = (uint32_t)((uint64_t)n * (j + 1) / W);
+			const uint32_t *sd = reinterpret_cast<const uint32_t *>(req + sizeof(BurstReq));
+			ok = n <= max_pkts;
+			for (uint32_t c0 = lo; ok && c0 < hi; c0 += kSliceLds) {
+				const uint32_t c1 = hi - c0 < kSliceLds ? hi : c0 + kSliceLds;
+				const uint32_t nd = 3 * (c1 - c0);
+				const uint4 hv = (c0 == lo && t < 4) ? src[t] : make_uint4(0, 0, 0, 0);
+				for (uint32_t i = t; i < nd; i += 4 * 256) {
+					uint32_t x[4];
+#pragma unroll
+					for (int k = 0; k < 4; ++k)
+						x[k] = i + k * 256 < nd ? gbl(sd)[3 * c0 + i + k * 256] : 0u;
+#pragma unroll
+					for (int k = 0; k < 4; ++k)
+						if (i + k * 256 < nd)
+							sdesc[i + k * 256] = x[k];
+				}
+				if (c0 == lo && t < 4)
+					hdr_w[t] = hv;
+				__syncthreads();
+				ok = burst_hdr_ok(h, n, max_pkts, cap);
+				if (ok) {
+					const uint64_t limit = burst_limit(h);
+					for (uint32_t i = t; i < c1 - c0; i += 256)
+						ok = ok && desc_inside(sdesc[3 * i], sdesc[3 * i + 1], sdesc[3 * i + 2], limit);
+				}
+				ok = __syncthreads_and(ok);
+#if CGCK_LAB
+				if (c0 == lo) {
+					lab_t1 = __builtin_amdgcn_s_memrealtime();
+					lab_c1 = __builtin_amdgcn_s_memtime();
+				}
+#endif
+				if (!ok)
+					break;
+				const uint8_t *base = h.base ? reinterpret_cast<const uint8_t *>(h.base) : req + h.p_off;
+				burst_body<true>(h, sdesc, c0, c1, o32, meta, ver, zero, base);
+				__syncthreads(); // the next pass rewrites sdesc
+			}
+		}
+		if (!ok && t == 0) {
+			__hip_atomic_store(&box->refused[seq & 1], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 			__hip_atomic_fetch_add(&box->bad_req, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 		}
 #if CGCK_LAB
@@ -496,10 +561,9 @@ __global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const 
 		}
 #endif
 		if (t == 0) {
-			__hip_atomic_store(&box->done[j], last, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+			__hip_atomic_store(&box->done[j], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 			if (j == 0 && K > 1 && W == 1)
-				__hip_atomic_store(dcmd, (uint64_t)last | (uint64_t)n << 32, __ATOMIC_RELAXED,
-						   __HIP_MEMORY_SCOPE_SYSTEM);
+				relay_store(dcmd + (seq & 1), (uint64_t)seq | (uint64_t)n << 32);
 		}
 	}
 	if (t == 0)
@@ -510,7 +574,7 @@ hipError_t launch_burst_server(BurstBox *box, const uint8_t *req, uint8_t *scrat
 			       const void *zero, uint32_t cap, uint32_t max_pkts, uint32_t wgs, uint32_t per_wg,
 			       uint32_t start_seq, uint32_t epoch, uint32_t opts, hipStream_t st)
 {
-	hipError_t e = hipMemsetAsync(dcmd, 0, sizeof(uint64_t), st);
+	hipError_t e = hipMemsetAsync(dcmd, 0, 3 * sizeof(uint64_t), st);
 	if (e != hipSuccess)
 		return e;
 	hipLaunchKernelGGL(burst_server_kernel, dim3(wgs), dim3(256), 0, st, box, req, scratch, resp, dcmd, zero, cap,

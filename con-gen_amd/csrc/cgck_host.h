@@ -9,6 +9,19 @@
 
 #include "cgck_internal.h"
 
+namespace cgck {
+// A request left posted on the burst server (desc_host_post): where its
+// outputs go when it is collected (burst_collect) and its result.
+struct BurstPending {
+	uint32_t seq; // 0: not pending
+	uint32_t n;
+	uint64_t range;
+	uint32_t *out, *meta;
+	uint8_t *verdict;
+	int rc;
+};
+} // namespace cgck
+
 struct cgck_ctx {
 	int device;
 	int num_cus;
@@ -57,7 +70,9 @@ struct cgck_ctx {
 	uint32_t bwgs;              // workgroups of the server (K)
 	uint32_t bper;              // packets per workgroup of a wide request
 	uint32_t bbad;              // bbox->bad_req as last seen
-	uint32_t bseq;
+	uint32_t bseq;              // the last request posted
+	uint32_t bdone;             // the last request known complete (a relaunch serves the ones after it)
+	cgck::BurstPending *bslot[2]; // a posted request not yet collected, per slot
 	hipStream_t bstream; // the server's own stream (it stays resident)
 };
 
@@ -88,6 +103,14 @@ int run(cgck_ctx *c, const KParams &p, uint32_t len_hint, hipStream_t st);
 // meta: kFlagRx's per-packet words (nullptr otherwise).
 int desc_host(cgck_ctx *c, void *base, size_t bytes, const cgck_desc_t *desc, uint64_t n, uint32_t flags,
 	      uint32_t *out, uint8_t *verdict, uint32_t *meta = nullptr);
+// The same, left posted when the burst server takes it: returns 1 and *pend
+// records the request (burst_collect waits for it and copies its outputs to
+// out / verdict / meta, which must stay valid until then); 0 when it was
+// computed at once (no server, or it does not fit); a negative errno.  A
+// later request on the context that needs the slot collects it first.
+int desc_host_post(cgck_ctx *c, void *base, size_t bytes, const cgck_desc_t *desc, uint64_t n, uint32_t flags,
+		   uint32_t *out, uint8_t *verdict, uint32_t *meta, BurstPending *pend);
+int burst_collect(cgck_ctx *c, BurstPending *pend);
 
 // Staging path of one region for the drop-in symbols (burst server when open,
 // else a launch on the context stream and a synchronisation).

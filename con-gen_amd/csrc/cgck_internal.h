@@ -67,27 +67,39 @@ struct KParams {
 };
 
 // Mailbox of the burst server (cgck_group.hip), in host-coherent pinned
-// memory.  The host writes a request block (BurstReq + descriptors + packet
-// bytes) into its staging, then `req` = seq | n << 32 in one 64-bit release
-// store (seq never 0); the server's leader workgroup polls it and relays a
-// wide request to the others through device memory, so each learns the
-// packet count, and with it its share, from its poll.  Workgroup j of the W = burst_wgs(n, K)
-// that serve a request answers with done[j] = seq (release) once its outputs
-// are visible.
+// memory.  Two request slots, so one request can be in flight while the host
+// posts the next (the pipelined RX / TX windows): request seq lives in slot
+// seq & 1 — its block at bstage + (seq & 1) * cap, its outputs at bresp +
+// (seq & 1) * burst_resp_slot(max_pkts), its mailbox word req[seq & 1] =
+// seq | n << 32, stored (release) after the block.  Seqs run 1, 2, ... by
+// burst_next (never 0, parity alternating through the wrap), and the server
+// serves them strictly in that order: its leader workgroup polls the slot of
+// the seq after the last it served and relays each request to the others
+// through device memory, so each learns the packet count, and with it its
+// share, from its poll.  Workgroup j of the W = burst_wgs(n, K) that serve a
+// request answers with done[j] = seq (release) once its outputs are visible;
+// a workgroup that refuses its slice (burst_hdr_ok / desc_inside) first
+// stores refused[seq & 1] = seq.
 constexpr uint32_t kBurstMaxWG = 32; // workgroups of a server (K)
 constexpr uint32_t kBurstOneWG = 64; // packets one workgroup serves alone (one wide read of the block)
 constexpr uint32_t kBurstPerWG = 64; // packets per workgroup of a wider request (default)
 struct BurstBox {
-	uint64_t req;        // host -> device: seq | n << 32
+	uint64_t req[2];     // host -> device: seq | n << 32 of the request in slot seq & 1
 	uint32_t stop;       // host -> device: exit now
-	uint32_t bad_req;    // device -> host: requests refused by the server's block check
+	uint32_t bad_req;    // device -> host: slices refused by the server's checks (a count)
 	uint64_t idle_ticks; // 100 MHz ticks without a request before the server exits
+	uint32_t refused[2]; // device -> host: seq of the last refused request in each slot
 	uint64_t lab_cyc;    // lab build: workgroup 0's shader clocks (s_memtime) over the compute phase
-	uint64_t lab_t[4];   // lab build: workgroup 0's s_memrealtime at seen / read / computed / published
+	uint32_t pad[4];
 	uint32_t done[kBurstMaxWG]; // device -> host: the last request workgroup j served
 	uint8_t alive[kBurstMaxWG]; // host sets 1 at launch; workgroup j clears its byte on exit
+	uint64_t lab_t[4];   // lab build: workgroup 0's s_memrealtime at seen / read / computed / published
 };
-static_assert(sizeof(BurstBox) == 64 + 5 * kBurstMaxWG, "mailbox line, the done lines, the alive lines");
+static_assert(sizeof(BurstBox) == 64 + 5 * kBurstMaxWG + 32, "mailbox line, the done lines, the alive lines, lab");
+
+// The seq after s: 1, 2, ..., 0xfffffffe, 1, ...: never 0 (the relay's
+// "nothing posted"), and s & 1 alternates through the wrap.
+__host__ __device__ constexpr uint32_t burst_next(uint32_t s) { return s >= 0xfffffffeu ? 1u : s + 1u; }
 
 // Workgroups that serve a request of n packets on a server of K with `per`
 // packets per workgroup: one up to kBurstOneWG packets (it reads the whole
@@ -117,7 +129,8 @@ struct BurstReq {
 	uint64_t base;    // device view of packets read in place (registered memory); 0: in the block
 	uint32_t d_off;   // descriptors: offset in the block
 	uint32_t p_off;   // packet bytes (base == 0): offset in the block
-	uint32_t pad[8];
+	uint64_t range;   // base != 0: bytes readable from base; the server refuses a descriptor past it
+	uint32_t pad[6];
 };
 static_assert(sizeof(BurstReq) == 64, "one header line");
 constexpr uint32_t kBurstFirst = 8192;
@@ -129,9 +142,17 @@ constexpr uint32_t kBurstFirst = 8192;
 // one-packet request took 36.8 us instead of 9.5: tools/txburst dropin.)
 __host__ __device__ constexpr uint32_t burst_meta_off(uint32_t n) { return (4 * n + 63) & ~63u; }
 __host__ __device__ constexpr uint32_t burst_ver_off(uint32_t n) { return 2 * burst_meta_off(n); }
-// dcmd: 8 bytes of device memory, the leader's relay word (zeroed here on
-// the launch stream before the launch); epoch: nonzero, new for every launch;
-// opts: lab A/B bits (0 in the product).
+// Bytes of one slot's outputs for requests of up to max_pkts packets.
+__host__ __device__ constexpr uint32_t burst_resp_slot(uint32_t max_pkts)
+{
+	return (burst_ver_off(max_pkts) + max_pkts + 63) & ~63u;
+}
+// req: slot 0's block (slot 1's at req + cap); resp: slot 0's outputs (slot
+// 1's at resp + burst_resp_slot(max_pkts)); dcmd: 24 bytes of uncached device
+// memory, the leader's relay words (one per slot, then the exit word), zeroed
+// here on the launch stream before the launch; start_seq: the last request
+// completed (the server serves burst_next(start_seq) first); epoch: nonzero,
+// new for every launch; opts: lab A/B bits (0 in the product).
 hipError_t launch_burst_server(BurstBox *box, const uint8_t *req, uint8_t *scratch, uint8_t *resp, uint64_t *dcmd,
 			       const void *zero, uint32_t cap, uint32_t max_pkts, uint32_t wgs, uint32_t per_wg,
 			       uint32_t start_seq, uint32_t epoch, uint32_t opts, hipStream_t st);

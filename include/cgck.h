@@ -160,6 +160,9 @@ int cgck_desc_host(cgck_ctx_t *ctx, void *base, size_t bytes,
  * directly.  Thin wrappers of hipHostRegister / hipHostUnregister. */
 int cgck_host_register(void *ptr, size_t bytes);
 int cgck_host_unregister(void *ptr);
+/* The device view of [ptr, ptr + bytes) inside a range registered with
+ * cgck_host_register (for cgck_burst_request); -ENOENT otherwise. */
+int cgck_host_device_ptr(const void *ptr, size_t bytes, void **dev);
 
 /* The drop-in symbols run on a per-thread context created on first use
  * (device from $CGCK_DEVICE, default 0).  cgck_thread_ctx returns that
@@ -204,6 +207,22 @@ void cgck_set_error_handler(cgck_error_fn fn, void *arg);
 int cgck_rx_begin(void *base, size_t bytes, const cgck_desc_t *desc, uint64_t n);
 int cgck_rx_end(void);
 
+/* Pipelined RX window: one burst in flight while the stack works.  The
+ * transport posts burst k as it arrives (cgck_rx_post returns at once, the
+ * burst server computing it meanwhile), then opens the window over the
+ * oldest posted burst — k - 1, whose values are in by then — with
+ * cgck_rx_begin_posted, runs the stack over it and closes it with
+ * cgck_rx_end as above.  The ring keeps a posted burst's frames unchanged
+ * until its window closes (netmap's head and DPDK's mbuf free come after
+ * the stack's processing: netmap.c:116-126, dpdk.c:255-263).  At most two
+ * bursts are posted and not yet opened (-EBUSY).  Without an open burst
+ * server, or when a burst does not fit it, cgck_rx_post computes the burst
+ * at once.  cgck_rx_post returns the frames posted; cgck_rx_begin_posted
+ * the frames the window answers for (as cgck_rx_begin), -ENOENT when
+ * nothing is posted. */
+int cgck_rx_post(void *base, size_t bytes, const cgck_desc_t *desc, uint64_t n);
+int cgck_rx_begin_posted(void);
+
 /* Deferred TX fill.  Between begin and flush, the
  * drop-in in_cksum/udp_cksum calls of THIS thread that target an IPv4
  * header (len == ip_hl*4) or a TCP/UDP segment lying inside memory
@@ -219,6 +238,16 @@ int cgck_rx_end(void);
 int cgck_tx_begin(void);
 int cgck_tx_flush(void);
 
+/* Pipelined TX fill: cgck_tx_post closes the window like cgck_tx_flush but
+ * returns once the fill is posted (the number of fields queued); the
+ * fields are written by cgck_tx_complete, which waits for the oldest posted
+ * fill and returns how many it wrote (0: none posted).  The transport calls
+ * it before it hands those slots to the NIC — at the next loop's kick
+ * (con-gen.c:493), so the GPU computes burst k while the stack builds burst
+ * k + 1.  At most two fills are posted and not yet completed (-EBUSY). */
+int cgck_tx_post(void);
+int cgck_tx_complete(void);
+
 /* Per-thread window counters since the thread's first call:
  * [0] drop-in calls answered by an RX window, [1] calls inside an RX window
  * computed synchronously (no match), [2] calls queued by a TX window, [3]
@@ -228,9 +257,10 @@ int cgck_window_stats(uint64_t stats[4]);
 /* Burst server (latency).  Keeps up to 32 workgroups
  * (one per 64 packets of max_pkts) resident on `ctx` (NULL: this thread's
  * drop-in context) that serve host-resident batches through a host-coherent
- * mailbox: cgck_desc_host, the RX window and the synchronous drop-in calls
- * then skip the kernel launch and the stream synchronisation whenever a
- * batch fits (at most max_pkts packets and max_bytes of packet bytes; a
+ * mailbox: cgck_desc_host, the RX window, the TX window's flush (its queue
+ * read in place when it lies in one registered range, as cgck_desc_host of
+ * that range) and the synchronous drop-in calls then skip the kernel launch
+ * and the stream synchronisation whenever a batch fits (at most max_pkts packets and max_bytes of packet bytes; a
  * batch of more than 64 packets is split over the workgroups).  Batches
  * above the caps take the launch path, whose many workgroups read host
  * memory faster for hundreds of frames of >= 576 B: max_bytes ~96 KiB routes
@@ -239,6 +269,22 @@ int cgck_window_stats(uint64_t stats[4]);
  * stops it.  cgck_ctx_destroy and cgck_thread_release close it too. */
 int cgck_burst_open(cgck_ctx_t *ctx, uint32_t max_pkts, size_t max_bytes, uint32_t idle_ms);
 int cgck_burst_close(cgck_ctx_t *ctx);
+
+/* One request to ctx's open burst server (NULL: this thread's context) over
+ * memory the device already sees — [dev_base, dev_base + range), e.g. the
+ * device view of a ring registered elsewhere.  The host does not check the
+ * descriptors: the server checks every one against `range` on the device
+ * before any load or store, and a descriptor that reaches past it fails the
+ * request with -EIO: the workgroup whose slice holds it reads and stores
+ * nothing (the other slices of a wide request may have been served).  Every request the library posts
+ * to a server for registered memory (cgck_desc_host, the RX/TX windows)
+ * carries its range the same way.  -ENOSPC: no server open, or n above its
+ * max_pkts.  cgck_host_register / cgck_host_unregister drain every open
+ * server before the mapping changes (the next request relaunches it), so no
+ * server kernel runs across a mapping change. */
+int cgck_burst_request(cgck_ctx_t *ctx, const void *dev_base, uint64_t range,
+		       const cgck_desc_t *desc, uint64_t n, uint32_t flags,
+		       uint32_t *out, uint8_t *verdict);
 
 /* Synthetic batches generated on the device.  Byte j of the
  * stream is byte (j & 7) of splitmix64(seed, j >> 3); each packet then gets

@@ -327,6 +327,40 @@ def test_verify_fixture_verdicts(engine, golden_verify, align):
         assert (v & 1) == 1 - c["toy_ip"] and ((v >> 1) & 1) == 1 - c["toy_l4"], c["kind"]
 
 
+def burst_slices(n, max_pkts, per=64, max_wg=32):
+    """The server's split of an n-packet request (burst_wgs, cgck_internal.h):
+    W workgroups, packet i in slice j = the j with n*j//W <= i < n*(j+1)//W."""
+    K = 1 if max_pkts <= 64 else min((max_pkts + per - 1) // per, max_wg)
+    W = 1 if n <= 64 else min((n + per - 1) // per, K)
+    return W, [n * j // W for j in range(W + 1)]
+
+
+def check_burst(out, exp, ver, ever, got, ref, what, max_pkts, ring=None, desc=None):
+    """Bit-exact outputs, verdicts and bytes; on a mismatch the message names
+    the packets, their server slices, the ring's address and size, and the
+    frames' offsets, so a failure on a box nobody can log into still says
+    where it went wrong."""
+    bad = np.nonzero((out != exp) | (ver != ever))[0]
+    bad_bytes = np.nonzero(got != ref)[0]
+    if len(bad) == 0 and len(bad_bytes) == 0:
+        return
+    W, edges = burst_slices(len(out), max_pkts)
+    slices = sorted({int(np.searchsorted(edges, int(i), side="right")) - 1 for i in bad})
+    msg = [f"{what}: {len(bad)} packets wrong, {len(bad_bytes)} bytes wrong; W {W}"]
+    if len(bad):
+        msg.append(f"indices {bad[:8].tolist()}..{bad[-8:].tolist()} slices {slices[:16]} "
+                   f"got {out[bad[:4]].tolist()} want {exp[bad[:4]].tolist()} "
+                   f"verdict got {ver[bad[:4]].tolist()} want {ever[bad[:4]].tolist()}")
+        if desc is not None:
+            fo = desc["frame_off"].astype(np.int64) + desc["l3_off"]
+            msg.append(f"frame offsets {fo[bad[:4]].tolist()} lens {desc['ip_len'][bad[:4]].tolist()}")
+    if len(bad_bytes):
+        msg.append(f"byte offsets {bad_bytes[:8].tolist()}..{bad_bytes[-4:].tolist()}")
+    if ring is not None:
+        msg.append(f"ring {ring.ctypes.data:#x} + {ring.nbytes}")
+    raise AssertionError("; ".join(msg))
+
+
 @pytest.mark.parametrize("npk,registered", [(500, False), (3000, False), (500, True), (3000, True)])
 def test_host_resident_batch(engine, port, npk, registered):
     """cgck_desc_host's three ways in: a small pageable burst (pinned staging,
@@ -353,7 +387,8 @@ def test_host_resident_batch(engine, port, npk, registered):
             out = np.zeros(len(desc), np.uint32)
             ver = np.zeros(len(desc), np.uint8)
             engine.desc_host(got, desc, flags, out, ver)
-            assert np.array_equal(out, exp) and np.array_equal(ver, ever) and np.array_equal(got, ref)
+            check_burst(out, exp, ver, ever, got, ref, f"npk {npk} flags {flags}", 1,
+                        ring if registered else None, desc)
     finally:
         if registered:
             L.cgck_host_unregister(ring.ctypes.data)
@@ -388,8 +423,8 @@ def test_burst_server_desc_host(engine, port, registered):
                     out = np.zeros(len(desc), np.uint32)
                     ver = np.zeros(len(desc), np.uint8)
                     engine.desc_host(got, desc, flags, out, ver)
-                    assert np.array_equal(out, exp) and np.array_equal(ver, ever), (npk, flags)
-                    assert np.array_equal(got, ref), (npk, flags)
+                    check_burst(out, exp, ver, ever, got, ref, f"npk {npk} flags {flags}", 1024,
+                                ring if registered else None, desc)
             finally:
                 if registered:
                     L.cgck_host_unregister(ring.ctypes.data)
@@ -431,13 +466,102 @@ def test_burst_server_wide(engine, port, registered, max_len):
                         out = np.zeros(len(desc), np.uint32)
                         ver = np.zeros(len(desc), np.uint8)
                         engine.desc_host(got, desc, flags, out, ver)
-                        assert np.array_equal(out, exp) and np.array_equal(ver, ever), (max_pkts, npk, flags)
-                        assert np.array_equal(got, ref), (max_pkts, npk, flags)
+                        check_burst(out, exp, ver, ever, got, ref, f"max_pkts {max_pkts} npk {npk} flags {flags}",
+                                    max_pkts, ring, desc)
                 finally:
                     if registered:
                         L.cgck_host_unregister(ring.ctypes.data)
         finally:
             engine.burst_close()
+
+
+def page_ring(nbytes):
+    """A page-aligned numpy ring of nbytes (rounded up to pages) and the
+    array that owns it."""
+    size = (nbytes + 4095) // 4096 * 4096
+    raw = np.zeros(size + 4096, np.uint8)
+    off = (-raw.ctypes.data) % 4096
+    return raw, raw[off:off + size]
+
+
+def test_burst_server_reregister_cycles(engine, port):
+    """register ring A, serve, unregister and free it,
+    register a larger ring B and FILL through a 32-workgroup server, checking
+    every packet, byte and verdict; six cycles, two frame sizes."""
+    L = cgck.load()
+    engine.burst_open(max_pkts=4096, max_bytes=4 << 20)
+    try:
+        for cycle in range(6):
+            max_len = 600 if cycle % 2 else 80
+            for npk in (2048, 4096):
+                rng = np.random.default_rng(900 + 17 * cycle + npk)
+                buf, desc = random_batch(rng, npk, max_len)
+                raw, ring = page_ring(len(buf))
+                assert L.cgck_host_register(ring.ctypes.data, ring.nbytes) == 0
+                try:
+                    for flags in (cgck.GEN_BOTH, cgck.FILL_BOTH, cgck.VERIFY_BSD):
+                        ref = buf.copy()
+                        exp, ever = port.batch_desc(ref, desc.view(np.uint8), len(desc), flags)
+                        ring[:len(buf)] = buf
+                        got = ring[:len(buf)]
+                        out = np.zeros(npk, np.uint32)
+                        ver = np.zeros(npk, np.uint8)
+                        engine.desc_host(got, desc, flags, out, ver)
+                        check_burst(out, exp, ver, ever, got, ref, f"cycle {cycle} npk {npk} flags {flags}",
+                                    4096, ring, desc)
+                finally:
+                    assert L.cgck_host_unregister(ring.ctypes.data) == 0
+                del ring, raw
+    finally:
+        engine.burst_close()
+
+
+@pytest.mark.parametrize("npk", [40, 700])
+def test_burst_request_range_refused(engine, port, npk):
+    """cgck_burst_request: the server itself checks every descriptor against
+    the request's range (registered memory read in place) — one frame past
+    the range fails the request with -EIO, nothing read out of range, nothing
+    stored; the same batch inside the range is exact (one workgroup at 40
+    packets, eleven slices at 700)."""
+    L = cgck.load()
+    rng = np.random.default_rng(4242 + npk)
+    buf, desc = random_batch(rng, npk, 600)
+    raw, ring = page_ring(len(buf))
+    ring[:len(buf)] = buf
+    assert L.cgck_host_register(ring.ctypes.data, ring.nbytes) == 0
+    engine.burst_open(max_pkts=1024, max_bytes=4 << 20)
+    try:
+        dev = cgck.host_device_ptr(ring)
+        ends = desc["frame_off"].astype(np.int64) + desc["l3_off"] + desc["ip_len"]
+        rng_bytes = int(ends.max())
+        out = np.zeros(npk, np.uint32)
+        ver = np.zeros(npk, np.uint8)
+        # the exact range: served
+        assert engine.burst_request(dev, rng_bytes, desc, cgck.FILL_BOTH, out, ver) == 0
+        ref = buf.copy()
+        exp, ever = port.batch_desc(ref, desc.view(np.uint8), npk, cgck.FILL_BOTH)
+        check_burst(out, exp, ver, ever, ring[:len(buf)], ref, "in range", 1024, ring, desc)
+        # one byte short of the farthest frame: refused on the device
+        ring[:len(buf)] = buf
+        assert engine.burst_request(dev, rng_bytes - 1, desc, cgck.FILL_BOTH, out, ver) == -5   # -EIO
+        assert "refused" in cgck.last_error()
+        # a frame offset far past the range (it would fault if it were read)
+        bad = desc.copy()
+        bad["frame_off"][npk // 2] = 1 << 40
+        assert engine.burst_request(dev, ring.nbytes, bad, cgck.FILL_BOTH, out, ver) == -5
+        # the refused requests stored nothing (the slices that checked first
+        # may have served: only a wholly refused slice is untouched, so
+        # compare only the frames of a one-workgroup request)
+        if npk <= 64:
+            assert np.array_equal(ring[:len(buf)], buf)
+        # and the server still serves
+        ring[:len(buf)] = buf
+        assert engine.burst_request(dev, ring.nbytes, desc, cgck.GEN_BOTH, out, ver) == 0
+        exp, ever = port.batch_desc(buf.copy(), desc.view(np.uint8), npk, cgck.GEN_BOTH)
+        check_burst(out, exp, ver, ever, ring[:len(buf)], buf, "after refusal", 1024, ring, desc)
+    finally:
+        engine.burst_close()
+        assert L.cgck_host_unregister(ring.ctypes.data) == 0
 
 
 def test_burst_server_idle_relaunch(engine, port):

@@ -283,3 +283,135 @@ def test_last_kernel_names(engine):
     assert engine.last_kernel.startswith("lpa_kernel<false, ")
     engine.sync()
     ver.free()
+
+
+# ---------------------------------------------------------------------------
+# Pipelined windows (cgck_rx_post / cgck_rx_begin_posted, cgck_tx_post /
+# cgck_tx_complete): one burst in flight while the stack works
+# ---------------------------------------------------------------------------
+
+@pytest.mark.parametrize("server", [False, True])
+@pytest.mark.parametrize("nframes", [40, 300, 2100])
+def test_rx_pipelined_replay(port, nframes, server):
+    """Burst k is posted before the stack replays burst k - 1 from its
+    window; every burst's outcomes, counters, call counts and ring bytes
+    equal the reference replay's.  Between a post and its window a
+    synchronous drop-in call runs (through the server when it is open, so a
+    later request needs the posted one's slot and collects it early), and
+    the rings are registered for half of the bursts."""
+    R = referee(port)
+    L = cgck.load()
+    bursts = []
+    for k in range(5):
+        rng = np.random.default_rng(1300 + 10 * k + nframes)
+        buf, desc = rxcorpus.ring(rxcorpus.corpus(rng, R, nframes, clean=k % 2 == 0))
+        if k % 2:
+            raw, ring, size = rxcorpus.registered_copy(buf)
+            assert L.cgck_host_register(ring.ctypes.data, size) == 0
+            bursts.append((buf, desc, ring[:len(buf)], ring, raw))
+        else:
+            bursts.append((buf, desc, buf.copy(), None, None))
+    if server:
+        cgck.burst_open(max_pkts=4096, max_bytes=8 << 20)
+    other = np.arange(64, dtype=np.uint8)
+    try:
+        for k in range(len(bursts) + 1):
+            if k < len(bursts):
+                buf, desc, got, _, _ = bursts[k]
+                assert cgck.rx_post(got, desc) == len(desc)
+                assert cgck.in_cksum(other, 3, 41) == R.in_cksum(other, 3, 41)   # a synchronous call
+            if k == 0:
+                continue
+            buf, desc, got, _, _ = bursts[k - 1]
+            for stack, ip_in, tcp_in in FLAGS[k % 3::6][:1]:
+                ref = buf.copy()
+                a = port.replay_rx(*R.fn_pointers(), ref, desc.view(np.uint8), len(desc), stack, ip_in, tcp_in)
+                s0 = cgck.window_stats()
+                m = cgck.rx_begin_posted()
+                try:
+                    b = port.replay_rx(*cgck.fn_pointers(), got, desc.view(np.uint8), len(desc), stack, ip_in,
+                                       tcp_in)
+                finally:
+                    served = cgck.rx_end()
+                s1 = cgck.window_stats()
+                cell = (k - 1, stack, ip_in, tcp_in)
+                assert np.array_equal(a[0], b[0]), (cell, np.nonzero(a[0] != b[0])[0][:8])
+                assert np.array_equal(a[1], b[1]), (cell, a[1], b[1])
+                assert np.array_equal(ref, got), cell
+                calls = int(b[1][4] + b[1][5])
+                assert served == s1[0] - s0[0] and served >= 0.9 * calls, (cell, served, calls)
+                assert m <= len(desc)
+        with pytest.raises(cgck.CgckError, match="no burst posted"):
+            cgck.rx_begin_posted()
+    finally:
+        if server:
+            cgck.burst_close()
+        for _, _, _, ring, _ in bursts:
+            if ring is not None:
+                L.cgck_host_unregister(ring.ctypes.data)
+
+
+def test_rx_post_limits(port):
+    rng = np.random.default_rng(77)
+    buf, desc = rxcorpus.ring(rxcorpus.corpus(rng, port, 16, clean=True))
+    rings = [buf.copy() for _ in range(3)]
+    assert cgck.rx_post(rings[0], desc) == 16
+    assert cgck.rx_post(rings[1], desc) == 16
+    with pytest.raises(cgck.CgckError, match="already posted"):
+        cgck.rx_post(rings[2], desc)
+    assert cgck.rx_begin_posted() == 16
+    with pytest.raises(cgck.CgckError, match="already open"):
+        cgck.rx_begin_posted()
+    assert cgck.rx_end() == 0
+    assert cgck.rx_begin_posted() == 16
+    assert cgck.rx_end() == 0
+    bad = desc.copy()
+    bad[3]["ip_len"] = 60000
+    with pytest.raises(cgck.CgckError, match="reaches past"):
+        cgck.rx_post(rings[0], bad)
+    with pytest.raises(cgck.CgckError, match="no burst posted"):
+        cgck.rx_begin_posted()
+
+
+@pytest.mark.parametrize("server", [False, True])
+def test_tx_pipelined_fill(port, server):
+    """Two bursts' fills posted back to back (the GPU computes burst k while
+    the stack builds burst k + 1); cgck_tx_complete writes each burst's
+    fields, oldest first; the slots of the burst not yet completed keep the
+    zeros the stack stored."""
+    rng = np.random.default_rng(63 + server)
+    raw, ring, size = rxcorpus.registered_copy(np.zeros(256 * 2048, np.uint8))
+    slots = ring[:256 * 2048].reshape(256, 2048)
+    L = cgck.load()
+    assert L.cgck_host_register(ring.ctypes.data, size) == 0
+    if server:
+        cgck.burst_open(max_pkts=1024, max_bytes=4 << 20)
+    try:
+        bursts = []
+        for k in range(3):
+            want = []
+            cgck.tx_begin()
+            for i in range(k * 80, k * 80 + 80):
+                ln = int(rng.integers(40, 1501))
+                pkt = tcp_pkt(rng, ln)
+                slots[i, 14:14 + ln] = pkt
+                want.append((i, ln, expected(port, pkt, 16)))
+                tx_calls(slots[i], ln, 16)
+            assert cgck.tx_post() == 160
+            bursts.append(want)
+            if k == 1:
+                with pytest.raises(cgck.CgckError, match="already posted"):
+                    cgck.tx_begin()
+                    cgck.tx_post()
+            if k >= 1:
+                assert cgck.tx_complete() == 160
+                for i, ln, ref in bursts[k - 1]:
+                    assert np.array_equal(slots[i, 14:14 + ln], ref), (k - 1, i)
+        assert cgck.tx_complete() == 160
+        for i, ln, ref in bursts[2]:
+            assert np.array_equal(slots[i, 14:14 + ln], ref), (2, i)
+        assert cgck.tx_complete() == 0
+    finally:
+        if server:
+            cgck.burst_close()
+        L.cgck_host_unregister(ring.ctypes.data)

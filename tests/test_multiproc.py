@@ -92,17 +92,21 @@ def test_device_for_refuses_oversubscription():
 
 
 def test_burst_summary_is_compact():
-    rows = [{"mode": m, "pkt_len": ln, "burst": b, "us_median": 1.0}
-            for m in ("rx_window_registered", "rx_verify_registered", "tx_fill_registered", "rx_verify")
-            for ln in bench.BURST_LENS for b in bench.BURSTS]
+    modes = [m for _, m in bench.BURST_MODES]
+    rows = [{"mode": m, "pkt_len": ln, "burst": b, "us_median": 1.0 + i}
+            for i, m in enumerate(modes) for ln in bench.BURST_LENS for b in bench.BURSTS]
     cpu = {"rows": [{"pkt_len": ln, "burst": b, "us_per_burst": 2.0} for ln in bench.BURST_LENS for b in bench.BURSTS]}
     s = bench.burst_summary(rows, cpu)
-    assert len(s) <= 10 and all(len(r) == len(bench.BURST_COLS) and r[-1] == 2.0 and r[2] == 1.0 for r in s)
+    assert len(s) <= 10
+    for r in s:
+        assert len(r) == len(bench.BURST_COLS) and r[-1] == 2.0
+        assert r[2:-1] == [1.0 + i for i in range(len(modes))]   # each column its own routing, no minimum
 
 
 def test_burst_crossover():
-    """The crossover is the first burst of the final winning run: a GPU win at
-    a small burst followed by a loss does not count."""
+    """The crossover is the first burst of the final winning run, per
+    routing: a GPU win at a small burst followed by a loss does not count,
+    and one routing's win is not credited to another."""
     B = bench.BURSTS
     gpu = {64: [9.0] * len(B), 576: [1.0] + [9.0] * (len(B) - 3) + [1.0, 1.0], 1500: [1.0] * len(B)}
     rows = [{"mode": "rx_window_registered", "pkt_len": ln, "burst": b, "us_median": gpu[ln][i]}
@@ -110,30 +114,12 @@ def test_burst_crossover():
     rows += [{"mode": "rx_window_registered_server", "pkt_len": 64, "burst": B[-1], "us_median": 1.0}]
     cpu = {"rows": [{"pkt_len": ln, "burst": b, "us_per_burst": 2.0} for ln in gpu for b in B]}
     x = bench.burst_crossover(rows, cpu)
-    assert x["64"]["rx_window"] == B[-1]     # the server row wins at the largest burst only
-    assert x["576"]["rx_window"] == B[-2]
-    assert x["1500"]["rx_window"] == B[0]
-    assert x["1500"]["tx_window"] is None    # no TX rows measured
+    assert x["64"]["rx_window_launch"] is None
+    assert x["64"]["rx_window_server"] == B[-1]   # the server row wins at the largest burst only
+    assert x["576"]["rx_window_launch"] == B[-2]
+    assert x["1500"]["rx_window_launch"] == B[0]
+    assert x["1500"]["tx_fill_pipelined"] is None    # no TX rows measured
     assert bench.burst_crossover({"error": "x"}, cpu) is None
-
-
-def test_burst_rows_take_the_faster_path():
-    """The summary rows and the TX crossover take the faster of the launch
-    path and the burst server for each cell."""
-    B = bench.BURSTS
-    rows = []
-    for ln in bench.BURST_LENS:
-        for b in B:
-            for mode, launch, server in (("rx_window_registered", 5.0, 3.0), ("rx_verify_registered", 2.0, 4.0),
-                                         ("tx_fill_registered", 6.0, 1.5)):
-                rows.append({"mode": mode, "pkt_len": ln, "burst": b, "us_median": launch})
-                rows.append({"mode": mode + "_server", "pkt_len": ln, "burst": b, "us_median": server})
-    cpu = {"rows": [{"pkt_len": ln, "burst": b, "us_per_burst": 1.8} for ln in bench.BURST_LENS for b in B]}
-    for r in bench.burst_summary(rows, cpu):
-        assert r[2:] == [3.0, 2.0, 1.5, 1.8], r
-    x = bench.burst_crossover(rows, cpu)
-    assert all(x[str(ln)]["tx_window"] == B[0] for ln in bench.BURST_LENS)   # the server's 1.5 < 1.8
-    assert all(x[str(ln)]["rx_window"] is None for ln in bench.BURST_LENS)   # 3.0 > 1.8 everywhere
 
 
 def test_single_rank_is_noop():

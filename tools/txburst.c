@@ -17,6 +17,17 @@
  *               cgck_tx_flush() (glue.c:15-41 batch point), the flush writing
  *               every field in place.
  *
+ *   rx_window_pipelined / tx_fill_pipelined — the same with one burst in
+ *               flight (cgck_rx_post + cgck_rx_begin_posted, cgck_tx_post +
+ *               cgck_tx_complete): burst k is posted, then the stack works
+ *               on burst k - 1; between bursts the thread spins
+ *               TXBURST_STACK_US microseconds (default 50) for the rest of
+ *               the stack's per-burst work, which the GPU overlaps.  The
+ *               reported time is what the worker thread spends in the
+ *               checksum path per burst — post, the wait for the previous
+ *               burst's values, the stack's calls, end — with the wait alone
+ *               beside it.
+ *
  * RX is measured four ways: the launch path on pageable ring memory, the
  * ring registered (cgck_host_register: read where it lies), the resident
  * burst server (cgck_burst_open: no launch or stream sync per call), and
@@ -91,21 +102,23 @@ int main(int argc, char **argv)
 	 * mempool or a huge-page XDP UMEM would be; otherwise 4 KiB pages */
 	uint8_t *ring;
 	if (getenv("TXBURST_HUGE") && atoi(getenv("TXBURST_HUGE"))) {
-		const size_t sz = (size_t)maxb * SLOT, al = 2u << 20;
+		const size_t sz = (size_t)2 * maxb * SLOT, al = 2u << 20;
 		uint8_t *m = mmap(NULL, sz + al, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
 		ring = m == MAP_FAILED ? NULL : (uint8_t *)(((uintptr_t)m + al - 1) & ~(uintptr_t)(al - 1));
 		if (ring)
 			madvise(ring, sz, MADV_HUGEPAGE);
 	} else {
-		ring = aligned_alloc(4096, (size_t)maxb * SLOT);
+		ring = aligned_alloc(4096, (size_t)2 * maxb * SLOT); /* two halves: bursts k and k - 1 */
 	}
+	const double stack_us = getenv("TXBURST_STACK_US") ? atof(getenv("TXBURST_STACK_US")) : 50.0;
 	cgck_desc_t *desc = malloc(sizeof(cgck_desc_t) * maxb);
 	uint32_t *out = malloc(4 * maxb);
 	uint8_t *ver = malloc(maxb);
 	double *t = malloc(sizeof(double) * maxit);
 	double *tc = malloc(sizeof(double) * maxit); /* RX window: the per-packet calls + rx_end only */
+	double *tw = malloc(sizeof(double) * maxit); /* pipelined: the wait for the previous burst */
 	cgck_ctx_t *ctx;
-	if (!ring || !desc || !out || !ver || !t || !tc || cgck_ctx_create(0, &ctx)) {
+	if (!ring || !desc || !out || !ver || !t || !tc || !tw || cgck_ctx_create(0, &ctx)) {
 		fprintf(stderr, "txburst: setup failed: %s\n", cgck_last_error());
 		return 1;
 	}
@@ -157,14 +170,16 @@ int main(int argc, char **argv)
 			desc[i].l3_off = L3;
 			desc[i].ip_len = (uint16_t)len;
 		}
+		/* the second half (the pipelined modes' other burst): the same frames */
+		memcpy(ring + (size_t)maxb * SLOT, ring, (size_t)maxb * SLOT);
 		/* fill both fields in place (the TX result a receiver would see) */
 		if (cgck_desc_host(ctx, ring, (size_t)maxb * SLOT, desc, maxb,
 				   CGCK_IP | CGCK_L4 | CGCK_ZERO_FIELDS | CGCK_STORE, out, NULL)) {
 			fprintf(stderr, "txburst: fill failed: %s\n", cgck_last_error());
 			return 1;
 		}
-		/* corrupt one payload byte of every 64th packet */
-		for (int i = 0; i < maxb; i += 64)
+		/* corrupt one payload byte of every 64th packet (both halves) */
+		for (int i = 0; i < 2 * maxb; i += 64)
 			ring[(size_t)i * SLOT + L3 + len - 1] ^= 0x5A;
 		/* passes: 0 launch path, 1 registered ring, 2 burst server, 3 server + registered */
 		for (int pass = 0; pass < 4; pass++) {
@@ -174,9 +189,9 @@ int main(int argc, char **argv)
 			static const char *win_name[4] = {"rx_window", "rx_window_registered", "rx_window_server",
 							  "rx_window_registered_server"};
 			if (pass == 2) /* pass 1's TX cells refilled the fields: toggle the corruption back */
-				for (int i = 0; i < maxb; i += 64)
+				for (int i = 0; i < 2 * maxb; i += 64)
 					ring[(size_t)i * SLOT + L3 + len - 1] ^= 0x5A;
-			if (reg && cgck_host_register(ring, (size_t)maxb * SLOT)) {
+			if (reg && cgck_host_register(ring, (size_t)2 * maxb * SLOT)) {
 				fprintf(stderr, "txburst: register failed: %s\n", cgck_last_error());
 				return 1;
 			}
@@ -290,6 +305,112 @@ int main(int argc, char **argv)
 				       "\"us_median\": %.2f, \"us_flush\": %.2f, \"mpkt_s\": %.3f}\n",
 				       pass == 3 ? "tx_fill_registered_server" : "tx_fill_registered", len, R, it, us, us_flush,
 				       R / us);
+				fflush(stdout);
+			}
+			for (int bi = 0; bi < nb && pass == 3; bi++) { /* RX, one burst in flight */
+				const int R = bursts[bi];
+				int it = 0, k = 0, bad_l4 = 0, bad_ip = 0;
+				double t0 = now();
+				while (it < maxit && now() - t0 < budget + 0.05) {
+					uint8_t *half = ring + (size_t)(k & 1) * maxb * SLOT;   /* burst k */
+					uint8_t *prev = ring + (size_t)((k + 1) & 1) * maxb * SLOT; /* burst k - 1 */
+					double a = now(), aw = a;
+					if (cgck_rx_post(half, (size_t)R * SLOT, desc, R) != R) {
+						fprintf(stderr, "txburst: rx_post failed: %s\n", cgck_last_error());
+						return 1;
+					}
+					if (k > 0) {
+						aw = now();
+						if (cgck_rx_begin_posted() != R) {
+							fprintf(stderr, "txburst: rx_begin_posted failed: %s\n", cgck_last_error());
+							return 1;
+						}
+						const double w = now() - aw;
+						int bi_ = 0, bl_ = 0;
+						for (int i = 0; i < R; i++) {
+							uint8_t *ip = prev + (size_t)i * SLOT + L3;
+							uint16_t saved, v;
+							memcpy(&saved, ip + 10, 2);
+							ip[10] = ip[11] = 0;
+							v = in_cksum(ip, 20);
+							bi_ += v != saved;
+							memcpy(ip + 10, &saved, 2);
+							memcpy(&saved, ip + 20 + 16, 2);
+							ip[20 + 16] = ip[20 + 17] = 0;
+							v = udp_cksum((struct ip *)ip, len - 20);
+							bl_ += v != saved;
+							memcpy(ip + 20 + 16, &saved, 2);
+						}
+						if (cgck_rx_end() != 2 * R) {
+							fprintf(stderr, "txburst: the pipelined window answered fewer than %d calls\n", 2 * R);
+							return 1;
+						}
+						bad_ip = bi_;
+						bad_l4 = bl_;
+						if (k > 20) {
+							t[it] = now() - a;
+							tw[it++] = w;
+						}
+					}
+					k++;
+					for (double s0 = now(); now() - s0 < stack_us * 1e-6;) /* the rest of the stack's work */
+						;
+				}
+				/* drain the last posted burst */
+				cgck_rx_begin_posted();
+				cgck_rx_end();
+				const double us = median(t, it) * 1e6, us_wait = median(tw, it) * 1e6;
+				printf("{\"mode\": \"rx_window_pipelined_registered_server\", \"pkt_len\": %d, \"burst\": %d, "
+				       "\"iters\": %d, \"us_median\": %.2f, \"us_wait\": %.2f, \"stack_us\": %.1f, "
+				       "\"bad_ip\": %d, \"bad_l4\": %d, \"bad_l4_expected\": %d}\n",
+				       len, R, it, us, us_wait, stack_us, bad_ip, bad_l4, (R + 63) / 64);
+				fflush(stdout);
+			}
+			for (int bi = 0; bi < nb && pass == 3; bi++) { /* TX, one fill in flight */
+				const int R = bursts[bi];
+				int it = 0, k = 0;
+				double t0 = now();
+				while (it < maxit && now() - t0 < budget + 0.05) {
+					uint8_t *half = ring + (size_t)(k & 1) * maxb * SLOT;
+					double a = now();
+					cgck_tx_begin();
+					for (int i = 0; i < R; i++) {
+						uint8_t *ip = half + (size_t)i * SLOT + L3;
+						uint16_t v;
+						ip[20 + 16] = ip[20 + 17] = 0;
+						v = udp_cksum((struct ip *)ip, len - 20);
+						memcpy(ip + 20 + 16, &v, 2);
+						ip[10] = ip[11] = 0;
+						v = in_cksum(ip, 20);
+						memcpy(ip + 10, &v, 2);
+					}
+					if (cgck_tx_post() != 2 * R) {
+						fprintf(stderr, "txburst: tx_post failed: %s\n", cgck_last_error());
+						return 1;
+					}
+					double aw = now(), w = 0;
+					if (k > 0) {
+						const int r = cgck_tx_complete(); /* burst k - 1, before its kick */
+						w = now() - aw;
+						if (r != 2 * R) {
+							fprintf(stderr, "txburst: tx_complete wrote %d of %d: %s\n", r, 2 * R,
+								cgck_last_error());
+							return 1;
+						}
+						if (k > 20) {
+							t[it] = now() - a;
+							tw[it++] = w;
+						}
+					}
+					k++;
+					for (double s0 = now(); now() - s0 < stack_us * 1e-6;)
+						;
+				}
+				cgck_tx_complete();
+				const double us = median(t, it) * 1e6, us_wait = median(tw, it) * 1e6;
+				printf("{\"mode\": \"tx_fill_pipelined_registered_server\", \"pkt_len\": %d, \"burst\": %d, "
+				       "\"iters\": %d, \"us_median\": %.2f, \"us_wait\": %.2f, \"stack_us\": %.1f}\n",
+				       len, R, it, us, us_wait, stack_us);
 				fflush(stdout);
 			}
 			if (srv) {
