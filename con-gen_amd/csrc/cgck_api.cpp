@@ -856,10 +856,10 @@ extern "C" int cgck_burst_request(cgck_ctx_t *c, const void *dev_base, uint64_t 
 // can tell ring memory from a caller's stack or heap, and its flush read the
 // queued packets where they lie.  Written only by register/unregister
 // (set-up time); lookups take the reader side.
+std::atomic<uint64_t> cgck::g_reg_gen{1}; // bumped by every register / unregister
 namespace {
 std::shared_mutex g_reg_mu;
 std::vector<RegRange> g_reg;
-std::atomic<uint64_t> g_reg_gen{1}; // bumped by every register / unregister
 // per thread: the range of the last hit, valid while the generation holds
 __attribute__((tls_model("initial-exec"))) thread_local uint64_t t_reg_gen = 0;
 __attribute__((tls_model("initial-exec"))) thread_local RegRange t_reg_last{nullptr, nullptr, nullptr};
@@ -884,8 +884,44 @@ bool cgck::reg_find(const void *p, size_t bytes, RegRange *r)
 	return false;
 }
 
+// Memory of the brk heap is refused.  Rings carved out of the heap (numpy
+// buffers in the tests, round 3's failing test among them) were read and
+// written by the GPU at an address 64 KiB or 128 KiB away from the right one
+// for a run of pages, intermittently: the allocator returns the heap's pages
+// to the kernel and faults fresh ones in at the same addresses, and pages
+// that moved under a registration stayed mapped to the GPU where they had
+// been (the failing values are the frames'
+// own at the shifted address; the same rings in mappings of their own were
+// exact in every run).  A ring belongs in a mapping of its own — mmap, a
+// hugetlbfs segment, a transport's pool — which nothing else in the process
+// unmaps or re-faults while it is registered.
+static bool in_brk_heap(const void *ptr, size_t bytes)
+{
+	FILE *f = fopen("/proc/self/maps", "r");
+	if (!f)
+		return false;
+	char line[512];
+	bool hit = false;
+	const uintptr_t a = (uintptr_t)ptr, e = a + bytes;
+	while (!hit && fgets(line, sizeof(line), f)) {
+		unsigned long lo, hi;
+		if (sscanf(line, "%lx-%lx", &lo, &hi) == 2 && strstr(line, "[heap]") && a < hi && e > lo)
+			hit = true;
+	}
+	fclose(f);
+	return hit;
+}
+
 extern "C" int cgck_host_register(void *ptr, size_t bytes)
 {
+	if (!ptr || !bytes)
+		return set_err(-EINVAL, "cgck_host_register: NULL or empty range");
+	if (in_brk_heap(ptr, bytes))
+		return set_err(-EINVAL,
+			       "cgck_host_register: [%p, +%zu) lies in the brk heap, whose pages the allocator returns "
+			       "and re-faults under a registration; register a mapping of its own (mmap, hugetlbfs, the "
+			       "transport's pool)",
+			       ptr, bytes);
 	std::unique_lock<std::shared_mutex> map_lk(g_map_mu);
 	burst_quiesce_all();
 	HIP_TRY(hipHostRegister(ptr, bytes, hipHostRegisterDefault));

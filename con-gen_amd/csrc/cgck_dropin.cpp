@@ -157,6 +157,10 @@ struct ThreadState {
 	unsigned rxp_head = 0, rxp_count = 0;
 	uint64_t rx_served0 = 0; // stats[0] at rx_begin
 	uint64_t stats[4] = {0, 0, 0, 0};
+	// the registered range of the last TX-window hit, valid while g_reg_gen
+	// holds reg_gen (the window's per-call check without a call out)
+	RegRange reg_last{nullptr, nullptr, nullptr};
+	uint64_t reg_gen = 0;
 };
 
 // The drop-ins read this on every call, so it is a plain pointer in the
@@ -257,6 +261,23 @@ inline bool rx_find(ThreadState &t, const uint8_t *p, uint32_t *v)
 		}
 	}
 	return rx_find_slow(t, p, v);
+}
+
+// Is [p, p + bytes) registered (the TX window queues only ring memory)?  The
+// range of the last hit first, then reg_find.  The generation is read before
+// the lookup, so a change racing it leaves the cache stale-marked.
+inline bool tx_registered(ThreadState &t, const uint8_t *p, size_t bytes)
+{
+	const uint64_t g = g_reg_gen.load(std::memory_order_acquire);
+	if (__builtin_expect(t.reg_gen == g && p >= t.reg_last.lo && p < t.reg_last.hi &&
+			     bytes <= (size_t)(t.reg_last.hi - p), 1))
+		return true;
+	RegRange r;
+	if (!reg_find(p, bytes, &r))
+		return false;
+	t.reg_last = r;
+	t.reg_gen = g;
+	return true;
 }
 
 // Queue one field; a header or segment queued again replaces its entry (the
@@ -394,8 +415,7 @@ extern "C" uint16_t in_cksum(void *data, int len)
 		rx_miss = true;
 	}
 	if (t.tx_open && len >= 20 && (b[0] >> 4) == 4 && len == (b[0] & 15) * 4) {
-		RegRange r;
-		if (reg_find(data, (size_t)len, &r)) {
+		if (tx_registered(t, b, (size_t)len)) {
 			tx_queue(t, (uint8_t *)data, (uint32_t)len, (uint16_t)len, -1);
 			t.stats[2]++;
 			return 0;
@@ -432,9 +452,8 @@ extern "C" uint16_t udp_cksum(struct ip *ipp, int len)
 	}
 	if (t.tx_open && hl >= 20 && ip_len <= 0xffff && (ip[9] == 6 || ip[9] == 17)) {
 		const int fo = ip[9] == 6 ? 16 : 6;
-		RegRange r;
 		if ((uint32_t)len >= (uint32_t)fo + 2) {
-			if (reg_find(ip, ip_len, &r)) {
+			if (tx_registered(t, ip, ip_len)) {
 				tx_queue(t, (uint8_t *)ip, ip_len, (uint16_t)hl, (int16_t)fo);
 				t.stats[2]++;
 				return 0;

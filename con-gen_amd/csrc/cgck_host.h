@@ -7,6 +7,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <atomic>
+
 #include "cgck_internal.h"
 
 namespace cgck {
@@ -124,6 +126,9 @@ struct RegRange {
 };
 // Is [p, p + bytes) inside one registered range?  Fills *r when it is.
 bool reg_find(const void *p, size_t bytes, RegRange *r);
+// Bumped by every cgck_host_register / _unregister: a range found under one
+// value stays valid while the value holds (the drop-ins' per-thread cache).
+extern std::atomic<uint64_t> g_reg_gen;
 
 // The calling thread's drop-in context (created on first use); nullptr with
 // the error text set when no gfx950 device can be used.

@@ -130,10 +130,11 @@ def ring(frames):
 
 
 def registered_copy(buf):
-    """A page-aligned copy of `buf` (for cgck_host_register) and its view."""
+    """A copy of `buf` in an anonymous mapping of its own (for
+    cgck_host_register, which refuses the brk heap): (owner, view, size)."""
+    import mmap
     size = (len(buf) + 4095) // 4096 * 4096
-    raw = np.zeros(size + 4096, np.uint8)
-    off = (-raw.ctypes.data) % 4096
-    r = raw[off:off + size]
+    m = mmap.mmap(-1, size, flags=mmap.MAP_PRIVATE | mmap.MAP_ANONYMOUS)
+    r = np.frombuffer(m, np.uint8)
     r[:len(buf)] = buf
-    return raw, r, size
+    return m, r, size

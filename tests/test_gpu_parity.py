@@ -8,6 +8,7 @@ import numpy as np
 import pytest
 
 import cgck
+import memdiag
 
 pytestmark = pytest.mark.gpu
 
@@ -335,7 +336,7 @@ def burst_slices(n, max_pkts, per=64, max_wg=32):
     return W, [n * j // W for j in range(W + 1)]
 
 
-def check_burst(out, exp, ver, ever, got, ref, what, max_pkts, ring=None, desc=None):
+def check_burst(out, exp, ver, ever, got, ref, what, max_pkts, ring=None, desc=None, vm=None):
     """Bit-exact outputs, verdicts and bytes; on a mismatch the message names
     the packets, their server slices, the ring's address and size, and the
     frames' offsets, so a failure on a box nobody can log into still says
@@ -355,10 +356,29 @@ def check_burst(out, exp, ver, ever, got, ref, what, max_pkts, ring=None, desc=N
             fo = desc["frame_off"].astype(np.int64) + desc["l3_off"]
             msg.append(f"frame offsets {fo[bad[:4]].tolist()} lens {desc['ip_len'][bad[:4]].tolist()}")
     if len(bad_bytes):
-        msg.append(f"byte offsets {bad_bytes[:8].tolist()}..{bad_bytes[-4:].tolist()}")
+        msg.append(f"byte offsets {bad_bytes[:8].tolist()}..{bad_bytes[-4:].tolist()} "
+                   f"got {got[bad_bytes[:8]].tolist()} want {ref[bad_bytes[:8]].tolist()} "
+                   f"4 KiB pages {sorted(set((bad_bytes // 4096).tolist()))[:16]}")
     if ring is not None:
         msg.append(f"ring {ring.ctypes.data:#x} + {ring.nbytes}")
+        msg.append(f"mappings {memdiag.vma_info(ring.ctypes.data, ring.nbytes)}")
+    if vm is not None:
+        msg.append(f"vmstat over the request {memdiag.vmstat_delta(vm, memdiag.vmstat())}")
+    path = memdiag.dump_failure(what, out=out, exp=exp, ver=ver, ever=ever, got=got, ref=ref,
+                                desc=desc if desc is not None else np.zeros(0, cgck.DESC_DTYPE),
+                                ring_addr=np.uint64(ring.ctypes.data if ring is not None else 0))
+    msg.append(f"arrays in {path}")
     raise AssertionError("; ".join(msg))
+
+
+def page_ring(nbytes):
+    """A ring of nbytes (rounded up to pages) in an anonymous mapping of its
+    own, as a transport's pool is (cgck_host_register refuses the brk heap):
+    (owner, view)."""
+    import mmap
+    size = (nbytes + 4095) // 4096 * 4096
+    m = mmap.mmap(-1, size, flags=mmap.MAP_PRIVATE | mmap.MAP_ANONYMOUS)
+    return m, np.frombuffer(m, np.uint8)
 
 
 @pytest.mark.parametrize("npk,registered", [(500, False), (3000, False), (500, True), (3000, True)])
@@ -370,11 +390,8 @@ def test_host_resident_batch(engine, port, npk, registered):
     buf, desc = random_batch(rng, npk, 1500)
     L = cgck.load()
     if registered:
-        size = (len(buf) + 4095) // 4096 * 4096
-        raw = np.zeros(size + 4096, np.uint8)
-        off = (-raw.ctypes.data) % 4096
-        ring = raw[off:off + size]
-        assert L.cgck_host_register(ring.ctypes.data, size) == 0
+        raw, ring = page_ring(len(buf))
+        assert L.cgck_host_register(ring.ctypes.data, ring.nbytes) == 0
     try:
         for flags in (cgck.GEN_BOTH, cgck.FILL_BOTH, cgck.VERIFY_BSD):
             ref = buf.copy()
@@ -406,11 +423,8 @@ def test_burst_server_desc_host(engine, port, registered):
             rng = np.random.default_rng(31 + npk)
             buf, desc = random_batch(rng, npk, 1500)
             if registered:
-                size = (len(buf) + 4095) // 4096 * 4096
-                raw = np.zeros(size + 4096, np.uint8)
-                off = (-raw.ctypes.data) % 4096
-                ring = raw[off:off + size]
-                assert L.cgck_host_register(ring.ctypes.data, size) == 0
+                raw, ring = page_ring(len(buf))
+                assert L.cgck_host_register(ring.ctypes.data, ring.nbytes) == 0
             try:
                 for flags in (cgck.GEN_BOTH, cgck.FILL_BOTH, cgck.VERIFY_BSD, cgck.VERIFY_TOY):
                     ref = buf.copy()
@@ -449,11 +463,8 @@ def test_burst_server_wide(engine, port, registered, max_len):
                 buf, desc = random_batch(rng, npk, max_len)
                 ring = None
                 if registered:
-                    size = (len(buf) + 4095) // 4096 * 4096
-                    raw = np.zeros(size + 4096, np.uint8)
-                    off = (-raw.ctypes.data) % 4096
-                    ring = raw[off:off + size]
-                    assert L.cgck_host_register(ring.ctypes.data, size) == 0
+                    raw, ring = page_ring(len(buf))
+                    assert L.cgck_host_register(ring.ctypes.data, ring.nbytes) == 0
                 try:
                     for flags in (cgck.GEN_BOTH, cgck.FILL_BOTH, cgck.VERIFY_BSD):
                         ref = buf.copy()
@@ -465,9 +476,10 @@ def test_burst_server_wide(engine, port, registered, max_len):
                             got = buf.copy()
                         out = np.zeros(len(desc), np.uint32)
                         ver = np.zeros(len(desc), np.uint8)
+                        vm = memdiag.vmstat()
                         engine.desc_host(got, desc, flags, out, ver)
                         check_burst(out, exp, ver, ever, got, ref, f"max_pkts {max_pkts} npk {npk} flags {flags}",
-                                    max_pkts, ring, desc)
+                                    max_pkts, ring, desc, vm)
                 finally:
                     if registered:
                         L.cgck_host_unregister(ring.ctypes.data)
@@ -475,23 +487,18 @@ def test_burst_server_wide(engine, port, registered, max_len):
             engine.burst_close()
 
 
-def page_ring(nbytes):
-    """A page-aligned numpy ring of nbytes (rounded up to pages) and the
-    array that owns it."""
-    size = (nbytes + 4095) // 4096 * 4096
-    raw = np.zeros(size + 4096, np.uint8)
-    off = (-raw.ctypes.data) % 4096
-    return raw, raw[off:off + size]
-
-
 def test_burst_server_reregister_cycles(engine, port):
-    """register ring A, serve, unregister and free it,
+    """register ring A, serve, unregister and unmap it,
     register a larger ring B and FILL through a 32-workgroup server, checking
-    every packet, byte and verdict; six cycles, two frame sizes."""
+    every packet, byte and verdict; sixteen cycles, two frame sizes.  (Round
+    3's test carved its rings out of the brk heap, where the allocator
+    returns and re-faults pages under a registration: the GPU then read and
+    wrote some pages 64 or 128 KiB off; cgck_host_register refuses the heap,
+    test_host_register_refuses_brk_heap.)"""
     L = cgck.load()
     engine.burst_open(max_pkts=4096, max_bytes=4 << 20)
     try:
-        for cycle in range(6):
+        for cycle in range(16):
             max_len = 600 if cycle % 2 else 80
             for npk in (2048, 4096):
                 rng = np.random.default_rng(900 + 17 * cycle + npk)
@@ -506,14 +513,30 @@ def test_burst_server_reregister_cycles(engine, port):
                         got = ring[:len(buf)]
                         out = np.zeros(npk, np.uint32)
                         ver = np.zeros(npk, np.uint8)
+                        vm = memdiag.vmstat()
                         engine.desc_host(got, desc, flags, out, ver)
                         check_burst(out, exp, ver, ever, got, ref, f"cycle {cycle} npk {npk} flags {flags}",
-                                    4096, ring, desc)
+                                    4096, ring, desc, vm)
                 finally:
                     assert L.cgck_host_unregister(ring.ctypes.data) == 0
-                del ring, raw
+                del ring, got, raw
     finally:
         engine.burst_close()
+
+
+def test_host_register_refuses_brk_heap(engine):
+    """A buffer of the brk heap ([heap] in /proc/self/maps) is refused with
+    -EINVAL; the same bytes in a mapping of their own register."""
+    L = cgck.load()
+    small = [np.zeros(16384, np.uint8) for _ in range(8)]   # small arrays come from the heap
+    heap = [a for a in small if memdiag.in_brk_heap(a.ctypes.data, a.nbytes)]
+    if not heap:
+        pytest.skip("no numpy buffer landed in the brk heap in this process")
+    assert L.cgck_host_register(heap[0].ctypes.data, heap[0].nbytes) == -22
+    assert "brk heap" in cgck.last_error()
+    raw, ring = page_ring(16384)
+    assert L.cgck_host_register(ring.ctypes.data, ring.nbytes) == 0
+    assert L.cgck_host_unregister(ring.ctypes.data) == 0
 
 
 @pytest.mark.parametrize("npk", [40, 700])
@@ -647,9 +670,8 @@ def test_deferred_tx_fill(engine, port, registered):
     sequence — queued and read in place from a registered ring, or answered
     synchronously when the memory is not registered."""
     rng = np.random.default_rng(23)
-    raw = np.zeros(256 * 2048 + 4096, np.uint8)
-    off = (-raw.ctypes.data) % 4096
-    ring = raw[off:off + 256 * 2048].reshape(256, 2048)   # netmap-like slots, IP at +14
+    raw, flat = page_ring(256 * 2048)
+    ring = flat.reshape(256, 2048)   # netmap-like slots, IP at +14
     if registered:
         assert cgck.load().cgck_host_register(ring.ctypes.data, ring.nbytes) == 0
     want = []

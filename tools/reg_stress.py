@@ -9,6 +9,10 @@ hinting faults and page migrations, THP collapses, compaction).
 usage: python tools/reg_stress.py [seconds] [mode] [libcgck.so]
   mode "plain": numpy rings as the test allocates them
   mode "lock":  the same rings mlock'ed and MADV_NOHUGEPAGE before registering
+  mode "heap":  plain rings after priming the heap as a long test process does
+                (a 30 MB array freed raises glibc's mmap threshold, then an 8 MB
+                array comes from the heap and numpy marks it MADV_HUGEPAGE)
+  mode "mmap":  each ring its own anonymous mmap, MADV_NOHUGEPAGE
 """
 import ctypes
 import os
@@ -83,8 +87,17 @@ def main():
     max_pkts, K = 4096, 32
     eng.burst_open(max_pkts=max_pkts, max_bytes=4 << 20)
     names = {cgck.GEN_BOTH: "GEN", cgck.FILL_BOTH: "FILL", cgck.VERIFY_BSD: "VBSD"}
+    if mode == "heap":
+        a = np.ones(30 << 20, np.uint8)
+        del a
+        b = np.ones(8 << 20, np.uint8)
+        del b
+    import mmap as _mmap
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import memdiag
     t_end = time.time() + seconds
     cycle = requests = bad_requests = 0
+    reg_ms, unreg_ms = [], []   # wall time of cgck_host_register / _unregister with the server open
     raw = None
     try:
         while time.time() < t_end:
@@ -94,15 +107,24 @@ def main():
                     buf, desc = random_batch(rng, npk, max_len)
                     size = (len(buf) + 4095) // 4096 * 4096
                     ring = None
-                    raw = np.zeros(size + 4096, np.uint8)
-                    off = (-raw.ctypes.data) % 4096
-                    ring = raw[off:off + size]
+                    if mode == "mmap":
+                        raw = _mmap.mmap(-1, size, flags=_mmap.MAP_PRIVATE | _mmap.MAP_ANONYMOUS)
+                        ring = np.frombuffer(raw, np.uint8)
+                        libc.madvise(ctypes.c_void_p(ring.ctypes.data), ctypes.c_size_t(size), MADV_NOHUGEPAGE)
+                    else:
+                        raw = np.zeros(size + 4096, np.uint8)
+                        off = (-raw.ctypes.data) % 4096
+                        ring = raw[off:off + size]
+                    if cycle == 0 and npk == 4096:
+                        print("ring mapping", memdiag.vma_info(ring.ctypes.data, size), flush=True)
                     if mode == "lock":
                         if libc.madvise(ctypes.c_void_p(ring.ctypes.data), ctypes.c_size_t(size), MADV_NOHUGEPAGE):
                             print("madvise errno", ctypes.get_errno())
                         if libc.mlock(ctypes.c_void_p(ring.ctypes.data), ctypes.c_size_t(size)):
                             print("mlock errno", ctypes.get_errno())
+                    t_reg = time.perf_counter()
                     assert L.cgck_host_register(ring.ctypes.data, size) == 0
+                    reg_ms.append((time.perf_counter() - t_reg) * 1e3)
                     try:
                         for flags in (cgck.GEN_BOTH, cgck.FILL_BOTH, cgck.VERIFY_BSD):
                             ref = buf.copy()
@@ -132,15 +154,24 @@ def main():
                                       f"slices {sl[:12]} bytes_bad {len(bytes_bad)} ring {ring.ctypes.data:#x} "
                                       f"size {size} bad_offsets {fo[bad[:4]].tolist()} "
                                       f"got {out[bad[:3]].tolist()} want {exp[bad[:3]].tolist()} "
-                                      f"vmstat {vdelta(v0, v1)}", flush=True)
+                                      f"vmstat {vdelta(v0, v1)} "
+                                      f"bytes got {got[bytes_bad[:6]].tolist()} want {ref[bytes_bad[:6]].tolist()} "
+                                      f"pages {sorted(set((bytes_bad // 4096).tolist()))[:12]} "
+                                      f"mapping {memdiag.vma_info(ring.ctypes.data, size)}", flush=True)
                     finally:
+                        t_unreg = time.perf_counter()
                         assert L.cgck_host_unregister(ring.ctypes.data) == 0
+                        unreg_ms.append((time.perf_counter() - t_unreg) * 1e3)
                         if mode == "lock":
                             libc.munlock(ctypes.c_void_p(ring.ctypes.data), ctypes.c_size_t(size))
+                        # (an mmap'ed ring is unmapped when its last view goes)
             cycle += 1
             print(f"cycle {cycle} requests {requests} bad {bad_requests} vmstat {vmstat()}", flush=True)
     finally:
         eng.burst_close()
+    import statistics
+    print(f"register ms median {statistics.median(reg_ms):.3f} max {max(reg_ms):.3f}; unregister ms median "
+          f"{statistics.median(unreg_ms):.3f} max {max(unreg_ms):.3f} (server open, idle 200 ms)", flush=True)
     print(f"DONE mode {mode} cycles {cycle} requests {requests} bad_requests {bad_requests}", flush=True)
     return 1 if bad_requests else 0
 

@@ -8,6 +8,7 @@
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <sys/mman.h>
 #include <string.h>
 #include <time.h>
 
@@ -41,7 +42,10 @@ int main(int argc, char **argv)
 {
 	const int len = argc > 1 ? atoi(argv[1]) : 64;
 	const int maxb = 2048, it = 2000;
-	uint8_t *ring = aligned_alloc(4096, (size_t)maxb * SLOT);
+	/* a mapping of its own (cgck_host_register refuses the brk heap) */
+	uint8_t *ring = mmap(NULL, (size_t)maxb * SLOT, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+	if (ring == MAP_FAILED)
+		ring = NULL;
 	cgck_desc_t *desc = malloc(sizeof(cgck_desc_t) * maxb);
 	uint32_t *out = malloc(4 * maxb);
 	uint8_t *ver = malloc(maxb);

@@ -108,7 +108,11 @@ int main(int argc, char **argv)
 		if (ring)
 			madvise(ring, sz, MADV_HUGEPAGE);
 	} else {
-		ring = aligned_alloc(4096, (size_t)2 * maxb * SLOT); /* two halves: bursts k and k - 1 */
+		/* a mapping of its own, as a transport's pool is (cgck_host_register
+		 * refuses the brk heap); two halves: bursts k and k - 1 */
+		ring = mmap(NULL, (size_t)2 * maxb * SLOT, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+		if (ring == MAP_FAILED)
+			ring = NULL;
 	}
 	const double stack_us = getenv("TXBURST_STACK_US") ? atof(getenv("TXBURST_STACK_US")) : 50.0;
 	cgck_desc_t *desc = malloc(sizeof(cgck_desc_t) * maxb);
