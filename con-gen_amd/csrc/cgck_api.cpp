@@ -634,16 +634,20 @@ static void *registered_ptr(void *p, size_t bytes)
 // the burst server it is left posted and *pend records where its outputs go
 // (1 is returned; burst_collect finishes it), otherwise it is computed at
 // once (0).
+// sum: a summary the library computed itself while building the
+// descriptors (they lie inside [base, base + bytes) by construction): the
+// per-descriptor pass is skipped.
 static int desc_host_impl(cgck_ctx *c, void *base, size_t bytes, const cgck_desc_t *desc, uint64_t n, uint32_t flags,
-			  uint32_t *out, uint8_t *verdict, uint32_t *meta, BurstPending *pend)
+			  uint32_t *out, uint8_t *verdict, uint32_t *meta, BurstPending *pend,
+			  const DescSummary *sum = nullptr)
 {
 	if (n == 0)
 		return 0;
 	if (!base || !desc)
 		return set_err(-EINVAL, "cgck_desc_host: NULL base or descriptors");
-	size_t pkt_bytes = 0;
-	uint32_t max_len = 0;
-	for (uint64_t i = 0; i < n; i++) {
+	size_t pkt_bytes = sum ? sum->pkt_bytes : 0;
+	uint32_t max_len = sum ? sum->max_len : 0;
+	for (uint64_t i = 0; i < n && !sum; i++) {
 		max_len = desc[i].ip_len > max_len ? desc[i].ip_len : max_len;
 		const uint64_t end = desc[i].frame_off + desc[i].l3_off + desc[i].ip_len;
 		if (end > bytes || end < desc[i].frame_off)
@@ -669,8 +673,11 @@ static int desc_host_impl(cgck_ctx *c, void *base, size_t bytes, const cgck_desc
 	// read) unless they are registered and either larger than that read or
 	// stored to in place; a pageable batch with in-place stores takes the
 	// launch path (the server's copy of the bytes is not written back).
+	// A posted request (pend) reads registered memory in place whatever its
+	// size: its latency is hidden, and copying the bytes would put them back
+	// on the poster's thread.
 	const bool store = flags & CGCK_STORE;
-	const bool in_place = dev_base && (store || burst_layout(pkt_bytes, n).bytes > kServerCopy);
+	const bool in_place = dev_base && (store || pend || burst_layout(pkt_bytes, n).bytes > kServerCopy);
 	if ((in_place || !store) && burst_fits(c, n, max_len, in_place ? 0 : pkt_bytes, pkt_bytes)) {
 		// the resident server: no launch, no stream sync
 		const BurstLayout L = burst_layout(in_place ? 0 : pkt_bytes, n);
@@ -796,11 +803,11 @@ int cgck::desc_host(cgck_ctx *c, void *base, size_t bytes, const cgck_desc_t *de
 }
 
 int cgck::desc_host_post(cgck_ctx *c, void *base, size_t bytes, const cgck_desc_t *desc, uint64_t n, uint32_t flags,
-			 uint32_t *out, uint8_t *verdict, uint32_t *meta, BurstPending *pend)
+			 uint32_t *out, uint8_t *verdict, uint32_t *meta, BurstPending *pend, const DescSummary *sum)
 {
 	pend->seq = 0;
 	pend->rc = 0;
-	return desc_host_impl(c, base, bytes, desc, n, flags, out, verdict, meta, pend);
+	return desc_host_impl(c, base, bytes, desc, n, flags, out, verdict, meta, pend, sum);
 }
 
 extern "C" int cgck_desc_host(cgck_ctx_t *c, void *base, size_t bytes, const cgck_desc_t *desc,

@@ -123,6 +123,7 @@ struct TxFill {
 	std::vector<cgck_desc_t> d;
 	std::vector<uint32_t> o, idx; // idx: the value (descriptor) of each queued entry
 	BurstPending pend{};
+	bool stored = false; // the kernel wrote the fields in place (CGCK_STORE): nothing left to write
 };
 
 struct ThreadState {
@@ -136,6 +137,17 @@ struct ThreadState {
 	TxFill txs;       // cgck_tx_flush's batch
 	TxFill txp[2];    // posted fills (cgck_tx_post), oldest at txp_head
 	unsigned txp_head = 0, txp_count = 0;
+	// The window's descriptors built as the calls come, while every call is
+	// at or above the highest header so far and inside one registered range
+	// (txd_ok): one per packet, its header and segment entries merged, so
+	// cgck_tx_post sends them as they are.  txd_h / txd_s: the current
+	// packet's header and segment spans (0: not queued); txd_noip: packets
+	// whose header was not queued.
+	std::vector<cgck_desc_t> txd_fast;
+	bool txd_ok = false;
+	const uint8_t *txd_lo = nullptr, *txd_hi = nullptr;
+	uint32_t txd_h = 0, txd_s = 0, txd_noip = 0, txd_max = 0;
+	size_t txd_bytes = 0; // 16-byte-rounded packet bytes of the closed descriptors
 	// RX window: frame i's header at rx_base + rxd[i].frame_off +
 	// rxd[i].l3_off; rxo[i] its values (lo16 header checksum, hi16 L4
 	// checksum, ICMP without the pseudo-header) and rxm[i] which calls they
@@ -285,6 +297,18 @@ inline bool tx_registered(ThreadState &t, const uint8_t *p, size_t bytes)
 // while every call is at or above the highest header queued so far a
 // duplicate can only be one of the last entries; the first call below it
 // (ring wrap, a slot handed out again) switches to a map of every entry.
+// The current packet's descriptor closed: its length and whether its header
+// was queued enter the window's summary.
+inline void txd_close(ThreadState &t)
+{
+	if (t.txd_fast.empty())
+		return;
+	const uint32_t len = t.txd_fast.back().ip_len;
+	t.txd_noip += t.txd_h == 0;
+	t.txd_max = len > t.txd_max ? len : t.txd_max;
+	t.txd_bytes += (len + 15) & ~15u;
+}
+
 void tx_queue(ThreadState &t, uint8_t *ip, uint32_t span, uint16_t hl, int16_t fo)
 {
 	const TxEntry e = {ip, span, hl, fo};
@@ -292,9 +316,27 @@ void tx_queue(ThreadState &t, uint8_t *ip, uint32_t span, uint16_t hl, int16_t f
 		if (ip > t.tx_max) {
 			t.tx_max = ip;
 			t.txq.push_back(e);
+			if (t.txd_ok) {
+				if (t.txd_fast.empty()) { // the range of the window's first call
+					t.txd_lo = t.reg_last.lo;
+					t.txd_hi = t.reg_last.hi;
+				}
+				if (ip >= t.txd_lo && ip + span <= t.txd_hi) {
+					txd_close(t);
+					t.txd_fast.push_back({(uint64_t)(ip - t.txd_lo), 0, (uint16_t)span});
+					t.txd_h = fo < 0 ? span : 0;
+					t.txd_s = fo < 0 ? 0 : span;
+				} else {
+					t.txd_ok = false; // a second range: the post builds the batch
+				}
+			}
 			return;
 		}
 		if (ip == t.tx_max) {
+			if (t.txd_ok) { // the current packet's other entry, or a later call for the same one
+				(fo < 0 ? t.txd_h : t.txd_s) = span;
+				t.txd_fast.back().ip_len = (uint16_t)(t.txd_h > t.txd_s ? t.txd_h : t.txd_s);
+			}
 			for (size_t i = t.txq.size(); i-- > 0 && t.txq[i].ip == ip;)
 				if ((t.txq[i].fo < 0) == (fo < 0)) {
 					t.txq[i] = e;
@@ -303,6 +345,7 @@ void tx_queue(ThreadState &t, uint8_t *ip, uint32_t span, uint16_t hl, int16_t f
 			t.txq.push_back(e);
 			return;
 		}
+		t.txd_ok = false; // out of address order: the map, and the post builds the batch
 		t.txidx.reset(2 * t.txq.size() + 64);
 		for (size_t i = 0; i < t.txq.size(); i++)
 			t.txidx.put(((uintptr_t)t.txq[i].ip << 1) | (t.txq[i].fo >= 0 ? 1u : 0u), (uint32_t)i);
@@ -620,6 +663,10 @@ extern "C" int cgck_tx_begin(void)
 	t.txq.clear();
 	t.tx_max = nullptr;
 	t.tx_map = false;
+	t.txd_fast.clear();
+	t.txd_ok = true;
+	t.txd_h = t.txd_s = t.txd_noip = t.txd_max = 0;
+	t.txd_bytes = 0;
 	return 0;
 }
 
@@ -654,9 +701,11 @@ int tx_compute(cgck_ctx *c, TxFill &f, bool post)
 	// the queue checked equals the header call's length) and the segment's
 	// L4 checksum from one read of the frame.
 	f.idx.resize(n);
+	f.stored = false;
 	if (inplace) {
 		f.d.resize(n);
 		uint64_t m = 0;
+		bool l4_alone = false; // a packet with its segment queued but not its header
 		for (uint64_t i = 0; i < n; i++) {
 			if (i > 0 && q[i].ip == q[i - 1].ip && (q[i].fo < 0) != (q[i - 1].fo < 0) && f.idx[i - 1] == m - 1 &&
 			    (i < 2 || f.idx[i - 2] != m - 1)) {
@@ -665,6 +714,8 @@ int tx_compute(cgck_ctx *c, TxFill &f, bool post)
 					f.d[m - 1].ip_len = (uint16_t)q[i].span;
 				continue;
 			}
+			if (q[i].fo >= 0 && !(i + 1 < n && q[i + 1].ip == q[i].ip && q[i + 1].fo < 0))
+				l4_alone = true;
 			f.idx[i] = (uint32_t)m;
 			f.d[m].frame_off = (uint64_t)(q[i].ip - reg.lo);
 			f.d[m].l3_off = 0;
@@ -672,9 +723,18 @@ int tx_compute(cgck_ctx *c, TxFill &f, bool post)
 			m++;
 		}
 		f.o.resize(m);
-		if (post)
-			return desc_host_post(c, reg.lo, (size_t)(reg.hi - reg.lo), f.d.data(), m, kTxFlags, f.o.data(),
-					      nullptr, nullptr, &f.pend);
+		if (post) {
+			// Posted: when every packet's header is queued (alone, or with its
+			// segment), the kernel stores the fields itself (CGCK_STORE: ip+10,
+			// and the L4 field of a descriptor that covers the segment), so
+			// completing the fill writes nothing on the host.  A header-only
+			// descriptor covers ip_hl * 4 bytes: no L4 field fits in it, none
+			// is stored.
+			f.stored = !l4_alone;
+			return desc_host_post(c, reg.lo, (size_t)(reg.hi - reg.lo), f.d.data(), m,
+					      kTxFlags | (f.stored ? CGCK_STORE : 0u), f.stored ? nullptr : f.o.data(), nullptr,
+					      nullptr, &f.pend);
+		}
 		return desc_host(c, reg.lo, (size_t)(reg.hi - reg.lo), f.d.data(), m, kTxFlags, f.o.data(), nullptr);
 	}
 	for (uint64_t i = 0; i < n; i++)
@@ -771,6 +831,10 @@ extern "C" int cgck_tx_post(void)
 		return set_err(-EBUSY, "cgck_tx_post: two fills already posted and not yet completed");
 	}
 	TxFill &f = t.txp[(t.txp_head + t.txp_count) & 1];
+	txd_close(t);
+	// the descriptors built as the calls came, when every packet's header is
+	// among them: the kernel stores every field (CGCK_STORE)
+	const bool fast = t.txd_ok && !t.tx_map && t.txd_noip == 0 && !t.txd_fast.empty();
 	tx_take(t, f);
 	f.pend.seq = 0;
 	f.pend.rc = 0;
@@ -779,7 +843,16 @@ extern "C" int cgck_tx_post(void)
 		cgck_ctx *c = thread_ctx();
 		if (!c)
 			return -ENODEV;
-		int rc = tx_compute(c, f, true);
+		int rc;
+		if (fast) {
+			f.d.swap(t.txd_fast);
+			f.stored = true;
+			const DescSummary sum = {t.txd_max, t.txd_bytes};
+			rc = desc_host_post(c, (void *)t.txd_lo, (size_t)(t.txd_hi - t.txd_lo), f.d.data(), f.d.size(),
+					    kTxFlags | CGCK_STORE, nullptr, nullptr, nullptr, &f.pend, &sum);
+		} else {
+			rc = tx_compute(c, f, true);
+		}
 		if (rc < 0) {
 			f.q.clear();
 			return rc;
@@ -801,6 +874,11 @@ extern "C" int cgck_tx_complete(void)
 	if (rc < 0) {
 		f.q.clear();
 		return rc;
+	}
+	if (f.stored) { // the kernel wrote them
+		const int n = (int)f.q.size();
+		f.q.clear();
+		return n;
 	}
 	return tx_write(f);
 }

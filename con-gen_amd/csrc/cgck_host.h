@@ -110,8 +110,16 @@ int desc_host(cgck_ctx *c, void *base, size_t bytes, const cgck_desc_t *desc, ui
 // out / verdict / meta, which must stay valid until then); 0 when it was
 // computed at once (no server, or it does not fit); a negative errno.  A
 // later request on the context that needs the slot collects it first.
+// sum (optional): the longest ip_len and the 16-byte-rounded packet bytes of
+// descriptors the library built itself inside [base, base + bytes), so the
+// per-descriptor check is skipped.
+struct DescSummary {
+	uint32_t max_len;
+	size_t pkt_bytes;
+};
 int desc_host_post(cgck_ctx *c, void *base, size_t bytes, const cgck_desc_t *desc, uint64_t n, uint32_t flags,
-		   uint32_t *out, uint8_t *verdict, uint32_t *meta, BurstPending *pend);
+		   uint32_t *out, uint8_t *verdict, uint32_t *meta, BurstPending *pend,
+		   const DescSummary *sum = nullptr);
 int burst_collect(cgck_ctx *c, BurstPending *pend);
 
 // Staging path of one region for the drop-in symbols (burst server when open,

@@ -17,6 +17,12 @@
  *               cgck_tx_flush() (glue.c:15-41 batch point), the flush writing
  *               every field in place.
  *
+ *   rx_reference_loop / tx_reference_loop — the same RX and TX loops (the
+ *               field save / zero / restore and stores included) calling the
+ *               reference's own in_cksum / udp_cksum (subr.c:186-223, built
+ *               by oracle/build_ref.sh into oracle/_ref/libref_cksum.so) on
+ *               one core: the CPU cost the windows replace, measured by the
+ *               same harness.
  *   rx_window_pipelined / tx_fill_pipelined — the same with one burst in
  *               flight (cgck_rx_post + cgck_rx_begin_posted, cgck_tx_post +
  *               cgck_tx_complete): burst k is posted, then the stack works
@@ -39,12 +45,15 @@
  *
  *   tools/txburst [seconds per cell, default 0.4]
  */
+#include <dlfcn.h>
+#include <libgen.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <sys/mman.h>
 #include <time.h>
+#include <unistd.h>
 
 #include "cgck.h"
 
@@ -165,6 +174,25 @@ int main(int argc, char **argv)
 		}
 		return 0;
 	}
+	/* the reference's checksum unit, for the same-harness CPU rows */
+	typedef uint16_t (*in_fn)(void *, int);
+	typedef uint16_t (*udp_fn)(struct ip *, int);
+	in_fn ref_in = NULL;
+	udp_fn ref_udp = NULL;
+	{
+		char exe[4096];
+		const ssize_t k = readlink("/proc/self/exe", exe, sizeof(exe) - 64);
+		if (k > 0) {
+			exe[k] = 0;
+			char path[4200];
+			snprintf(path, sizeof(path), "%s/../oracle/_ref/libref_cksum.so", dirname(exe));
+			void *h = dlopen(path, RTLD_NOW | RTLD_LOCAL);
+			if (h) {
+				ref_in = (in_fn)dlsym(h, "in_cksum");
+				ref_udp = (udp_fn)dlsym(h, "udp_cksum");
+			}
+		}
+	}
 	for (int li = 0; li < nl; li++) {
 		const int len = lens[li];
 		uint64_t s = 0x9E3779B97F4A7C15ull;
@@ -185,6 +213,54 @@ int main(int argc, char **argv)
 		/* corrupt one payload byte of every 64th packet (both halves) */
 		for (int i = 0; i < 2 * maxb; i += 64)
 			ring[(size_t)i * SLOT + L3 + len - 1] ^= 0x5A;
+		uint8_t *keep = ref_in && ref_udp ? malloc((size_t)2 * maxb * SLOT) : NULL;
+		if (keep) /* the reference rows rewrite fields: the ring is put back afterwards */
+			memcpy(keep, ring, (size_t)2 * maxb * SLOT);
+		for (int bi = 0; bi < nb && keep; bi++) { /* the reference loop, same harness */
+			const int R = bursts[bi];
+			for (int mode = 0; mode < 2; mode++) {
+				int it = 0, w = 0;
+				volatile int sink = 0;
+				double t0 = now();
+				while (it < maxit && now() - t0 < budget) {
+					double a = now();
+					int bad = 0;
+					for (int i = 0; i < R; i++) {
+						uint8_t *ip = ring + (size_t)i * SLOT + L3;
+						uint16_t saved, v;
+						if (mode == 0) { /* RX: verify, field zeroed and restored */
+							memcpy(&saved, ip + 10, 2);
+							ip[10] = ip[11] = 0;
+							v = ref_in(ip, 20);
+							bad += v != saved;
+							memcpy(ip + 10, &saved, 2);
+							memcpy(&saved, ip + 20 + 16, 2);
+							ip[20 + 16] = ip[20 + 17] = 0;
+							v = ref_udp((struct ip *)ip, len - 20);
+							bad += v != saved;
+							memcpy(ip + 20 + 16, &saved, 2);
+						} else { /* TX: fill */
+							ip[20 + 16] = ip[20 + 17] = 0;
+							v = ref_udp((struct ip *)ip, len - 20);
+							memcpy(ip + 20 + 16, &v, 2);
+							ip[10] = ip[11] = 0;
+							v = ref_in(ip, 20);
+							memcpy(ip + 10, &v, 2);
+						}
+					}
+					sink += bad;
+					if (w++ >= 20)
+						t[it++] = now() - a;
+				}
+				printf("{\"mode\": \"%s\", \"pkt_len\": %d, \"burst\": %d, \"iters\": %d, \"us_median\": %.2f}\n",
+				       mode ? "tx_reference_loop" : "rx_reference_loop", len, R, it, median(t, it) * 1e6);
+				fflush(stdout);
+			}
+		}
+		if (keep) {
+			memcpy(ring, keep, (size_t)2 * maxb * SLOT);
+			free(keep);
+		}
 		/* passes: 0 launch path, 1 registered ring, 2 burst server, 3 server + registered */
 		for (int pass = 0; pass < 4; pass++) {
 			const int reg = pass & 1, srv = pass >= 2;
@@ -325,6 +401,8 @@ int main(int argc, char **argv)
 					}
 					if (k > 0) {
 						aw = now();
+						if (k > 20)
+							tc[it] = aw - a; /* the post */
 						if (cgck_rx_begin_posted() != R) {
 							fprintf(stderr, "txburst: rx_begin_posted failed: %s\n", cgck_last_error());
 							return 1;
@@ -363,11 +441,12 @@ int main(int argc, char **argv)
 				/* drain the last posted burst */
 				cgck_rx_begin_posted();
 				cgck_rx_end();
-				const double us = median(t, it) * 1e6, us_wait = median(tw, it) * 1e6;
+				const double us = median(t, it) * 1e6, us_wait = median(tw, it) * 1e6,
+					     us_post = median(tc, it) * 1e6;
 				printf("{\"mode\": \"rx_window_pipelined_registered_server\", \"pkt_len\": %d, \"burst\": %d, "
-				       "\"iters\": %d, \"us_median\": %.2f, \"us_wait\": %.2f, \"stack_us\": %.1f, "
-				       "\"bad_ip\": %d, \"bad_l4\": %d, \"bad_l4_expected\": %d}\n",
-				       len, R, it, us, us_wait, stack_us, bad_ip, bad_l4, (R + 63) / 64);
+				       "\"iters\": %d, \"us_median\": %.2f, \"us_wait\": %.2f, \"us_post\": %.2f, "
+				       "\"stack_us\": %.1f, \"bad_ip\": %d, \"bad_l4\": %d, \"bad_l4_expected\": %d}\n",
+				       len, R, it, us, us_wait, us_post, stack_us, bad_ip, bad_l4, (R + 63) / 64);
 				fflush(stdout);
 			}
 			for (int bi = 0; bi < nb && pass == 3; bi++) { /* TX, one fill in flight */
