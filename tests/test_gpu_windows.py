@@ -415,3 +415,76 @@ def test_tx_pipelined_fill(port, server):
         if server:
             cgck.burst_close()
         L.cgck_host_unregister(ring.ctypes.data)
+
+
+def expected_calls(port, pkt, fo, seg, hdr):
+    """The packet's bytes after the calls the stack made on it: the segment's
+    field when udp_cksum was queued, the header's when in_cksum was."""
+    ref = pkt.copy()
+    if seg:
+        ref[20 + fo:22 + fo] = 0
+        ref[20 + fo:22 + fo] = np.frombuffer(np.uint16(port.udp_cksum(ref, 0, len(ref) - 20)).tobytes(), np.uint8)
+    if hdr:
+        ref[10:12] = 0
+        ref[10:12] = np.frombuffer(np.uint16(port.in_cksum(ref, 0, 20)).tobytes(), np.uint8)
+    return ref
+
+
+@pytest.mark.parametrize("server", [False, True])
+@pytest.mark.parametrize("shape", ["header_only", "segment_only", "out_of_order", "replaced", "unregistered"])
+def test_tx_pipelined_irregular(port, server, shape):
+    """The posted fill off the common path: packets with only their header
+    queued (an ICMP reply, ip_output alone), packets with only their segment
+    queued, slots queued out of address order (a ring wrap), a slot queued
+    again with a shorter packet, and stack-local packets among the ring's.
+    Each burst's fields equal the reference's over the packet's final bytes
+    and tx_post counts the queued fields."""
+    rng = np.random.default_rng(900 + 10 * server + len(shape))
+    raw, ring, size = rxcorpus.registered_copy(np.zeros(128 * 2048, np.uint8))
+    slots = ring[:128 * 2048].reshape(128, 2048)
+    local = np.zeros((128, 2048), np.uint8)
+    L = cgck.load()
+    assert L.cgck_host_register(ring.ctypes.data, size) == 0
+    if server:
+        cgck.burst_open(max_pkts=1024, max_bytes=4 << 20)
+    try:
+        for k in range(3):
+            order = list(range(k * 40, k * 40 + 40))
+            if shape == "out_of_order":
+                order = order[20:] + order[:20]
+            want, fields = {}, 0
+            cgck.tx_begin()
+            for j, i in enumerate(order):
+                tgt = local if shape == "unregistered" and j % 3 == 1 else slots
+                seg = not (shape == "header_only" and j % 4 == 2)
+                hdr = not (shape == "segment_only" and j % 5 == 3)
+                ln = int(rng.integers(40, 1501))
+                pkt = tcp_pkt(rng, ln)
+                tgt[i, 14:14 + ln] = pkt
+                if seg:
+                    tgt[i, 14 + 36:14 + 38] = 0
+                    v = cgck.udp_cksum(tgt[i], 14, ln - 20)
+                    tgt[i, 14 + 36:14 + 38] = np.frombuffer(np.uint16(v).tobytes(), np.uint8)
+                if hdr:
+                    tgt[i, 14 + 10:14 + 12] = 0
+                    v = cgck.ip_cksum(tgt[i], 14)
+                    tgt[i, 14 + 10:14 + 12] = np.frombuffer(np.uint16(v).tobytes(), np.uint8)
+                if shape == "replaced" and j == 7:     # the slot gets a shorter packet before the post
+                    ln2 = int(rng.integers(40, ln + 1))
+                    pkt = tcp_pkt(rng, ln2)
+                    tgt[i, 14:14 + ln] = 0
+                    tgt[i, 14:14 + ln2] = pkt
+                    ln = ln2
+                    tx_calls(tgt[i], ln, 16)
+                fields += (seg + hdr) if tgt is slots else 0
+                want[(id(tgt), i)] = (tgt, i, ln, pkt.copy(), seg, hdr)
+            assert cgck.tx_post() == fields, (shape, k)
+            assert cgck.tx_complete() == fields
+            for tgt, i, ln, pkt, seg, hdr in want.values():
+                ref = expected_calls(port, pkt, 16, seg, hdr)   # a field not asked for keeps its bytes
+                assert np.array_equal(tgt[i, 14:14 + ln], ref), (shape, k, i, seg, hdr)
+        assert cgck.tx_complete() == 0
+    finally:
+        if server:
+            cgck.burst_close()
+        L.cgck_host_unregister(ring.ctypes.data)

@@ -24,6 +24,10 @@ for step in "$@"; do
 	testsk) run pytest_gpu 900 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread || true ;;
 	quick) run pytest_quick 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "burst or window or pipelined or rx_post or tx_" || exit 1 ;;
 	txburst) run txburst 400 tools/txburst 0.2 || exit 1 ;;
+	txstack) # the same rows with 150 us of other stack work between bursts
+		TXBURST_STACK_US=150 run txburst_stack150 400 tools/txburst 0.2 || exit 1 ;;
+	txtouch) # the TX rows with each frame's line written by the core before the clock starts
+		TXBURST_PRETOUCH=1 run txburst_pretouch 400 tools/txburst 0.2 || exit 1 ;;
 	bench) run bench 600 python -u bench.py || exit 1 ;;
 	bench2) run bench_n2 600 python -u bench.py --gpus 2 --allow-shared-devices --steps 5 --warmup 2 --no-burst || exit 1 ;;
 	stress) run stress 110 python -u tools/reg_stress.py 60 plain || exit 1 ;;

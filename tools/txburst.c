@@ -97,6 +97,12 @@ static double median(double *t, int n)
 	return t[n / 2];
 }
 
+/* after median() sorted t: the p-th percentile */
+static double pct(const double *t, int n, int p)
+{
+	return t[(long)n * p / 100 < n ? (long)n * p / 100 : n - 1];
+}
+
 int main(int argc, char **argv)
 {
 	const double budget = argc > 1 ? atof(argv[1]) : 0.4;
@@ -124,12 +130,14 @@ int main(int argc, char **argv)
 			ring = NULL;
 	}
 	const double stack_us = getenv("TXBURST_STACK_US") ? atof(getenv("TXBURST_STACK_US")) : 50.0;
+	const int pretouch = getenv("TXBURST_PRETOUCH") && atoi(getenv("TXBURST_PRETOUCH"));
 	cgck_desc_t *desc = malloc(sizeof(cgck_desc_t) * maxb);
 	uint32_t *out = malloc(4 * maxb);
 	uint8_t *ver = malloc(maxb);
 	double *t = malloc(sizeof(double) * maxit);
 	double *tc = malloc(sizeof(double) * maxit); /* RX window: the per-packet calls + rx_end only */
 	double *tw = malloc(sizeof(double) * maxit); /* pipelined: the wait for the previous burst */
+	double *tp = malloc(sizeof(double) * maxit); /* pipelined TX: cgck_tx_post */
 	cgck_ctx_t *ctx;
 	if (!ring || !desc || !out || !ver || !t || !tc || !tw || cgck_ctx_create(0, &ctx)) {
 		fprintf(stderr, "txburst: setup failed: %s\n", cgck_last_error());
@@ -455,6 +463,11 @@ int main(int argc, char **argv)
 				double t0 = now();
 				while (it < maxit && now() - t0 < budget + 0.05) {
 					uint8_t *half = ring + (size_t)(k & 1) * maxb * SLOT;
+					if (pretouch) /* lab split: the frames' lines owned by this core before the clock starts */
+						for (int i = 0; i < R; i++) {
+							volatile uint8_t *ip = half + (size_t)i * SLOT + L3;
+							ip[36] = ip[36];
+						}
 					double a = now();
 					cgck_tx_begin();
 					for (int i = 0; i < R; i++) {
@@ -467,12 +480,17 @@ int main(int argc, char **argv)
 						v = in_cksum(ip, 20);
 						memcpy(ip + 10, &v, 2);
 					}
+					const double ap = now();
+					if (k > 20)
+						tc[it] = ap - a;
 					if (cgck_tx_post() != 2 * R) {
 						fprintf(stderr, "txburst: tx_post failed: %s\n", cgck_last_error());
 						return 1;
 					}
 					double aw = now(), w = 0;
 					if (k > 0) {
+						if (k > 20)
+							tp[it] = aw - ap;
 						const int r = cgck_tx_complete(); /* burst k - 1, before its kick */
 						w = now() - aw;
 						if (r != 2 * R) {
@@ -491,9 +509,14 @@ int main(int argc, char **argv)
 				}
 				cgck_tx_complete();
 				const double us = median(t, it) * 1e6, us_wait = median(tw, it) * 1e6;
+				const double p10 = pct(t, it, 10) * 1e6, p90 = pct(t, it, 90) * 1e6;
+				const double us_calls = median(tc, it) * 1e6, calls_p90 = pct(tc, it, 90) * 1e6;
+				const double us_post = median(tp, it) * 1e6, post_p90 = pct(tp, it, 90) * 1e6;
 				printf("{\"mode\": \"tx_fill_pipelined_registered_server\", \"pkt_len\": %d, \"burst\": %d, "
-				       "\"iters\": %d, \"us_median\": %.2f, \"us_wait\": %.2f, \"stack_us\": %.1f}\n",
-				       len, R, it, us, us_wait, stack_us);
+				       "\"iters\": %d, \"us_median\": %.2f, \"us_p10\": %.2f, \"us_p90\": %.2f, "
+				       "\"us_wait\": %.2f, \"us_calls\": %.2f, \"us_calls_p90\": %.2f, \"us_post\": %.2f, "
+				       "\"us_post_p90\": %.2f, \"stack_us\": %.1f}\n",
+				       len, R, it, us, p10, p90, us_wait, us_calls, calls_p90, us_post, post_p90, stack_us);
 				fflush(stdout);
 			}
 			if (srv) {
