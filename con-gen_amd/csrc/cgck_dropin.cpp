@@ -124,7 +124,10 @@ struct TxFill {
 	std::vector<uint32_t> o, idx; // idx: the value (descriptor) of each queued entry
 	BurstPending pend{};
 	bool stored = false; // the kernel wrote the fields in place (CGCK_STORE): nothing left to write
-	int n = 0;           // the fields it stands for (q is empty when stored)
+	bool fast = false;   // posted in the fast form: o[k] is descriptor k's values, hs its spans
+	int n = 0;           // the fields it stands for (q is empty in the fast form)
+	std::vector<uint32_t> hs;
+	uint8_t *lo = nullptr;
 };
 
 struct ThreadState {
@@ -298,7 +301,7 @@ inline bool tx_registered(ThreadState &t, const uint8_t *p, size_t bytes)
 
 // The current packet's descriptor closed: its spans, its length and whether
 // its header was queued enter the window's summary.
-inline void txd_close(ThreadState &t)
+__attribute__((always_inline)) inline void txd_close(ThreadState &t)
 {
 	if (t.txd_fast.size() == t.txd_hs.size())
 		return; // none open
@@ -337,8 +340,10 @@ __attribute__((noinline)) void txd_spill(ThreadState &t)
 // duplicate can only be the current packet's (the fast form keeps only the
 // descriptors; the general form scans the last entries); the first call
 // below it (ring wrap, a slot handed out again) switches to a map of every
-// entry.
-void tx_queue(ThreadState &t, uint8_t *ip, uint32_t span, uint16_t hl, int16_t fo)
+// entry.  tx_queue: the fast form's two common calls (the next packet in
+// the range, the current packet's other entry) inline in the drop-ins; the
+// window's first call and everything else here.
+__attribute__((noinline)) void tx_queue_slow(ThreadState &t, uint8_t *ip, uint32_t span, uint16_t hl, int16_t fo)
 {
 	const TxEntry e = {ip, span, hl, fo};
 	if (!t.tx_map) {
@@ -393,6 +398,31 @@ void tx_queue(ThreadState &t, uint8_t *ip, uint32_t span, uint16_t hl, int16_t f
 	}
 	t.txidx.put(k, (uint32_t)t.txq.size());
 	t.txq.push_back(e);
+}
+
+__attribute__((always_inline)) inline void tx_queue(ThreadState &t, uint8_t *ip, uint32_t span, uint16_t hl,
+						     int16_t fo)
+{
+	if (__builtin_expect(t.txd_ok, 1)) {
+		// (a non-empty fast form: txd_lo <= tx_max, so ip > tx_max is in the range from below)
+		if (ip > t.tx_max && !t.txd_fast.empty() && ip + span <= t.txd_hi) {
+			t.tx_max = ip;
+			txd_close(t);
+			t.txd_fast.push_back({(uint64_t)(ip - t.txd_lo), 0, (uint16_t)span});
+			t.txd_h = fo < 0 ? span : 0;
+			t.txd_s = fo < 0 ? 0 : span;
+			t.txd_calls++;
+			return;
+		}
+		if (ip == t.tx_max) {
+			uint32_t &sp = fo < 0 ? t.txd_h : t.txd_s;
+			t.txd_calls += sp == 0;
+			sp = span;
+			t.txd_fast.back().ip_len = (uint16_t)(t.txd_h > t.txd_s ? t.txd_h : t.txd_s);
+			return;
+		}
+	}
+	tx_queue_slow(t, ip, span, hl, fo);
 }
 
 } // namespace
@@ -713,6 +743,15 @@ namespace {
 // gbtcp/tcp.c:426,436).
 constexpr uint32_t kTxFlags = CGCK_IP | CGCK_L4 | CGCK_ZERO_FIELDS;
 
+// Posted fills return values and the completion writes the fields on the
+// host (see cgck_tx_post); the lab build's $CGCK_TX_KSTORE has the kernel
+// store them instead (CGCK_STORE), for the A/B.
+inline bool tx_kstore()
+{
+	static const bool k = CGCK_ENV("CGCK_TX_KSTORE") != nullptr;
+	return k;
+}
+
 // Compute the values of f.q: when every entry lies in one registered range
 // (the transport's pool) the batch is described in place, as cgck_desc_host
 // of that range — the burst server when one is open on this context and the
@@ -759,13 +798,13 @@ int tx_compute(cgck_ctx *c, TxFill &f, bool post)
 		}
 		f.o.resize(m);
 		if (post) {
-			// Posted: when every packet's header is queued (alone, or with its
-			// segment), the kernel stores the fields itself (CGCK_STORE: ip+10,
-			// and the L4 field of a descriptor that covers the segment), so
-			// completing the fill writes nothing on the host.  A header-only
-			// descriptor covers ip_hl * 4 bytes: no L4 field fits in it, none
-			// is stored.
-			f.stored = !l4_alone;
+			// Posted: completing the fill writes the fields from the values
+			// (tx_write).  Lab ($CGCK_TX_KSTORE): when every packet's header
+			// is queued (alone, or with its segment), the kernel stores them
+			// (CGCK_STORE: ip+10, and the L4 field of a descriptor that
+			// covers the segment; a header-only descriptor covers
+			// ip_hl * 4 bytes, so no L4 field fits in it and none is stored).
+			f.stored = tx_kstore() && !l4_alone;
 			return desc_host_post(c, reg.lo, (size_t)(reg.hi - reg.lo), f.d.data(), m,
 					      kTxFlags | (f.stored ? CGCK_STORE : 0u), f.stored ? nullptr : f.o.data(), nullptr,
 					      nullptr, &f.pend);
@@ -820,6 +859,28 @@ int tx_write(TxFill &f)
 	}
 	f.q.clear();
 	return (int)n;
+}
+
+// The fields of a fill posted in the fast form, from descriptor k's values:
+// its header's (ip+10) when the header was queued, its segment's when the
+// segment was (at ip_hl * 4 + 16 for TCP, + 6 for UDP, read from the packet
+// as the call read them).
+int tx_write_fast(TxFill &f)
+{
+	const size_t m = f.d.size();
+	for (size_t k = 0; k < m; k++) {
+		uint8_t *ip = f.lo + f.d[k].frame_off;
+		const uint32_t r = f.o[k], hs = f.hs[k];
+		if (hs & 0xffff) {
+			const uint16_t v = (uint16_t)(r >> 16);
+			memcpy(ip + (ip[0] & 15) * 4 + (ip[9] == 6 ? 16 : 6), &v, 2);
+		}
+		if (hs >> 16) {
+			const uint16_t v = (uint16_t)r;
+			memcpy(ip + 10, &v, 2);
+		}
+	}
+	return f.n;
 }
 
 // Close the window and move its queue into f.
@@ -879,20 +940,31 @@ extern "C" int cgck_tx_post(void)
 	f.pend.seq = 0;
 	f.pend.rc = 0;
 	f.n = n;
+	f.fast = false;
 	if (n) {
 		cgck_ctx *c = thread_ctx();
 		if (!c)
 			return -ENODEV;
 		int rc;
 		if (fast) {
-			// (the kernel's stores against a host write-back from the values,
-			// A/B'd on one box: 3.9 / 3.7 us at 256 x 64 B, 27.3 / 25.1 at
-			// 2048; stored keeps the completion off the worker thread)
+			// The kernel returns each descriptor's two values and the
+			// completion writes the fields (tx_write_fast): a ring line
+			// the GPU stores into leaves the worker's caches, so the stack's
+			// next writes to that slot miss (kernel
+			// stores 3.9 against 3.7 us at 256 x 64 B, and 27-55 against 25
+			// at 2048).
+			const bool kstore = tx_kstore();
 			f.d.swap(t.txd_fast);
-			f.stored = true;
+			f.hs.swap(t.txd_hs);
+			f.lo = const_cast<uint8_t *>(t.txd_lo);
+			f.stored = kstore;
+			f.fast = !kstore;
+			if (f.fast)
+				f.o.resize(f.d.size());
 			const DescSummary sum = {t.txd_max, t.txd_bytes};
 			rc = desc_host_post(c, (void *)t.txd_lo, (size_t)(t.txd_hi - t.txd_lo), f.d.data(), f.d.size(),
-					    kTxFlags | CGCK_STORE, nullptr, nullptr, nullptr, &f.pend, &sum);
+					    kTxFlags | (kstore ? CGCK_STORE : 0u), kstore ? nullptr : f.o.data(), nullptr, nullptr,
+					    &f.pend, &sum);
 		} else {
 			rc = tx_compute(c, f, true);
 		}
@@ -922,6 +994,8 @@ extern "C" int cgck_tx_complete(void)
 		f.q.clear();
 		return f.n;
 	}
+	if (f.fast)
+		return tx_write_fast(f);
 	return tx_write(f);
 }
 

@@ -241,10 +241,10 @@ int cgck_tx_flush(void);
 /* Pipelined TX fill: cgck_tx_post closes the window like cgck_tx_flush but
  * returns once the fill is posted (the number of fields queued); the fields
  * are final once cgck_tx_complete, which waits for the oldest posted fill,
- * returns how many it wrote (0: none posted).  When every queued packet's
- * header is among the calls (the finalisers' order: segment, then header),
- * the kernel writes the fields in place itself; otherwise the completion
- * writes them from the host.  The transport calls
+ * returns how many it wrote (0: none posted).  The kernel returns the
+ * values and the completion writes the fields from the host, so the ring
+ * lines stay in the worker's caches for the stack's next writes to those
+ * slots.  The transport calls
  * it before it hands those slots to the NIC — at the next loop's kick
  * (con-gen.c:493), so the GPU computes burst k while the stack builds burst
  * k + 1.  At most two fills are posted and not yet completed (-EBUSY). */

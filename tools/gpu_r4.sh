@@ -26,6 +26,8 @@ for step in "$@"; do
 	txburst) run txburst 400 tools/txburst 0.2 || exit 1 ;;
 	txstack) # the same rows with 150 us of other stack work between bursts
 		TXBURST_STACK_US=150 run txburst_stack150 400 tools/txburst 0.2 || exit 1 ;;
+	txkstore) # lab: the kernel stores the posted fills' fields (CGCK_STORE) instead of the host
+		LD_LIBRARY_PATH=$PWD/tools/labso CGCK_TX_KSTORE=1 run txburst_kstore 400 tools/txburst 0.2 || exit 1 ;;
 	txtouch) # the TX rows with each frame's line written by the core before the clock starts
 		TXBURST_PRETOUCH=1 run txburst_pretouch 400 tools/txburst 0.2 || exit 1 ;;
 	bench) run bench 600 python -u bench.py || exit 1 ;;
