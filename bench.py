@@ -364,7 +364,8 @@ def bench_burst():
 
 
 BURST_COLS = ["pkt_len", "burst", "rx_window_launch_us", "rx_window_server_us", "rx_window_pipelined_us",
-              "tx_fill_launch_us", "tx_fill_server_us", "tx_fill_pipelined_us", "cpu_ref_us"]
+              "tx_fill_launch_us", "tx_fill_server_us", "tx_fill_pipelined_us", "rx_ref_loop_us", "tx_ref_loop_us",
+              "cpu_ref_us"]
 # (column, txburst mode): each column is ONE routing, as measured (no per-cell
 # minimum over routings): the launch path (no server open), the burst server
 # opened wide (every burst of the cell goes to it), and the server with one
@@ -376,6 +377,10 @@ BURST_MODES = (("rx_window_launch_us", "rx_window_registered"),
                ("tx_fill_launch_us", "tx_fill_registered"),
                ("tx_fill_server_us", "tx_fill_registered_server"),
                ("tx_fill_pipelined_us", "tx_fill_pipelined_registered_server"))
+# the reference's own in_cksum / udp_cksum (oracle/_ref) in the same binary on
+# the same ring: the RX loop saves / zeroes / computes / restores each field,
+# the TX loop zeroes / computes / stores (one core, the harness's thread)
+BURST_REF = (("rx_ref_loop_us", "rx_reference_loop"), ("tx_ref_loop_us", "tx_reference_loop"))
 
 
 def burst_summary(rows, cpu):
@@ -387,7 +392,7 @@ def burst_summary(rows, cpu):
         return rows
     by = {(r["mode"], r["pkt_len"], r["burst"]): r["us_median"] for r in rows}
     cpu_by = {(r["pkt_len"], r["burst"]): round(r["us_per_burst"], 2) for r in (cpu or {}).get("rows", [])}
-    return [[ln, b] + [by.get((m, ln, b)) for _, m in BURST_MODES] + [cpu_by.get((ln, b))]
+    return [[ln, b] + [by.get((m, ln, b)) for _, m in BURST_MODES + BURST_REF] + [cpu_by.get((ln, b))]
             for ln in sorted(BURST_LENS) for b in (32, 256, 2048)]
 
 

@@ -92,7 +92,7 @@ def test_device_for_refuses_oversubscription():
 
 
 def test_burst_summary_is_compact():
-    modes = [m for _, m in bench.BURST_MODES]
+    modes = [m for _, m in bench.BURST_MODES + bench.BURST_REF]
     rows = [{"mode": m, "pkt_len": ln, "burst": b, "us_median": 1.0 + i}
             for i, m in enumerate(modes) for ln in bench.BURST_LENS for b in bench.BURSTS]
     cpu = {"rows": [{"pkt_len": ln, "burst": b, "us_per_burst": 2.0} for ln in bench.BURST_LENS for b in bench.BURSTS]}

@@ -31,6 +31,7 @@ for step in "$@"; do
 	txtouch) # the TX rows with each frame's line written by the core before the clock starts
 		TXBURST_PRETOUCH=1 run txburst_pretouch 400 tools/txburst 0.2 || exit 1 ;;
 	bench) run bench 600 python -u bench.py || exit 1 ;;
+	smoke) run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" || exit 1 ;;
 	bench2) run bench_n2 600 python -u bench.py --gpus 2 --allow-shared-devices --steps 5 --warmup 2 --no-burst || exit 1 ;;
 	stress) run stress 110 python -u tools/reg_stress.py 60 plain || exit 1 ;;
 	stressm) for m in heap plain lock mmap; do run stress_$m 110 python -u tools/reg_stress.py 40 $m || exit 1; done ;;
