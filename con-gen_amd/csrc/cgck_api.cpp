@@ -508,6 +508,11 @@ static int burst_wait(cgck_ctx *c, uint32_t seq, uint32_t n, uint64_t range)
 #if CGCK_LAB
 	t_lab_host[1] = (uint64_t)(now_s() * 1e9);
 #endif
+	// The response lines were written by the GPU, so none is in this core's
+	// caches: start their first misses now, beside the refused word's.
+	const uint8_t *o = burst_resp(c, seq);
+	for (uint32_t at = 0; at < 4 * n && at < 512; at += 64)
+		__builtin_prefetch(o + at);
 	c->bdone = seq;
 	if (__atomic_load_n(&b->refused[seq & 1], __ATOMIC_ACQUIRE) == seq)
 		return set_err(-EIO,
