@@ -488,3 +488,71 @@ def test_tx_pipelined_irregular(port, server, shape):
         if server:
             cgck.burst_close()
         L.cgck_host_unregister(ring.ctypes.data)
+
+
+def test_rx_tx_pipelined_loop(port):
+    """con-gen's worker loop with both windows pipelined on one thread and
+    one burst server (con-gen.c:484-538): each iteration completes the
+    previous TX fill before the kick, posts the next receive burst, replays
+    the stack's RX calls over the previous one from its window, then builds
+    and posts this iteration's TX fill.  RX outcomes and ring bytes equal the
+    reference replay's and every TX field equals the reference's, with RX and
+    TX requests sharing the server's two request slots."""
+    R = referee(port)
+    L = cgck.load()
+    raw_tx, tx_ring, tx_size = rxcorpus.registered_copy(np.zeros(2 * 96 * 2048, np.uint8))
+    slots = tx_ring[:2 * 96 * 2048].reshape(2, 96, 2048)
+    assert L.cgck_host_register(tx_ring.ctypes.data, tx_size) == 0
+    rx = []
+    for k in range(6):
+        rng = np.random.default_rng(4200 + k)
+        buf, desc = rxcorpus.ring(rxcorpus.corpus(rng, R, 70 + 30 * k, clean=k % 3 != 1))
+        owner, ring, size = rxcorpus.registered_copy(buf)
+        assert L.cgck_host_register(ring.ctypes.data, size) == 0
+        rx.append((buf, desc, ring[:len(buf)], ring, owner))
+    cgck.burst_open(max_pkts=4096, max_bytes=8 << 20)
+    rng = np.random.default_rng(4300)
+    tx_prev = None
+    try:
+        for k in range(len(rx) + 1):
+            if tx_prev is not None:                      # io_tx(): the previous fill, before the kick
+                assert cgck.tx_complete() == 2 * len(tx_prev)
+                for h, i, ln, ref in tx_prev:
+                    assert np.array_equal(slots[h, i, 14:14 + ln], ref), (k, h, i)
+                tx_prev = None
+            if k < len(rx):
+                _, desc, got, _, _ = rx[k]
+                assert cgck.rx_post(got, desc) == len(desc)
+            if k > 0:                                    # the receive burst of the previous iteration
+                buf, desc, got, _, _ = rx[k - 1]
+                stack, ip_in, tcp_in = FLAGS[(5 * k) % len(FLAGS)]
+                ref = buf.copy()
+                a = port.replay_rx(*R.fn_pointers(), ref, desc.view(np.uint8), len(desc), stack, ip_in, tcp_in)
+                cgck.rx_begin_posted()
+                try:
+                    b = port.replay_rx(*cgck.fn_pointers(), got, desc.view(np.uint8), len(desc), stack, ip_in,
+                                       tcp_in)
+                finally:
+                    cgck.rx_end()
+                cell = (k - 1, stack, ip_in, tcp_in)
+                assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]), cell
+                assert np.array_equal(ref, got), cell
+            if k == len(rx):
+                break
+            h = k & 1                                     # bsd_flush(): this iteration's segments
+            want = []
+            cgck.tx_begin()
+            for i in range(40 + 10 * k):
+                ln = int(rng.integers(40, 1501))
+                pkt = tcp_pkt(rng, ln)
+                slots[h, i, 14:14 + ln] = pkt
+                want.append((h, i, ln, expected(port, pkt, 16)))
+                tx_calls(slots[h, i], ln, 16)
+            assert cgck.tx_post() == 2 * len(want)
+            tx_prev = want
+        assert tx_prev is None and cgck.tx_complete() == 0
+    finally:
+        cgck.burst_close()
+        for _, _, _, ring, _ in rx:
+            L.cgck_host_unregister(ring.ctypes.data)
+        L.cgck_host_unregister(tx_ring.ctypes.data)
