@@ -201,6 +201,67 @@ __global__ __launch_bounds__(256) void toeplitz12x4_ab_kernel(RssParams p, uint6
 	}
 }
 
+// 12-bit tables.  The record's 96 bits, read as one little-endian integer X
+// (dwords w0 w1 w2), split into eight 12-bit fields f = (X >> 12k) & 0xfff, so
+// a tuple costs 8 LDS lookups instead of 12.  T12[k][v] comes from the byte
+// tables by linearity: an even field 2m is byte 3m and the low nibble of byte
+// 3m + 1, an odd field 2m + 1 the high nibble of byte 3m + 1 and byte 3m + 2.
+// The eight tables take 128 KiB of LDS: one workgroup per CU, up to 16 waves.
+__device__ __forceinline__ uint32_t hash12_t12(const uint32_t *T, uint32_t w0, uint32_t w1, uint32_t w2)
+{
+	const uint32_t f2 = __builtin_amdgcn_alignbit(w1, w0, 24), f5 = __builtin_amdgcn_alignbit(w2, w1, 28);
+	return T[w0 & 0xfffu] ^ T[4096 + ((w0 >> 12) & 0xfffu)] ^ T[2 * 4096 + (f2 & 0xfffu)] ^
+	       T[3 * 4096 + ((w1 >> 4) & 0xfffu)] ^ T[4 * 4096 + ((w1 >> 16) & 0xfffu)] ^
+	       T[5 * 4096 + (f5 & 0xfffu)] ^ T[6 * 4096 + ((w2 >> 8) & 0xfffu)] ^ T[7 * 4096 + (w2 >> 20)];
+}
+
+constexpr uint32_t kT12Words = 8 * 4096;
+
+template <int DEPTH, int TPB>
+__global__ __launch_bounds__(TPB) void toeplitz12x4_t12_kernel(RssParams p, uint64_t ng)
+{
+	__shared__ __attribute__((aligned(16))) uint32_t smem[kT12Words + 12 * 256];
+	uint32_t *t8 = smem + kT12Words;
+	const uint32_t CGCK_GLOBAL *gt = (const uint32_t CGCK_GLOBAL *)p.tab;
+	for (uint32_t i = threadIdx.x; i < 12 * 256; i += TPB)
+		t8[i] = gt[i];
+	__syncthreads();
+	for (uint32_t e = threadIdx.x; e < kT12Words; e += TPB) {
+		const uint32_t k = e >> 12, v = e & 4095u, m = k >> 1;
+		smem[e] = (k & 1) ? t8[(3 * m + 1) * 256 + ((v & 15u) << 4)] ^ t8[(3 * m + 2) * 256 + (v >> 4)]
+				  : t8[3 * m * 256 + (v & 255u)] ^ t8[(3 * m + 1) * 256 + ((v >> 8) & 15u)];
+	}
+	__syncthreads();
+	const u32x4_t CGCK_GLOBAL *src = (const u32x4_t CGCK_GLOBAL *)p.data;
+	const uint64_t NI = (ng + TPB - 1) / TPB, S = gridDim.x;
+	uint64_t it = blockIdx.x;
+	if (it >= NI)
+		return;
+	// the register ring of toeplitz12x4_ab_kernel, TPB groups per block step
+	auto gof = [&](uint64_t i) { return (i < NI ? i : it) * TPB + threadIdx.x; };
+	u32x4_t R[DEPTH][3];
+#pragma unroll
+	for (int d = 0; d < DEPTH - 1; ++d)
+		t12_load(src, gof(it + d * S), ng, R[d]);
+	for (;;) {
+#pragma unroll
+		for (int d = 0; d < DEPTH; ++d) {
+			t12_load(src, gof(it + (uint64_t)(d + DEPTH - 1) * S), ng, R[(d + DEPTH - 1) % DEPTH]);
+			const uint64_t g = (it + d * S) * TPB + threadIdx.x;
+			u32x4_t h;
+			h.x = hash12_t12(smem, R[d][0].x, R[d][0].y, R[d][0].z) & p.mask;
+			h.y = hash12_t12(smem, R[d][0].w, R[d][1].x, R[d][1].y) & p.mask;
+			h.z = hash12_t12(smem, R[d][1].z, R[d][1].w, R[d][2].x) & p.mask;
+			h.w = hash12_t12(smem, R[d][2].y, R[d][2].z, R[d][2].w) & p.mask;
+			if (g < ng)
+				t12_store(p.out, g, h);
+			if (it + (uint64_t)(d + 1) * S >= NI)
+				return;
+		}
+		it += (uint64_t)DEPTH * S;
+	}
+}
+
 hipError_t launch_toeplitz(const RssParams &p0, int num_cus, hipStream_t st)
 {
 	if (p0.n == 0)
@@ -242,7 +303,24 @@ hipError_t launch_toeplitz(const RssParams &p0, int num_cus, hipStream_t st)
 		hipLaunchKernelGGL(toeplitz12x4_ab_kernel<D>, gb, dim3(256), 12 * 256 * 4, st, p, ng); \
 	} while (0)
 #if CGCK_LAB
-		if (var == 2 && depth == 16)
+		// var 3: 12-bit tables, $CGCK_RSS_TPB threads (256 | 512 | 1024), one workgroup per CU
+		static const int tpb = [] {
+			const char *e = CGCK_ENV("CGCK_RSS_TPB");
+			const int t = e ? atoi(e) : 512;
+			return t == 256 || t == 1024 ? t : 512;
+		}();
+#define CGCK_RSS_T12(D, T)                                                                              \
+	if (depth == D && tpb == T) {                                                                   \
+		const uint64_t wt = (ng + T - 1) / T;                                                   \
+		const dim3 gt((unsigned)(wt < (uint64_t)num_cus ? wt : (uint64_t)num_cus));             \
+		CGCK_NOTE_KERNEL("toeplitz12x4_t12_kernel<%d, %d>", D, T);                               \
+		hipLaunchKernelGGL((toeplitz12x4_t12_kernel<D, T>), gt, dim3(T), 0, st, p, ng);          \
+	} else
+		if (var == 3) {
+			CGCK_RSS_T12(2, 1024) CGCK_RSS_T12(3, 1024) CGCK_RSS_T12(4, 512) CGCK_RSS_T12(6, 512)
+			CGCK_RSS_T12(8, 512) CGCK_RSS_T12(4, 256) CGCK_RSS_T12(8, 256) CGCK_RSS_T12(12, 256)
+			CGCK_RSS_T12(4, 1024) CGCK_RSS_AB(12);
+		} else if (var == 2 && depth == 16)
 			CGCK_RSS_AB(16);
 		else if (var == 2 && depth == 12)
 			CGCK_RSS_AB(12);
@@ -273,6 +351,9 @@ hipError_t launch_toeplitz(const RssParams &p0, int num_cus, hipStream_t st)
 		CGCK_RSS_AB(12); // the measured default; the other depths and forms are lab builds
 #endif
 #undef CGCK_RSS_AB
+#if CGCK_LAB
+#undef CGCK_RSS_T12
+#endif
 		hipError_t e = hipGetLastError();
 		if (e != hipSuccess || ng * 4 == p.n)
 			return e;

@@ -110,11 +110,24 @@ def main():
                 assert L.cgck_event_elapsed_ms(a, b, ctypes.byref(ms)) == 0
                 if r > 0:
                     res[(w, i)].append(algo / (ms.value / args.launches * 1e-3))
+    # parity of the two builds on every workload (the same outputs, byte for byte)
+    import numpy as np
+    same = {}
+    for w, (fn, _) in work.items():
+        got = []
+        for L, c in zip(libs, ctxs):
+            assert fn(L, c) == 0, L.cgck_last_error()
+            assert L.cgck_ctx_sync(c) == 0
+            h = np.zeros(16 * n, np.uint8)
+            out.download(h)
+            got.append(h)
+        same[w] = bool(np.array_equal(got[0], got[1]))
     table = {}
     for w in work:
         m = [statistics.median(res[(w, i)]) for i in range(2)]
-        table[w] = {"A": m[0] / HBM, "B": m[1] / HBM, "B_over_A": m[1] / m[0]}
-        print(f"{w:>5}: A {m[0] / HBM:6.1%}  B {m[1] / HBM:6.1%}  B/A {m[1] / m[0]:.3f}", flush=True)
+        table[w] = {"A": m[0] / HBM, "B": m[1] / HBM, "B_over_A": m[1] / m[0], "same_outputs": same[w]}
+        print(f"{w:>5}: A {m[0] / HBM:6.1%}  B {m[1] / HBM:6.1%}  B/A {m[1] / m[0]:.3f}  same outputs {same[w]}",
+              flush=True)
     print(json.dumps({"libs": paths, "results": table}))
 
 
