@@ -556,3 +556,48 @@ def test_rx_tx_pipelined_loop(port):
         for _, _, _, ring, _ in rx:
             L.cgck_host_unregister(ring.ctypes.data)
         L.cgck_host_unregister(tx_ring.ctypes.data)
+
+
+def test_pipelined_across_server_idle(port):
+    """A posted burst or fill whose completion comes after the server idled
+    out (idle_ms 20, then 100 ms of other work), and a post made while no
+    server workgroup is alive: the post relaunches it, every value is exact."""
+    import time
+    R = referee(port)
+    L = cgck.load()
+    raw, tx_ring, size = rxcorpus.registered_copy(np.zeros(64 * 2048, np.uint8))
+    slots = tx_ring[:64 * 2048].reshape(64, 2048)
+    assert L.cgck_host_register(tx_ring.ctypes.data, size) == 0
+    cgck.burst_open(max_pkts=1024, max_bytes=4 << 20, idle_ms=20)
+    try:
+        rng = np.random.default_rng(4400)
+        for rep in range(3):
+            buf, desc = rxcorpus.ring(rxcorpus.corpus(rng, R, 90, clean=rep != 1))
+            got = buf.copy()
+            assert cgck.rx_post(got, desc) == len(desc)
+            want = []
+            cgck.tx_begin()
+            for i in range(32):
+                ln = int(rng.integers(40, 1501))
+                pkt = tcp_pkt(rng, ln)
+                slots[i, 14:14 + ln] = pkt
+                want.append((i, ln, expected(port, pkt, 16)))
+                tx_calls(slots[i], ln, 16)
+            assert cgck.tx_post() == 64
+            time.sleep(0.1)                      # > idle_ms: the server exits once both are served
+            stack, ip_in, tcp_in = FLAGS[(7 * rep) % len(FLAGS)]
+            ref = buf.copy()
+            a = port.replay_rx(*R.fn_pointers(), ref, desc.view(np.uint8), len(desc), stack, ip_in, tcp_in)
+            cgck.rx_begin_posted()
+            try:
+                b = port.replay_rx(*cgck.fn_pointers(), got, desc.view(np.uint8), len(desc), stack, ip_in, tcp_in)
+            finally:
+                cgck.rx_end()
+            assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and np.array_equal(ref, got), rep
+            assert cgck.tx_complete() == 64
+            for i, ln, r in want:
+                assert np.array_equal(slots[i, 14:14 + ln], r), (rep, i)
+            time.sleep(0.1)                      # the next posts find no workgroup alive
+    finally:
+        cgck.burst_close()
+        L.cgck_host_unregister(tx_ring.ctypes.data)
