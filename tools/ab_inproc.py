@@ -23,7 +23,9 @@ sys.path.insert(0, os.path.join(ROOT, "con-gen_amd"))
 import cgck  # noqa: E402
 
 HBM = 8.0e12
-KEY = bytes(range(7, 7 + 40))
+# the bench's key (bench.py RSS_KEY, the Microsoft RSS test key); $AB_KEY=seq: bytes 7..46
+KEY = (bytes(range(7, 7 + 40)) if os.environ.get("AB_KEY") == "seq" else
+       bytes.fromhex("6d5a56da255b0ec24167253d43a38fb0d0ca2bcbae7b30b477cb2da38030f20c6a42b73bbeac01fa"))
 
 
 def main():
