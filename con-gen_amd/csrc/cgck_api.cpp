@@ -508,11 +508,6 @@ static int burst_wait(cgck_ctx *c, uint32_t seq, uint32_t n, uint64_t range)
 #if CGCK_LAB
 	t_lab_host[1] = (uint64_t)(now_s() * 1e9);
 #endif
-	// The response lines were written by the GPU, so none is in this core's
-	// caches: start their first misses now, beside the refused word's.
-	const uint8_t *o = burst_resp(c, seq);
-	for (uint32_t at = 0; at < 4 * n && at < 512; at += 64)
-		__builtin_prefetch(o + at);
 	c->bdone = seq;
 	if (__atomic_load_n(&b->refused[seq & 1], __ATOMIC_ACQUIRE) == seq)
 		return set_err(-EIO,
@@ -532,6 +527,20 @@ int cgck::burst_collect(cgck_ctx *c, BurstPending *p)
 	p->seq = 0;
 	if (c->bslot[seq & 1] == p)
 		c->bslot[seq & 1] = nullptr;
+	// The GPU wrote the done words and the response, so none of their lines
+	// is in this core's caches: a posted request is usually served by now,
+	// so start those misses together instead of one after the other.
+	{
+		const uint8_t *o = burst_resp(c, seq);
+		__builtin_prefetch(&c->bbox->done[0]);
+		const uint32_t lim = 4 * p->n < 512 ? 4 * p->n : 512;
+		for (uint32_t at = 0; at < lim; at += 64) {
+			if (p->out)
+				__builtin_prefetch(o + at);
+			if (p->meta)
+				__builtin_prefetch(o + burst_meta_off(p->n) + at);
+		}
+	}
 	int rc = burst_wait(c, seq, p->n, p->range);
 	if (rc == 0) {
 		const uint8_t *o = burst_resp(c, seq);
