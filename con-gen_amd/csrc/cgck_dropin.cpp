@@ -899,6 +899,28 @@ extern "C" int cgck_tx_flush(void)
 	ThreadState &t = tstate();
 	if (!t.tx_open)
 		return set_err(-EINVAL, "cgck_tx_flush: no open window on this thread");
+	txd_close(t);
+	if (t.txd_ok && t.txd_noip == 0 && !t.txd_fast.empty()) {
+		// the fast form: its descriptors as they are, the fields written from
+		// the values (as cgck_tx_post + cgck_tx_complete, waited for at once)
+		TxFill &f = t.txs;
+		tx_take(t, f);
+		cgck_ctx *c = thread_ctx();
+		if (!c)
+			return -ENODEV;
+		f.d.swap(t.txd_fast);
+		f.hs.swap(t.txd_hs);
+		f.lo = const_cast<uint8_t *>(t.txd_lo);
+		f.n = (int)t.txd_calls;
+		f.o.resize(f.d.size());
+		const DescSummary sum = {t.txd_max, t.txd_bytes};
+		int rc = desc_host_post(c, (void *)t.txd_lo, (size_t)(t.txd_hi - t.txd_lo), f.d.data(), f.d.size(),
+					kTxFlags, f.o.data(), nullptr, nullptr, &f.pend, &sum);
+		if (rc >= 0)
+			rc = f.pend.seq ? burst_collect(c, &f.pend) : f.pend.rc;
+		f.q.clear();
+		return rc < 0 ? rc : tx_write_fast(f);
+	}
 	if (t.txd_ok)
 		txd_spill(t);
 	tx_take(t, t.txs);
