@@ -275,6 +275,44 @@ __global__ __launch_bounds__(128) void dstr_kernel(KParams p)
 				const int c = c0 + 16 * s + gl;
 				w[s] = *reinterpret_cast<const uint4 *>(sl + 16 * (c < kDsChunks ? c : kDsChunks - 1));
 			}
+#if CGCK_DSTR_REGHDR
+			// (lab A/B) only the six chunk reads before the refill: the last
+			// chunk is the register of the lane holding it, the header dwords
+			// come from w[0] of this lane and the next (DPP row_shl:1)
+			asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+			issue(j + D);
+			uint4 wt = make_uint4(0, 0, 0, 0);
+			bool ht = false;
+#pragma unroll
+			for (int s = 0; s < kDsS; ++s) {
+				const bool t = 16 * s + gl == nch - 1;
+				const uint32_t mt = opaque(t ? ~0u : 0u);
+				wt = make_uint4(pick(mt, w[s].x, wt.x), pick(mt, w[s].y, wt.y), pick(mt, w[s].z, wt.z),
+						pick(mt, w[s].w, wt.w));
+				ht = ht || t;
+			}
+			const uint32_t n0 = __builtin_amdgcn_mov_dpp(w[0].x, 0x101, 0xF, 0xF, false);
+			const uint32_t n1 = __builtin_amdgcn_mov_dpp(w[0].y, 0x101, 0xF, 0xF, false);
+			const uint32_t n2 = __builtin_amdgcn_mov_dpp(w[0].z, 0x101, 0xF, 0xF, false);
+			const uint32_t n3 = __builtin_amdgcn_mov_dpp(w[0].w, 0x101, 0xF, 0xF, false);
+			const uint32_t dd[8] = {w[0].x, w[0].y, w[0].z, w[0].w, n0, n1, n2, n3};
+			const int q4 = q >> 2;
+			const uint32_t m0 = opaque(q4 == 0 ? ~0u : 0u), m1 = opaque(q4 == 1 ? ~0u : 0u),
+				       m2 = opaque(q4 == 2 ? ~0u : 0u);
+			uint32_t hh[5];
+#pragma unroll
+			for (int i = 0; i < 5; ++i)
+				hh[i] = pick(m0, dd[i], pick(m1, dd[i + 1], pick(m2, dd[i + 2], dd[i + 3])));
+			const uint32_t h2 = hh[2], h3 = hh[3], h4 = hh[4];
+			const uint32_t hd = hh[0] & 15;
+			uint32_t ip = hsum(h4, hsum(h3, hsum(h2, hsum(hh[1], hsum(hh[0], 0)))));
+			if (gl == 0 && hd != 5 && f0 + g < n) { // options or a short header (rare): global memory
+				const uint64_t fa = base + (f0 + g) * stride;
+				ip = 0;
+				for (uint32_t i = 0; i < hd; ++i)
+					ip = hsum(*gbl_at<const uint32_t>(fa + 4 * i), ip);
+			}
+#else
 			const uint4 wt = *reinterpret_cast<const uint4 *>(sl + 16 * (c0 + nch - 1)); // the last chunk
 			const uint32_t *hw = reinterpret_cast<const uint32_t *>(sl + o);
 			const uint32_t h0 = hw[0], h1 = hw[1], h2 = hw[2], h3 = hw[3], h4 = hw[4];
@@ -289,6 +327,7 @@ __global__ __launch_bounds__(128) void dstr_kernel(KParams p)
 			// in flight while this one is reduced.
 			asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 			issue(j + D);
+#endif
 
 			// independent per-chunk chains (no dependent v_dot2 wait states),
 			// then the chunks inside the frame
@@ -314,7 +353,11 @@ __global__ __launch_bounds__(128) void dstr_kernel(KParams p)
 			} else {
 				tail = msum(wt, 0, e, 16, 0);
 			}
+#if CGCK_DSTR_REGHDR
+			const uint32_t corr = (gl == 0 ? lead : 0u) + (ht ? tail : 0u);
+#else
 			const uint32_t corr = gl == 0 ? lead + tail : 0u;
+#endif
 			uint32_t tot = fold16(body) + (0xffffu - fold16(corr));
 			tot = fold16(gsum<16>(tot));
 
