@@ -49,6 +49,12 @@ namespace cgck {
 constexpr int kDsS = 6;                     // DMA instructions (KiB) per step
 constexpr uint32_t kDsSlot = kDsS * 1024;   // bytes per ring slot
 constexpr int kDsChunks = kDsS * 64;        // 16-byte chunks per slot
+// Every chunk a lane of the reducing wave reads lies in its slot, so the
+// reads need no clamp: frame g of a step starts at most 15 + 3 * 1520 bytes
+// into the slot (dstr_ok: stride <= 1520), and a lane reads up to 95 chunks
+// past the frame's first (16 s + gl).  (Unclamped: 1.004 of the clamped
+// reads in one process, twice, bit-exact; profiles/r04/dstr_ab/.)
+static_assert(((15 + 3 * 1520) >> 4) + 16 * (kDsS - 1) + 15 < kDsChunks, "a reducing lane's chunk lies in its slot");
 
 template <int D, int C, bool W, int F>
 __global__ __launch_bounds__(128) void dstr_kernel(KParams p)
@@ -273,7 +279,7 @@ __global__ __launch_bounds__(128) void dstr_kernel(KParams p)
 #pragma unroll
 			for (int s = 0; s < kDsS; ++s) {
 				const int c = c0 + 16 * s + gl;
-				w[s] = *reinterpret_cast<const uint4 *>(sl + 16 * (c < kDsChunks ? c : kDsChunks - 1));
+				w[s] = *reinterpret_cast<const uint4 *>(sl + 16 * c);
 			}
 #if CGCK_DSTR_REGHDR
 			// (lab A/B) only the six chunk reads before the refill: the last
