@@ -24,6 +24,8 @@ for step in "$@"; do
 	testsk) run pytest_gpu 900 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread || true ;;
 	quick) run pytest_quick 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "burst or window or pipelined or rx_post or tx_" || exit 1 ;;
 	txburst) run txburst 400 tools/txburst 0.2 || exit 1 ;;
+	txlens) # con-gen's typical frames (54-130 B): 128 B beside 64 B
+		TXBURST_LENS=128,64 run txburst_128 400 tools/txburst 0.2 || exit 1 ;;
 	txstack) # the same rows with 150 us of other stack work between bursts
 		TXBURST_STACK_US=150 run txburst_stack150 400 tools/txburst 0.2 || exit 1 ;;
 	txkstore) # lab: the kernel stores the posted fills' fields (CGCK_STORE) instead of the host

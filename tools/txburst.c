@@ -110,8 +110,24 @@ int main(int argc, char **argv)
 	const int nb = (int)(sizeof(bursts) / sizeof(bursts[0]));
 	/* 1500 B MTU frames, 576 B (con-gen's MTU 522 + headers, con-gen.c:741,
 	 * rounded up to the IMIX class) and 64 B minimum frames */
-	const int lens[] = {1500, 576, 64};
-	const int nl = (int)(sizeof(lens) / sizeof(lens[0]));
+	int lens[8] = {1500, 576, 64};
+	int nl = 3;
+	/* TXBURST_LENS=128,64: other frame lengths (con-gen's own frames are
+	 * mostly 54-130 B), 40..1500 each */
+	if (getenv("TXBURST_LENS")) {
+		nl = 0;
+		for (char *e = getenv("TXBURST_LENS"); *e && nl < 8;) {
+			const int v = (int)strtol(e, &e, 10);
+			if (v >= 40 && v <= 1500)
+				lens[nl++] = v;
+			while (*e == ',')
+				e++;
+			if (*e && (*e < '0' || *e > '9'))
+				break;
+		}
+		if (!nl)
+			return 2;
+	}
 	const int maxb = 2048, maxit = 100000;
 	/* TXBURST_HUGE=1: the ring on transparent huge pages (2 MiB), as a DPDK
 	 * mempool or a huge-page XDP UMEM would be; otherwise 4 KiB pages */
@@ -210,21 +226,26 @@ int main(int argc, char **argv)
 			desc[i].l3_off = L3;
 			desc[i].ip_len = (uint16_t)len;
 		}
-		/* the second half (the pipelined modes' other burst): the same frames */
-		memcpy(ring + (size_t)maxb * SLOT, ring, (size_t)maxb * SLOT);
 		/* fill both fields in place (the TX result a receiver would see) */
 		if (cgck_desc_host(ctx, ring, (size_t)maxb * SLOT, desc, maxb,
 				   CGCK_IP | CGCK_L4 | CGCK_ZERO_FIELDS | CGCK_STORE, out, NULL)) {
 			fprintf(stderr, "txburst: fill failed: %s\n", cgck_last_error());
 			return 1;
 		}
+		/* the second half (the pipelined modes' other burst): the same frames */
+		memcpy(ring + (size_t)maxb * SLOT, ring, (size_t)maxb * SLOT);
 		/* corrupt one payload byte of every 64th packet (both halves) */
 		for (int i = 0; i < 2 * maxb; i += 64)
 			ring[(size_t)i * SLOT + L3 + len - 1] ^= 0x5A;
-		uint8_t *keep = ref_in && ref_udp ? malloc((size_t)2 * maxb * SLOT) : NULL;
-		if (keep) /* the reference rows rewrite fields: the ring is put back afterwards */
-			memcpy(keep, ring, (size_t)2 * maxb * SLOT);
-		for (int bi = 0; bi < nb && keep; bi++) { /* the reference loop, same harness */
+		/* the ring as received: the reference rows and the TX rows rewrite
+		 * fields, so it is put back before each RX pass */
+		uint8_t *keep = malloc((size_t)2 * maxb * SLOT);
+		if (!keep) {
+			fprintf(stderr, "txburst: out of memory\n");
+			return 1;
+		}
+		memcpy(keep, ring, (size_t)2 * maxb * SLOT);
+		for (int bi = 0; bi < nb && ref_in && ref_udp; bi++) { /* the reference loop, same harness */
 			const int R = bursts[bi];
 			for (int mode = 0; mode < 2; mode++) {
 				int it = 0, w = 0;
@@ -267,7 +288,6 @@ int main(int argc, char **argv)
 		}
 		if (keep) {
 			memcpy(ring, keep, (size_t)2 * maxb * SLOT);
-			free(keep);
 		}
 		/* passes: 0 launch path, 1 registered ring, 2 burst server, 3 server + registered */
 		for (int pass = 0; pass < 4; pass++) {
@@ -397,6 +417,7 @@ int main(int argc, char **argv)
 			}
 			for (int bi = 0; bi < nb && pass == 3; bi++) { /* RX, one burst in flight */
 				const int R = bursts[bi];
+				memcpy(ring, keep, (size_t)2 * maxb * SLOT); /* both halves as received */
 				int it = 0, k = 0, bad_l4 = 0, bad_ip = 0;
 				double t0 = now();
 				while (it < maxit && now() - t0 < budget + 0.05) {
@@ -526,6 +547,7 @@ int main(int argc, char **argv)
 			if (reg)
 				cgck_host_unregister(ring);
 		}
+		free(keep);
 		/* drop-in latency: one synchronous in_cksum(ip, 20), launch path vs server */
 		for (int srv = 0; srv < 2; srv++) {
 			int it = 0;
