@@ -474,8 +474,10 @@ int main(int argc, char **argv)
 					     us_post = median(tc, it) * 1e6;
 				printf("{\"mode\": \"rx_window_pipelined_registered_server\", \"pkt_len\": %d, \"burst\": %d, "
 				       "\"iters\": %d, \"us_median\": %.2f, \"us_wait\": %.2f, \"us_post\": %.2f, "
-				       "\"stack_us\": %.1f, \"bad_ip\": %d, \"bad_l4\": %d, \"bad_l4_expected\": %d}\n",
-				       len, R, it, us, us_wait, us_post, stack_us, bad_ip, bad_l4, (R + 63) / 64);
+				       "\"stack_us\": %.1f, \"bad_ip\": %d, \"bad_l4\": %d, \"bad_l4_expected\": %d, "
+				       "\"exact\": %s}\n",
+				       len, R, it, us, us_wait, us_post, stack_us, bad_ip, bad_l4, (R + 63) / 64,
+				       bad_ip == 0 && bad_l4 == (R + 63) / 64 ? "true" : "false");
 				fflush(stdout);
 			}
 			for (int bi = 0; bi < nb && pass == 3; bi++) { /* TX, one fill in flight */
