@@ -69,6 +69,7 @@ EXPORTS = (
     "cgck_rx_begin", "cgck_rx_end", "cgck_window_stats", "cgck_ctx_last_kernel", "cgck_set_desc_layout",
     "cgck_ctx_set_kernel", "cgck_synth_imix_ring", "cgck_burst_request", "cgck_host_device_ptr",
     "cgck_rx_post", "cgck_rx_begin_posted", "cgck_tx_post", "cgck_tx_complete",
+    "cgck_rx_pending", "cgck_rx_ready",
 )
 # Descriptor layout hint (cgck_set_desc_layout)
 LAYOUT_ANY = 0
@@ -282,6 +283,17 @@ def rx_post(base, desc):
 def rx_begin_posted():
     """cgck_rx_begin_posted: open the window over the oldest posted burst."""
     return _check(load().cgck_rx_begin_posted(), "cgck_rx_begin_posted")
+
+
+def rx_pending():
+    """cgck_rx_pending: bursts posted and not yet opened (the drain rule)."""
+    return _check(load().cgck_rx_pending(), "cgck_rx_pending")
+
+
+def rx_ready():
+    """cgck_rx_ready: 1 when the oldest posted burst's values are in, 0 while
+    the GPU still computes it (no wait)."""
+    return _check(load().cgck_rx_ready(), "cgck_rx_ready")
 
 
 def window_stats():

@@ -339,8 +339,47 @@ std::mutex g_srv_mu;
 std::vector<cgck_ctx *> g_srv;
 } // namespace
 
+static bool burst_all_alive(const cgck_ctx *c);
+static int burst_restart(cgck_ctx *c);
+
+// Serve every request posted to c and not collected yet (the seqs after
+// bdone up to bseq: a pipelined window's burst or fill), relaunching the
+// server if it idled out, without collecting them: their outputs stay in
+// their slots for the poster's own collect, which then finds them done.
+// The caller holds g_map_mu exclusively, so neither seq moves meanwhile.
+// A request not served in 2 s is abandoned (the next launch starts after
+// it; its poster's collect times out): it must not be served after the
+// mapping it reads has changed.
+static void burst_finish_posted(cgck_ctx *c)
+{
+	BurstBox *b = c->bbox;
+	for (uint32_t s = c->bdone, k = 0; s != c->bseq && k < 4; k++) {
+		s = burst_next(s);
+		const uint32_t n = (uint32_t)(__atomic_load_n(&b->req[s & 1], __ATOMIC_ACQUIRE) >> 32);
+		const uint32_t W = burst_wgs(n, c->bwgs, c->bper);
+		const double t0 = now_s();
+		for (uint32_t j = 0, spin = 0; j < W;) {
+			if ((int32_t)(__atomic_load_n(&b->done[j], __ATOMIC_ACQUIRE) - s) >= 0) {
+				j++;
+				continue;
+			}
+			__builtin_ia32_pause();
+			if ((++spin & 1023) != 0)
+				continue;
+			if (!burst_all_alive(c) && burst_restart(c) != 0)
+				break;
+			if (now_s() - t0 > 2.0) {
+				c->bdone = c->bseq;
+				return;
+			}
+		}
+	}
+}
+
 // Stop every open server and wait until its workgroups have left (caller
-// holds g_map_mu exclusively, so no request is in flight).
+// holds g_map_mu exclusively, so no request is posted meanwhile).  Requests
+// already posted are served first (burst_finish_posted): a relaunch after
+// the mapping change must not read or store through a range that is gone.
 static void burst_quiesce_all()
 {
 	std::lock_guard<std::mutex> lk(g_srv_mu);
@@ -348,6 +387,7 @@ static void burst_quiesce_all()
 		if (!c->bbox)
 			continue;
 		(void)hipSetDevice(c->device);
+		burst_finish_posted(c);
 		__atomic_store_n(&c->bbox->stop, 1u, __ATOMIC_RELEASE);
 		(void)hipStreamSynchronize(c->bstream);
 		__atomic_store_n(&c->bbox->stop, 0u, __ATOMIC_RELEASE);
@@ -456,6 +496,18 @@ static const uint8_t *burst_resp(const cgck_ctx *c, uint32_t seq)
 	return c->bresp + (size_t)(seq & 1) * burst_resp_slot(c->bmax);
 }
 
+// Requests complete in order, so the last one known complete is the latest
+// seq collected, whatever order the posted requests are collected in (the
+// pipelined windows collect a TX fill, then the older RX burst that shares
+// nothing with it).  bdone only moves forward: a relaunch starts after it, and
+// one that started after an older seq would have its leader poll a slot the
+// host has since posted a later request into.
+static void burst_done_at(cgck_ctx *c, uint32_t seq)
+{
+	if ((int32_t)(seq - c->bdone) > 0)
+		c->bdone = seq;
+}
+
 // Wait until request seq (n packets) is served.  Requests complete in order,
 // so a workgroup's done word at or past seq means its slice is in.
 static int burst_wait(cgck_ctx *c, uint32_t seq, uint32_t n, uint64_t range)
@@ -497,7 +549,7 @@ static int burst_wait(cgck_ctx *c, uint32_t seq, uint32_t n, uint64_t range)
 			__atomic_store_n(&b->stop, 0u, __ATOMIC_RELEASE);
 			uint64_t relay[3] = {0, 0, 0};
 			(void)hipMemcpy(relay, c->brelay, sizeof(relay), hipMemcpyDeviceToHost);
-			c->bdone = seq; // abandoned: the next launch starts after it
+			burst_done_at(c, seq); // abandoned: the next launch starts after it
 			return set_err(-ETIMEDOUT,
 				       "burst server: request %u (n %u, W %u) not served in 2 s; missing (wg:done)%s; "
 				       "relay %#llx %#llx %#llx",
@@ -508,7 +560,7 @@ static int burst_wait(cgck_ctx *c, uint32_t seq, uint32_t n, uint64_t range)
 #if CGCK_LAB
 	t_lab_host[1] = (uint64_t)(now_s() * 1e9);
 #endif
-	c->bdone = seq;
+	burst_done_at(c, seq);
 	if (__atomic_load_n(&b->refused[seq & 1], __ATOMIC_ACQUIRE) == seq)
 		return set_err(-EIO,
 			       "burst server: request %u refused (block header, or a descriptor outside the block or "
@@ -553,6 +605,17 @@ int cgck::burst_collect(cgck_ctx *c, BurstPending *p)
 	}
 	p->rc = rc;
 	return rc;
+}
+
+int cgck::burst_ready(const cgck_ctx *c, const BurstPending *p)
+{
+	if (!p->seq)
+		return 1;
+	const uint32_t W = burst_wgs(p->n, c->bwgs, c->bper);
+	for (uint32_t j = 0; j < W; j++)
+		if ((int32_t)(__atomic_load_n(&c->bbox->done[j], __ATOMIC_ACQUIRE) - p->seq) < 0)
+			return 0;
+	return 1;
 }
 
 // The block of the next request, with its slot free: a posted request still

@@ -24,6 +24,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <atomic>
 #include <vector>
 
@@ -125,6 +126,7 @@ struct TxFill {
 	BurstPending pend{};
 	bool stored = false; // the kernel wrote the fields in place (CGCK_STORE): nothing left to write
 	bool fast = false;   // posted in the fast form: o[k] is descriptor k's values, hs its spans
+	bool icmp = false;   // holds ICMP messages (their L4 value without the pseudo-header)
 	int n = 0;           // the fields it stands for (q is empty in the fast form)
 	std::vector<uint32_t> hs;
 	uint8_t *lo = nullptr;
@@ -134,6 +136,7 @@ struct ThreadState {
 	cgck_ctx *ctx = nullptr;
 	// TX window
 	bool tx_open = false;
+	bool tx_icmp = false; // an ICMP message was queued (icmp_send, ip_icmp.c:68-80)
 	std::vector<TxEntry> txq;
 	const uint8_t *tx_max = nullptr; // highest header address queued so far
 	bool tx_map = false;             // txidx built (the first call below tx_max)
@@ -171,6 +174,10 @@ struct ThreadState {
 	PtrMap rxidx; // ip -> frame << 1; ip + hl (ICMP message) -> frame << 1 | 1
 	const cgck_desc_t *rxd = nullptr;
 	const uint32_t *rxo = nullptr, *rxm = nullptr;
+	// the burst's frames as sorted [start, end) byte ranges, built on the
+	// first TX-window call of the window (rx_owns)
+	bool rx_iv_built = false;
+	std::vector<std::pair<uintptr_t, uintptr_t>> rx_iv;
 	RxBurst rxs;      // cgck_rx_begin's burst
 	RxBurst rxp[2];   // posted bursts (cgck_rx_post), oldest at rxp_head
 	unsigned rxp_head = 0, rxp_count = 0;
@@ -282,6 +289,41 @@ inline bool rx_find(ThreadState &t, const uint8_t *p, uint32_t *v)
 	return rx_find_slow(t, p, v);
 }
 
+// The L4 checksum field after the IPv4 header, by protocol, as the
+// finalisers store it: TCP +16 (tcp_output.c:417), UDP +6 (udp_usrreq.c:
+// 189), ICMP +2 (icmp_send, ip_icmp.c:76-77).
+inline int l4_fo(const uint8_t *ip) { return ip[9] == 6 ? 16 : ip[9] == 17 ? 6 : 2; }
+
+// Does p lie inside one of the open RX window's frames?  Both windows are
+// open across con-gen's whole loop iteration, so a
+// call the RX window does not answer may still be the stack verifying a
+// received frame (a UDP datagram whose uh_ulen is below ip_len, an ICMP
+// message too short to check); it needs its value now, so it must not be
+// queued by the TX window even though the frame lies in the registered
+// pool.  The frames' ranges are sorted once per window, on the first call
+// that asks (a burst that draws no reply never pays for it).
+__attribute__((noinline)) bool rx_owns(ThreadState &t, const uint8_t *p)
+{
+	if (!t.rx_iv_built) {
+		t.rx_iv.resize(t.rx_n);
+		bool sorted = true;
+		for (size_t i = 0; i < t.rx_n; i++) {
+			const uintptr_t a = (uintptr_t)(t.rx_base + t.rxd[i].frame_off);
+			t.rx_iv[i] = {a, a + t.rxd[i].l3_off + t.rxd[i].ip_len};
+			sorted = sorted && (i == 0 || t.rx_iv[i - 1].first <= a);
+		}
+		if (!sorted)
+			std::sort(t.rx_iv.begin(), t.rx_iv.end());
+		// a running maximum of the ends, so one probe answers for overlaps
+		for (size_t i = 1; i < t.rx_n; i++)
+			t.rx_iv[i].second = std::max(t.rx_iv[i].second, t.rx_iv[i - 1].second);
+		t.rx_iv_built = true;
+	}
+	const uintptr_t a = (uintptr_t)p;
+	auto it = std::upper_bound(t.rx_iv.begin(), t.rx_iv.end(), std::make_pair(a, UINTPTR_MAX));
+	return it != t.rx_iv.begin() && (it - 1)->second > a;
+}
+
 // Is [p, p + bytes) registered (the TX window queues only ring memory)?  The
 // range of the last hit first, then reg_find.  The generation is read before
 // the lookup, so a change racing it leaves the cache stale-marked.
@@ -325,7 +367,7 @@ __attribute__((noinline)) void txd_spill(ThreadState &t)
 		uint8_t *ip = const_cast<uint8_t *>(t.txd_lo) + t.txd_fast[k].frame_off;
 		const uint32_t h = hs >> 16, sp = hs & 0xffff;
 		if (sp)
-			t.txq.push_back({ip, sp, (uint16_t)((ip[0] & 15) * 4), (int16_t)(ip[9] == 6 ? 16 : 6)});
+			t.txq.push_back({ip, sp, (uint16_t)((ip[0] & 15) * 4), (int16_t)l4_fo(ip)});
 		if (h)
 			t.txq.push_back({ip, h, (uint16_t)h, -1});
 	}
@@ -504,6 +546,7 @@ extern "C" uint16_t in_cksum(void *data, int len)
 	ThreadState &t = tstate();
 	const uint8_t *b = (const uint8_t *)data;
 	bool rx_miss = false; // counted in stats[1] only when the call is computed here
+	bool rx_frame = false; // the call is about a received frame: never queued
 	if (t.rx_open) {
 		// ip_cksum(ip) at ip_input.c:51 / inet.c:322, or the ICMP message at
 		// ip_icmp.c:189, after the caller zeroed the field
@@ -518,16 +561,37 @@ extern "C" uint16_t in_cksum(void *data, int len)
 				t.stats[0]++;
 				return (uint16_t)(t.rxo[v >> 1] >> 16);
 			}
+			rx_frame = true;
 		}
 		rx_miss = true;
 	}
-	if (t.tx_open && len >= 20 && (b[0] >> 4) == 4 && len == (b[0] & 15) * 4) {
-		if (tx_registered(t, b, (size_t)len)) {
-			tx_queue(t, (uint8_t *)data, (uint32_t)len, (uint16_t)len, -1);
-			t.stats[2]++;
-			return 0;
+	if (t.tx_open && !rx_frame && !(rx_miss && rx_owns(t, b))) {
+		if (len >= 20 && (b[0] >> 4) == 4 && len == (b[0] & 15) * 4) {
+			// ip_cksum(ip) in ip_output (ip_output.c:62)
+			if (tx_registered(t, b, (size_t)len)) {
+				tx_queue(t, (uint8_t *)data, (uint32_t)len, (uint16_t)len, -1);
+				t.stats[2]++;
+				return 0;
+			}
+			t.stats[3]++;
+		} else if (len >= 8 && len <= 0xffff - 20) {
+			// icmp_send's in_cksum(icp, ip_len - 20) (ip_icmp.c:77): the
+			// message right after a 20-byte IPv4 header of protocol 1, its
+			// field at +2 just zeroed; queued as the packet's L4 entry.  The
+			// header bytes are read only when they are registered or on
+			// the message's own page.
+			const uint8_t *ip = b - 20;
+			if (tx_registered(t, ip, 20 + (size_t)len)) {
+				if (ip[0] == 0x45 && ip[9] == 1) {
+					tx_queue(t, const_cast<uint8_t *>(ip), 20 + (uint32_t)len, 20, 2);
+					t.tx_icmp = true;
+					t.stats[2]++;
+					return 0;
+				}
+			} else if (((uintptr_t)b & 4095) >= 20 && ip[0] == 0x45 && ip[9] == 1) {
+				t.stats[3]++;
+			}
 		}
-		t.stats[3]++;
 	}
 	t.stats[1] += rx_miss;
 	return (uint16_t)sync_region(data, (uint32_t)len, (uint32_t)len, CGCK_RAW);
@@ -544,20 +608,24 @@ extern "C" uint16_t udp_cksum(struct ip *ipp, int len)
 	const uint32_t hl = (ip[0] & 15) * 4;
 	const uint32_t ip_len = hl + (uint32_t)len;
 	bool rx_miss = false; // counted in stats[1] only when the call is computed here
+	bool rx_frame = false; // the call is about a received frame: never queued
 	if (t.rx_open) {
 		// tcp_cksum(ip, ip->ip_len) at tcp_input.c:78 / inet.c:145, or
 		// udp_cksum(ip, len) at udp_usrreq.c:89
 		uint32_t v;
-		if (rx_find(t, ip, &v) && !(v & 1)) {
+		if (rx_find(t, ip, &v)) {
 			const uint32_t m = t.rxm[v >> 1];
-			if ((m & (kRxOkL4 | kRxIcmp)) == kRxOkL4 && (uint32_t)len == m >> 16 && hl == (m >> 8 & 0xff)) {
+			if (!(v & 1) && (m & (kRxOkL4 | kRxIcmp)) == kRxOkL4 && (uint32_t)len == m >> 16 &&
+			    hl == (m >> 8 & 0xff)) {
 				t.stats[0]++;
 				return (uint16_t)(t.rxo[v >> 1] >> 16);
 			}
+			rx_frame = true;
 		}
 		rx_miss = true;
 	}
-	if (t.tx_open && hl >= 20 && ip_len <= 0xffff && (ip[9] == 6 || ip[9] == 17)) {
+	if (t.tx_open && !rx_frame && hl >= 20 && ip_len <= 0xffff && (ip[9] == 6 || ip[9] == 17) &&
+	    !(rx_miss && rx_owns(t, ip))) {
 		const int fo = ip[9] == 6 ? 16 : 6;
 		if ((uint32_t)len >= (uint32_t)fo + 2) {
 			if (tx_registered(t, ip, ip_len)) {
@@ -606,6 +674,7 @@ int rx_open_on(ThreadState &t, const RxBurst &r, bool posted)
 	t.rx_n = r.n;
 	t.rx_cur = 0;
 	t.rx_map = false;
+	t.rx_iv_built = false;
 	t.rx_open = true;
 	t.rx_posted = posted;
 	t.rx_served0 = t.stats[0];
@@ -698,6 +767,23 @@ extern "C" int cgck_rx_begin_posted(void)
 	return rx_open_on(t, r, true);
 }
 
+// The drain rule's two questions (include/cgck.h): is a burst still posted,
+// and would opening the oldest one wait for the GPU?
+extern "C" int cgck_rx_pending(void)
+{
+	const ThreadState *t = t_st;
+	return t ? (int)t->rxp_count : 0;
+}
+
+extern "C" int cgck_rx_ready(void)
+{
+	const ThreadState *t = t_st;
+	if (!t || t->rxp_count == 0)
+		return set_err(-ENOENT, "cgck_rx_ready: no burst posted");
+	const RxBurst &r = t->rxp[t->rxp_head];
+	return r.pend.seq ? burst_ready(t->ctx, &r.pend) : 1;
+}
+
 extern "C" int cgck_rx_end(void)
 {
 	ThreadState &t = tstate();
@@ -724,6 +810,7 @@ extern "C" int cgck_tx_begin(void)
 	if (t.tx_open)
 		return set_err(-EBUSY, "cgck_tx_begin: window already open on this thread");
 	t.tx_open = true;
+	t.tx_icmp = false;
 	t.txq.clear();
 	t.tx_max = nullptr;
 	t.tx_map = false;
@@ -742,6 +829,12 @@ namespace {
 // reference's callers have just stored them (ip_output.c:61, tcp_subr.c:75 /
 // gbtcp/tcp.c:426,436).
 constexpr uint32_t kTxFlags = CGCK_IP | CGCK_L4 | CGCK_ZERO_FIELDS;
+
+// A fill with ICMP messages also asks for their values without the
+// pseudo-header (kFlagL4Auto: by ip_p, as the RX window does); TCP and UDP
+// keep it.  Only then, because the lane-per-packet kernels take no
+// kFlagL4Auto and the group kernel is slower on small frames.
+inline uint32_t tx_flags(const TxFill &f) { return kTxFlags | (f.icmp ? kFlagL4Auto : 0u); }
 
 // Posted fills return values and the completion writes the fields on the
 // host (see cgck_tx_post); the lab build's $CGCK_TX_KSTORE has the kernel
@@ -762,6 +855,7 @@ int tx_compute(cgck_ctx *c, TxFill &f, bool post)
 {
 	const std::vector<TxEntry> &q = f.q;
 	const uint64_t n = q.size();
+	const uint32_t flags = tx_flags(f);
 	HIP_TRY(hipSetDevice(c->device));
 	RegRange reg{nullptr, nullptr, nullptr};
 	bool inplace = reg_find(q[0].ip, q[0].span, &reg);
@@ -806,10 +900,10 @@ int tx_compute(cgck_ctx *c, TxFill &f, bool post)
 			// ip_hl * 4 bytes, so no L4 field fits in it and none is stored).
 			f.stored = tx_kstore() && !l4_alone;
 			return desc_host_post(c, reg.lo, (size_t)(reg.hi - reg.lo), f.d.data(), m,
-					      kTxFlags | (f.stored ? CGCK_STORE : 0u), f.stored ? nullptr : f.o.data(), nullptr,
+					      flags | (f.stored ? CGCK_STORE : 0u), f.stored ? nullptr : f.o.data(), nullptr,
 					      nullptr, &f.pend);
 		}
-		return desc_host(c, reg.lo, (size_t)(reg.hi - reg.lo), f.d.data(), m, kTxFlags, f.o.data(), nullptr);
+		return desc_host(c, reg.lo, (size_t)(reg.hi - reg.lo), f.d.data(), m, flags, f.o.data(), nullptr);
 	}
 	for (uint64_t i = 0; i < n; i++)
 		f.idx[i] = (uint32_t)i;
@@ -831,7 +925,7 @@ int tx_compute(cgck_ctx *c, TxFill &f, bool post)
 		d[i].ip_len = (uint16_t)q[i].span;
 		at += (q[i].span + 15) & ~(size_t)15;
 	}
-	KParams p = {h, d, n, 0, 0, 0, kTxFlags, o, nullptr, nullptr, 0, nullptr};
+	KParams p = {h, d, n, 0, 0, 0, flags, o, nullptr, nullptr, 0, nullptr};
 	if ((rc = run(c, p, 1500, c->stream)))
 		return rc;
 	HIP_TRY(hipStreamSynchronize(c->stream));
@@ -873,7 +967,7 @@ int tx_write_fast(TxFill &f)
 		const uint32_t r = f.o[k], hs = f.hs[k];
 		if (hs & 0xffff) {
 			const uint16_t v = (uint16_t)(r >> 16);
-			memcpy(ip + (ip[0] & 15) * 4 + (ip[9] == 6 ? 16 : 6), &v, 2);
+			memcpy(ip + (ip[0] & 15) * 4 + l4_fo(ip), &v, 2);
 		}
 		if (hs >> 16) {
 			const uint16_t v = (uint16_t)r;
@@ -888,6 +982,7 @@ void tx_take(ThreadState &t, TxFill &f)
 {
 	t.tx_open = false;
 	t.tx_map = false;
+	f.icmp = t.tx_icmp;
 	f.q.swap(t.txq);
 	t.txq.clear();
 }
@@ -915,7 +1010,7 @@ extern "C" int cgck_tx_flush(void)
 		f.o.resize(f.d.size());
 		const DescSummary sum = {t.txd_max, t.txd_bytes};
 		int rc = desc_host_post(c, (void *)t.txd_lo, (size_t)(t.txd_hi - t.txd_lo), f.d.data(), f.d.size(),
-					kTxFlags, f.o.data(), nullptr, nullptr, &f.pend, &sum);
+					tx_flags(f), f.o.data(), nullptr, nullptr, &f.pend, &sum);
 		if (rc >= 0)
 			rc = f.pend.seq ? burst_collect(c, &f.pend) : f.pend.rc;
 		f.q.clear();
@@ -946,9 +1041,17 @@ extern "C" int cgck_tx_post(void)
 	if (!t.tx_open)
 		return set_err(-EINVAL, "cgck_tx_post: no open window on this thread");
 	if (t.txp_count == 2) {
-		t.tx_open = false;
-		t.txq.clear();
-		return set_err(-EBUSY, "cgck_tx_post: two fills already posted and not yet completed");
+		// A third fill: the oldest completes first (its fields are written
+		// now, before the kick that was to wait for them — final values
+		// either way), so no queued field is dropped.
+		const int rc = cgck_tx_complete();
+		if (rc < 0) {
+			t.tx_open = false;
+			t.txq.clear();
+			char msg[256];
+			snprintf(msg, sizeof(msg), "%s", err_text());
+			return set_err(rc, "cgck_tx_post: completing the oldest fill: %s", msg);
+		}
 	}
 	TxFill &f = t.txp[(t.txp_head + t.txp_count) & 1];
 	txd_close(t);
@@ -985,7 +1088,7 @@ extern "C" int cgck_tx_post(void)
 				f.o.resize(f.d.size());
 			const DescSummary sum = {t.txd_max, t.txd_bytes};
 			rc = desc_host_post(c, (void *)t.txd_lo, (size_t)(t.txd_hi - t.txd_lo), f.d.data(), f.d.size(),
-					    kTxFlags | (kstore ? CGCK_STORE : 0u), kstore ? nullptr : f.o.data(), nullptr, nullptr,
+					    tx_flags(f) | (kstore ? CGCK_STORE : 0u), kstore ? nullptr : f.o.data(), nullptr, nullptr,
 					    &f.pend, &sum);
 		} else {
 			rc = tx_compute(c, f, true);

@@ -387,8 +387,15 @@ __global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const 
 						c = 2;
 					else if ((uint32_t)r == want)
 						c = 1, last = want, n = (uint32_t)(r >> 32);
-					else if ((uint32_t)r != 0 && (int32_t)((uint32_t)r - want) > 0)
-						last = want; // not ours: on to the next seq
+					else if ((uint32_t)r != 0 && (int32_t)((uint32_t)r - want) > 0) {
+						// not ours: on to the next seq.  Its done word
+						// moves along with it, so done[j] never lags the
+						// host's seqs by more than the two in flight (a
+						// stale word would pass the host's serial compare
+						// once 2^31 requests had gone by without j)
+						last = want;
+						__hip_atomic_store(&box->done[j], want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+					}
 					else if (__builtin_amdgcn_s_memrealtime() - t0 > 4 * idle)
 						c = 2;
 					else
@@ -415,6 +422,11 @@ __global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const 
 		if (j >= W || cmd == 3) {
 			if (t == 0 && j == 0 && K > 1 && W == 1)
 				relay_store(dcmd + (seq & 1), (uint64_t)seq | (uint64_t)n << 32);
+			// a workgroup outside the request's W keeps its done word at the
+			// seq it stepped over (see the step-over above); the host reads
+			// done[j] only for j < W of the request it waits for
+			if (t == 0 && cmd == 1)
+				__hip_atomic_store(&box->done[j], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 			__syncthreads(); // cmd / cmd_n are rewritten by the next poll
 			continue;
 		}

@@ -223,6 +223,22 @@ int cgck_rx_end(void);
 int cgck_rx_post(void *base, size_t bytes, const cgck_desc_t *desc, uint64_t n);
 int cgck_rx_begin_posted(void);
 
+/* The drain rule.  con-gen's loop calls io_rx only on POLLIN
+ * (con-gen.c:508-517), so the burst posted last before a quiet spell would
+ * otherwise wait for the next frame to arrive.  Every thread_process
+ * iteration that posts no burst drains: while cgck_rx_pending() > 0, the
+ * transport opens the oldest posted burst (cgck_rx_begin_posted, which
+ * waits for its values if the GPU is not done), runs the stack over it,
+ * closes it and releases its slots.  A burst therefore
+ * never waits longer than one loop iteration after its post.
+ * cgck_rx_pending returns the bursts posted and not yet opened (0..2);
+ * cgck_rx_ready, without waiting, 1 when the oldest one's values are in
+ * (opening it will not wait), 0 while the GPU still computes it, -ENOENT
+ * when nothing is posted.  A transport may also drain a ready burst early,
+ * in the iteration that posted it (after check_timers, con-gen.c:524). */
+int cgck_rx_pending(void);
+int cgck_rx_ready(void);
+
 /* Deferred TX fill.  Between begin and flush, the
  * drop-in in_cksum/udp_cksum calls of THIS thread that target an IPv4
  * header (len == ip_hl*4) or a TCP/UDP segment lying inside memory
@@ -247,7 +263,8 @@ int cgck_tx_flush(void);
  * slots.  The transport calls
  * it before it hands those slots to the NIC — at the next loop's kick
  * (con-gen.c:493), so the GPU computes burst k while the stack builds burst
- * k + 1.  At most two fills are posted and not yet completed (-EBUSY). */
+ * k + 1.  At most two fills are posted and not yet completed: a third
+ * cgck_tx_post completes the oldest first (its fields are written then). */
 int cgck_tx_post(void);
 int cgck_tx_complete(void);
 

@@ -109,6 +109,10 @@ class Port:
         L.oracle_replay_rx.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                        ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                        ctypes.c_void_p, ctypes.c_void_p]
+        L.oracle_replay_rx_rsp.argtypes = ([ctypes.c_void_p] * 4 + [ctypes.c_uint64, ctypes.c_int, ctypes.c_int]
+                                           + [ctypes.c_void_p] * 3 + [ctypes.c_uint64, ctypes.c_uint32,
+                                           ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p,
+                                           ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p])
 
     # -- pure functions (subr.c:186-195, 212-223) --
     def in_cksum(self, buf, off=0, n=None):
@@ -239,6 +243,28 @@ class Port:
         self.lib.oracle_replay_rx(fin, fudp, base.ctypes.data, desc12.ctypes.data, n, stack, ip_in, tcp_in,
                                   res.ctypes.data, ctr.ctypes.data)
         return res[:n], ctr
+
+    R_NOTOURS = 5    # oracle_replay_rx_rsp: ip_input.c:90, answered with icmp_error
+    KA_DTYPE = np.dtype([("laddr", "<u4"), ("faddr", "<u4"), ("lport", "<u2"), ("fport", "<u2"),
+                         ("rcv_nxt", "<u4"), ("snd_una", "<u4"), ("hiwat", "<u4"), ("scale", "<u4")])
+
+    def replay_rx_rsp(self, fin, fudp, base, desc12, n, ip_in, tcp_in, tx, slot, cap, local, laddr, ka, ip_id):
+        """bsd44's receive burst plus the packets it sends back (RSTs, ICMP
+        unreachables, echo replies) and nka keepalives from check_timers,
+        built into the transmit ring `tx` (cap slots of `slot` bytes; packets
+        built while it is full go to `local`, 2048 B each).  Returns
+        (outcomes, counters, txs, ip_id): txs = [slots used, pkt_body packets,
+        RSTs, ICMP errors, echo replies, keepalives]."""
+        res = np.zeros(max(n, 1), np.uint8)
+        ctr = np.zeros(6, np.uint64)
+        txs = np.zeros(6, np.uint32)
+        idc = ctypes.c_uint16(ip_id)
+        ka = np.zeros(0, self.KA_DTYPE) if ka is None else ka
+        self.lib.oracle_replay_rx_rsp(fin, fudp, base.ctypes.data, desc12.ctypes.data, n, ip_in, tcp_in,
+                                      res.ctypes.data, ctr.ctypes.data, tx.ctypes.data, slot, cap,
+                                      local.ctypes.data, laddr[0], laddr[1], ka.ctypes.data, len(ka),
+                                      ctypes.byref(idc), txs.ctypes.data)
+        return res[:n], ctr, txs, idc.value
 
     def cpu_bench(self, fin, fudp, base, n, stride, ip_len, threads=1, reps=1):
         sink = ctypes.c_uint64()

@@ -24,9 +24,10 @@ def le16(p, off, v):
     p[off + 1] = (v >> 8) & 0xFF
 
 
-def frame(rng, ck, proto, l4len, ihl=5, df=True, ttl=64, ulen=None, tcp_off=5, fill=True):
+def frame(rng, ck, proto, l4len, ihl=5, df=True, ttl=64, ulen=None, tcp_off=5, fill=True, pre=None):
     """One IPv4 datagram of ihl*4 + l4len bytes with correct checksums
-    (`ck` has in_cksum(buf, off, n) and udp_cksum(buf, off, n))."""
+    (`ck` has in_cksum(buf, off, n) and udp_cksum(buf, off, n)); `pre(p,
+    hl)` sets further fields before the checksums are filled."""
     hl = 4 * ihl
     ln = hl + l4len
     p = rng.integers(0, 256, ln, dtype=np.uint8)
@@ -40,6 +41,8 @@ def frame(rng, ck, proto, l4len, ihl=5, df=True, ttl=64, ulen=None, tcp_off=5, f
         p[hl + 12] = (tcp_off << 4) | (int(p[hl + 12]) & 0x0F)
     if proto == 17 and l4len >= 6:
         be16(p, hl + 4, l4len if ulen is None else ulen)
+    if pre is not None:
+        pre(p, hl)
     if fill:
         if proto == 6 and l4len >= 18:
             le16(p, hl + 16, 0)
@@ -138,3 +141,78 @@ def registered_copy(buf):
     r = np.frombuffer(m, np.uint8)
     r[:len(buf)] = buf
     return m, r, size
+
+LADDR = (0x0A000001, 0x0A000004)   # t_ip_laddr_min/max of the response corpora (10.0.0.1-4)
+
+
+def rsp_corpus(rng, ck, n, laddr=LADDR):
+    """n frames that draw replies from bsd44 with no PCB
+    (oracle_replay_rx_rsp): TCP segments of every flag mix to closed ports
+    (RST, tcp_input.c:881-899), UDP datagrams to closed ports (port
+    unreachable, udp_usrreq.c:98-108), ICMP echo requests (echo reply,
+    ip_icmp.c:282-288) and other ICMP types, datagrams for addresses that
+    are not ours (net unreachable, ip_input.c:90), fragments; one in eight
+    corrupted (payload, header or L4 field), some with uh_ulen below ip_len
+    or an ICMP message below ICMP_ADVLENMIN."""
+    out = []
+    for i in range(n):
+        kind = int(rng.integers(0, 100))
+        proto = (6, 6, 17, 1)[i % 4]
+        ours = kind >= 12
+        dst = int(rng.integers(laddr[0], laddr[1] + 1)) if ours else int(rng.integers(0x0B000000, 0x0C000000))
+        if proto == 6:
+            l4 = int(rng.choice([20, 20, 24, 32, 52, 300, 1460]))
+        elif proto == 17:
+            l4 = int(rng.choice([8, 9, 20, 64, 512, 1472]))
+        else:
+            l4 = int(rng.choice([8, 20, 36, 40, 64, 84, 1000]))
+        ihl = 5 if i % 9 else int(rng.integers(6, 9))
+        if ihl * 4 + l4 > 1500:
+            l4 = 1500 - ihl * 4
+        tflags = int(rng.choice([0x02, 0x10, 0x12, 0x04, 0x14, 0x18, 0x11, 0x00, 0x01, 0x03]))
+        itype, icode = (8, 0) if kind % 3 else (int(rng.choice([3, 3, 11, 12, 4, 5, 0, 13, 30])),
+                                                int(rng.integers(0, 16)))
+
+        def pre(p, hl, dst=dst, proto=proto, tflags=tflags, itype=itype, icode=icode):
+            p[16], p[17], p[18], p[19] = (dst >> 24) & 255, (dst >> 16) & 255, (dst >> 8) & 255, dst & 255
+            if proto == 6 and len(p) >= hl + 14:
+                p[hl + 13] = tflags
+            if proto == 1 and len(p) >= hl + 2:
+                p[hl], p[hl + 1] = itype, icode
+                if itype != 8 and len(p) >= hl + 28:     # an inner IPv4 header for the error types
+                    p[hl + 8] = 0x45
+        ulen = None
+        if proto == 17 and kind % 17 == 5:
+            ulen = max(8, l4 - int(rng.integers(1, 8)))
+        p = frame(rng, ck, proto, l4, ihl=ihl, ulen=ulen, pre=pre, df=kind % 23 != 7)
+        if kind % 23 == 7:                  # a fragment (ip_off MF): no error for it, no delivery
+            p[6] = 0x20
+            le16(p, 10, 0)
+            le16(p, 10, ck.in_cksum(p, 0, ihl * 4))
+        c = int(rng.integers(0, 8))
+        if c == 0:                          # payload bit flip
+            j = int(rng.integers(ihl * 4, len(p)))
+            p[j] ^= 1 << int(rng.integers(0, 8))
+        elif c == 1 and kind % 2:           # header bit flip
+            p[int(rng.choice([4, 5, 8, 12, 15]))] ^= 0x10
+        elif c == 1:                        # wrong L4 field
+            p[ihl * 4 + {6: 16, 17: 6, 1: 2}[proto]] ^= 0x01
+        out.append(p)
+    return out
+
+
+def pool(frames, tx_slots):
+    """One registered-style pool of 2048-byte slots, as a netmap pool holds
+    both rings: receive frame k in slot 2k at +14, transmit slot j at slot
+    2j + 1 while j < len(frames), then after them.  Returns (pool bytes,
+    DESC_DTYPE descriptors, transmit base offset, transmit stride)."""
+    nrx = len(frames)
+    nslots = 2 * max(nrx, tx_slots) + 1
+    buf = np.zeros(nslots * SLOT, np.uint8)
+    desc = np.zeros(nrx, cgck.DESC_DTYPE)
+    for k, p in enumerate(frames):
+        o = 2 * k * SLOT
+        buf[o:o + L2] = (0x02, 0, 0, 0, 0, 1, 0x02, 0, 0, 0, 0, 2, 0x08, 0x00)
+        buf[o + L2:o + L2 + len(p)] = p
+        desc[k] = (o, L2, len(p))
+    return buf, desc, SLOT, 2 * SLOT

@@ -399,10 +399,6 @@ def test_tx_pipelined_fill(port, server):
                 tx_calls(slots[i], ln, 16)
             assert cgck.tx_post() == 160
             bursts.append(want)
-            if k == 1:
-                with pytest.raises(cgck.CgckError, match="already posted"):
-                    cgck.tx_begin()
-                    cgck.tx_post()
             if k >= 1:
                 assert cgck.tx_complete() == 160
                 for i, ln, ref in bursts[k - 1]:
@@ -605,3 +601,322 @@ def test_pipelined_across_server_idle(port):
     finally:
         cgck.burst_close()
         L.cgck_host_unregister(tx_ring.ctypes.data)
+
+
+# ---------------------------------------------------------------------------
+# The drain rule (include/cgck.h: cgck_rx_pending / cgck_rx_ready) and the
+# burst server's bookkeeping across out-of-order collects
+# ---------------------------------------------------------------------------
+
+def replay_posted(port, R, buf, desc, got, cell):
+    """Open the oldest posted burst, replay the stack over it, compare with
+    the reference replay of the same bytes."""
+    stack, ip_in, tcp_in = cell
+    ref = buf.copy()
+    a = port.replay_rx(*R.fn_pointers(), ref, desc.view(np.uint8), len(desc), stack, ip_in, tcp_in)
+    s0 = cgck.window_stats()
+    cgck.rx_begin_posted()
+    try:
+        b = port.replay_rx(*cgck.fn_pointers(), got, desc.view(np.uint8), len(desc), stack, ip_in, tcp_in)
+    finally:
+        served = cgck.rx_end()
+    s1 = cgck.window_stats()
+    assert np.array_equal(a[0], b[0]), (cell, np.nonzero(a[0] != b[0])[0][:8])
+    assert np.array_equal(a[1], b[1]), (cell, a[1], b[1])
+    assert np.array_equal(ref, got), cell
+    return served, [y - x for x, y in zip(s0, s1)], int(b[1][4] + b[1][5])
+
+
+@pytest.mark.parametrize("server", [False, True])
+@pytest.mark.parametrize("nframes", [1, 3, 40, 700])
+def test_rx_lone_burst_drained(port, nframes, server):
+    """A burst posted with nothing after it (the last one before a quiet
+    spell: con-gen.c:508-517 calls io_rx only on POLLIN) is drained in the
+    iteration that follows — cgck_rx_pending says one is posted,
+    cgck_rx_ready turns 1 without a wait, and the window over it replays
+    bit-exact with every call answered — and every iteration with nothing
+    posted finds nothing to drain."""
+    import time
+    R = referee(port)
+    L = cgck.load()
+    if server:
+        cgck.burst_open(max_pkts=1024, max_bytes=4 << 20)
+    rings = []
+    try:
+        for it in range(3):
+            rng = np.random.default_rng(5100 + 10 * it + nframes)
+            buf, desc = rxcorpus.ring(rxcorpus.corpus(rng, R, nframes, clean=True))
+            raw, ring, size = rxcorpus.registered_copy(buf)
+            assert L.cgck_host_register(ring.ctypes.data, size) == 0
+            rings.append((raw, ring))
+            got = ring[:len(buf)]
+            assert cgck.rx_pending() == 0
+            with pytest.raises(cgck.CgckError, match="no burst posted"):
+                cgck.rx_ready()
+            assert cgck.rx_post(got, desc) == nframes       # io_rx: the burst, then a quiet spell
+            assert cgck.rx_pending() == 1
+            t0 = time.monotonic()
+            while not cgck.rx_ready():                       # the next iteration's check (no wait)
+                assert time.monotonic() - t0 < 2.0
+            cell = FLAGS[(3 * it + nframes) % len(FLAGS)]
+            served, d, calls = replay_posted(port, R, buf, desc, got, cell)
+            # (a payload bit flip can land in a UDP length, making a call the
+            # window does not hold: it is computed synchronously, still exact)
+            assert served == d[0] and served + d[1] == calls and d[1] <= calls // 100, (cell, served, calls, d)
+            assert cgck.rx_pending() == 0
+    finally:
+        if server:
+            cgck.burst_close()
+        for raw, ring in rings:
+            L.cgck_host_unregister(ring.ctypes.data)
+
+
+@pytest.mark.parametrize("gap", ["idle", "register"])
+def test_burst_relaunch_after_out_of_order_collect(port, gap):
+    """The pipelined loop collects out of seq order: TX fill b completes
+    before the older RX burst a, whose slot the next post then needs.  The
+    server then goes away — it idles out, or another range's registration
+    stops it — and the next post relaunches it.  The relaunch starts after
+    the latest seq collected (b), so it serves c and d; had it started after
+    a, its leader would wait for b in a slot that holds d."""
+    import time
+    R = referee(port)
+    L = cgck.load()
+    raw_tx, tx_ring, tx_size = rxcorpus.registered_copy(np.zeros(64 * 2048, np.uint8))
+    slots = tx_ring[:64 * 2048].reshape(64, 2048)
+    assert L.cgck_host_register(tx_ring.ctypes.data, tx_size) == 0
+    cgck.burst_open(max_pkts=1024, max_bytes=4 << 20, idle_ms=20)
+    rng = np.random.default_rng(5200)
+    bursts = [rxcorpus.ring(rxcorpus.corpus(rng, R, 50 + 20 * k, clean=True)) for k in range(2)]
+    gots = [b.copy() for b, _ in bursts]
+    other = None
+
+    def fill(lo):
+        want = []
+        cgck.tx_begin()
+        for i in range(lo, lo + 16):
+            ln = int(rng.integers(40, 1501))
+            pkt = tcp_pkt(rng, ln)
+            slots[i, 14:14 + ln] = pkt
+            want.append((i, ln, expected(port, pkt, 16)))
+            tx_calls(slots[i], ln, 16)
+        assert cgck.tx_post() == 32
+        return want
+
+    try:
+        assert cgck.rx_post(gots[0], bursts[0][1]) == len(bursts[0][1])   # seq a
+        w_b = fill(0)                                                      # seq b
+        assert cgck.tx_complete() == 32                                     # collect b
+        for i, ln, r in w_b:
+            assert np.array_equal(slots[i, 14:14 + ln], r)
+        assert cgck.rx_post(gots[1], bursts[1][1]) == len(bursts[1][1])   # collects a, posts c
+        if gap == "idle":
+            time.sleep(0.1)                                                # > idle_ms
+        else:
+            other = rxcorpus.registered_copy(np.zeros(8192, np.uint8))
+            assert L.cgck_host_register(other[1].ctypes.data, other[2]) == 0
+        w_d = fill(16)                                                     # seq d: relaunches
+        assert cgck.tx_complete() == 32
+        for i, ln, r in w_d:
+            assert np.array_equal(slots[i, 14:14 + ln], r)
+        for k in range(2):
+            replay_posted(port, R, bursts[k][0], bursts[k][1], gots[k], FLAGS[4 + k])
+    finally:
+        cgck.burst_close()
+        L.cgck_host_unregister(tx_ring.ctypes.data)
+        if other is not None:
+            L.cgck_host_unregister(other[1].ctypes.data)
+
+
+def test_posted_burst_survives_unregister(port):
+    """A burst posted over a registered ring, then the ring unregistered
+    before its window opens: cgck_host_unregister serves the posted request
+    before the mapping changes (the server never reads the range after), so
+    the window's values are the ring's."""
+    R = referee(port)
+    L = cgck.load()
+    cgck.burst_open(max_pkts=1024, max_bytes=4 << 20)
+    try:
+        rng = np.random.default_rng(5300)
+        buf, desc = rxcorpus.ring(rxcorpus.corpus(rng, R, 300, clean=True))
+        raw, ring, size = rxcorpus.registered_copy(buf)
+        assert L.cgck_host_register(ring.ctypes.data, size) == 0
+        got = ring[:len(buf)]
+        assert cgck.rx_post(got, desc) == 300
+        assert L.cgck_host_unregister(ring.ctypes.data) == 0
+        served, d, calls = replay_posted(port, R, buf, desc, got, FLAGS[7])
+        assert served == d[0] and served + d[1] == calls and d[1] <= calls // 100
+    finally:
+        cgck.burst_close()
+
+
+@pytest.mark.parametrize("server", [False, True])
+def test_tx_third_post_completes_oldest(port, server):
+    """Two fills posted and a third window closed: cgck_tx_post completes the
+    oldest first (its fields written), so no queued field is dropped."""
+    rng = np.random.default_rng(5400 + server)
+    raw, ring, size = rxcorpus.registered_copy(np.zeros(96 * 2048, np.uint8))
+    slots = ring[:96 * 2048].reshape(96, 2048)
+    L = cgck.load()
+    assert L.cgck_host_register(ring.ctypes.data, size) == 0
+    if server:
+        cgck.burst_open(max_pkts=1024, max_bytes=4 << 20)
+    try:
+        bursts = []
+        for k in range(3):
+            want = []
+            cgck.tx_begin()
+            for i in range(k * 32, k * 32 + 32):
+                ln = int(rng.integers(40, 1501))
+                pkt = tcp_pkt(rng, ln)
+                slots[i, 14:14 + ln] = pkt
+                want.append((i, ln, expected(port, pkt, 16)))
+                tx_calls(slots[i], ln, 16)
+            assert cgck.tx_post() == 64
+            bursts.append(want)
+        for i, ln, ref in bursts[0]:                     # written by the third post
+            assert np.array_equal(slots[i, 14:14 + ln], ref), (0, i)
+        assert cgck.tx_complete() == 64 and cgck.tx_complete() == 64 and cgck.tx_complete() == 0
+        for k in (1, 2):
+            for i, ln, ref in bursts[k]:
+                assert np.array_equal(slots[i, 14:14 + ln], ref), (k, i)
+    finally:
+        if server:
+            cgck.burst_close()
+        L.cgck_host_unregister(ring.ctypes.data)
+
+
+# ---------------------------------------------------------------------------
+# The TX window across the whole loop iteration: replies built while the
+# stack processes a receive burst (tcp_respond RSTs, icmp_error, echo
+# replies) and keepalives at check_timers are queued, not computed one call
+# at a time
+# ---------------------------------------------------------------------------
+
+def ka_records(rng, n):
+    ka = np.zeros(n, oracle.Port.KA_DTYPE)
+    for f, hi in (("laddr", 2 ** 32), ("faddr", 2 ** 32), ("rcv_nxt", 2 ** 32), ("snd_una", 2 ** 32)):
+        ka[f] = rng.integers(0, hi, n, dtype=np.uint64)
+    ka["lport"] = rng.integers(0, 2 ** 16, n)
+    ka["fport"] = rng.integers(0, 2 ** 16, n)
+    ka["hiwat"] = rng.integers(0, 2 ** 20, n)
+    ka["scale"] = rng.integers(0, 9, n)
+    return ka
+
+
+class Iteration:
+    """One side (reference functions, or libcgck's drop-ins inside the
+    windows) of thread_process iterations over one pool: the receive burst
+    with its replies, then check_timers' keepalives, replies built into the
+    transmit slots in order."""
+
+    def __init__(self, port, fns, pool, tx_base, tx_stride, cap):
+        self.port, self.fns, self.pool = port, fns, pool
+        self.tx_base, self.tx_stride, self.cap = tx_base, tx_stride, cap
+        self.local = np.zeros(2048 * 256, np.uint8)
+        self.used = self.nlocal = 0
+        self.ip_id = 4242
+        self.sent = np.zeros(4, np.int64)
+
+    def _run(self, desc, n, ip_in, tcp_in, ka):
+        tx = self.pool[self.tx_base + self.used * self.tx_stride:]
+        loc = self.local[self.nlocal * 2048:]
+        res, ctr, txs, self.ip_id = self.port.replay_rx_rsp(
+            self.fns[0], self.fns[1], self.pool, desc.view(np.uint8), n, ip_in, tcp_in, tx, self.tx_stride,
+            max(self.cap - self.used, 0), loc, rxcorpus.LADDR, ka, self.ip_id)
+        self.used += int(txs[0])
+        self.nlocal += int(txs[1])
+        self.sent += txs[2:].astype(np.int64)
+        return res, ctr
+
+    def burst(self, desc, ip_in, tcp_in):
+        return self._run(desc, len(desc), ip_in, tcp_in, None)
+
+    def timers(self, ka):
+        return self._run(np.zeros(0, cgck.DESC_DTYPE), 0, 0, 0, ka)
+
+
+@pytest.mark.parametrize("mode", ["sync", "pipelined"])
+@pytest.mark.parametrize("ring", ["room", "full"])
+def test_rsp_iteration_tx_window(port, mode, ring):
+    """con-gen's loop with the TX window open from the kick to the flush:
+    io_tx, then the receive burst through the RX window (cgck_rx_begin, or
+    pipelined: post burst k, replay burst k - 1, drain the last one), the
+    stack's replies to it and check_timers' keepalives, then the flush (or
+    cgck_tx_post, completed before the next kick).  The corpus draws RSTs,
+    net / port unreachables and echo replies (oracle_replay_rx_rsp).  RX
+    outcomes, counters and the whole pool — receive frames and replies —
+    equal the reference replay's byte for byte; every reply call in ring
+    memory is queued (window_stats[3] = 0 with room in the ring) and no
+    received frame's verify call is (the replay would count it bad).  With
+    the ring full the replies built in pkt_body are computed synchronously
+    (window_stats[3] > 0) and are exact too."""
+    R = referee(port)
+    L = cgck.load()
+    rng = np.random.default_rng(6100 + (mode == "pipelined") + 2 * (ring == "full"))
+    nb = 4
+    bursts = [rxcorpus.rsp_corpus(rng, R, 60 + 70 * k) for k in range(nb)]
+    frames = [f for b in bursts for f in b]
+    kas = [ka_records(rng, 6) for _ in range(nb)]
+    cap = 2000 if ring == "room" else 40
+    buf, desc_all, tx_base, tx_stride = rxcorpus.pool(frames, 1200)
+    descs, at = [], 0
+    for b in bursts:
+        descs.append(desc_all[at:at + len(b)])
+        at += len(b)
+    ref = buf.copy()
+    raw, got, size = rxcorpus.registered_copy(buf)
+    assert L.cgck_host_register(got.ctypes.data, size) == 0
+    got = got[:len(buf)]
+    A = Iteration(port, R.fn_pointers(), ref, tx_base, tx_stride, cap)
+    B = Iteration(port, cgck.fn_pointers(), got, tx_base, tx_stride, cap)
+    cgck.burst_open(max_pkts=4096, max_bytes=8 << 20)
+    s0 = cgck.window_stats()
+    try:
+        for k in range(nb + (mode == "pipelined")):
+            flags = FLAGS[(7 * k + 3) % 9]           # bsd44 cells
+            if mode == "pipelined":
+                cgck.tx_complete()                   # before io_tx (con-gen.c:493)
+            cgck.tx_begin()
+            if mode == "sync":
+                cgck.rx_begin(got, descs[k])
+                todo = k
+            else:
+                if k < nb:
+                    cgck.rx_post(got, descs[k])
+                todo = k - 1
+                if k == nb:                          # nothing received: the drain rule
+                    assert cgck.rx_pending() == 1
+            if todo >= 0:
+                if mode == "pipelined":
+                    cgck.rx_begin_posted()
+                try:
+                    rb = B.burst(descs[todo], flags[1], flags[2])
+                finally:
+                    cgck.rx_end()
+                ra = A.burst(descs[todo], flags[1], flags[2])
+                assert np.array_equal(ra[0], rb[0]), (k, np.nonzero(ra[0] != rb[0])[0][:8])
+                assert np.array_equal(ra[1], rb[1]), (k, ra[1], rb[1])
+                A.timers(kas[todo])
+                B.timers(kas[todo])
+            if mode == "sync":
+                cgck.tx_flush()
+            else:
+                cgck.tx_post()
+        if mode == "pipelined":
+            cgck.tx_complete()
+            assert cgck.tx_complete() == 0 and cgck.rx_pending() == 0
+        s1 = cgck.window_stats()
+    finally:
+        cgck.burst_close()
+        L.cgck_host_unregister(got.ctypes.data)
+    d = [y - x for x, y in zip(s0, s1)]
+    assert A.used == B.used and A.nlocal == B.nlocal and np.array_equal(A.sent, B.sent)
+    assert min(A.sent) > 0, A.sent
+    assert np.array_equal(ref, got), np.nonzero(ref != got)[0][:16]
+    assert np.array_equal(A.local[:A.nlocal * 2048], B.local[:B.nlocal * 2048])
+    tx_calls = 2 * int(A.sent.sum())
+    if ring == "room":
+        assert d[3] == 0 and d[2] == tx_calls, (d, tx_calls)
+    else:
+        assert d[3] == 2 * B.nlocal and d[2] == 2 * B.used, (d, B.used, B.nlocal)

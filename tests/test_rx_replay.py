@@ -161,3 +161,91 @@ def test_thread_ctx_and_rx_begin_without_device():
     with pytest.raises(cgck.CgckError, match="no HIP device"):
         cgck.rx_begin(buf, desc)
     assert cgck.window_stats() == [0, 0, 0, 0]
+
+
+# ---------------------------------------------------------------------------
+# bsd44 with the packets RX processing sends back (oracle_replay_rx_rsp)
+# ---------------------------------------------------------------------------
+
+def rsp_replay(port, fns, buf, desc, tx_base, tx_stride, cap, ip_in, tcp_in, ka=None, ip_id=77):
+    local = np.zeros(2048 * 64, np.uint8)
+    tx = buf[tx_base:]
+    res, ctr, txs, idn = port.replay_rx_rsp(fns[0], fns[1], buf, desc.view(np.uint8), len(desc), ip_in, tcp_in,
+                                            tx, tx_stride, cap, local, rxcorpus.LADDR, ka, ip_id)
+    return res, ctr, txs, idn, local
+
+
+def keepalives(rng, n):
+    ka = np.zeros(n, P.KA_DTYPE)
+    ka["laddr"] = rng.integers(0, 2 ** 32, n, dtype=np.uint64)
+    ka["faddr"] = rng.integers(0, 2 ** 32, n, dtype=np.uint64)
+    ka["lport"] = rng.integers(0, 2 ** 16, n)
+    ka["fport"] = rng.integers(0, 2 ** 16, n)
+    ka["rcv_nxt"] = rng.integers(0, 2 ** 32, n, dtype=np.uint64)
+    ka["snd_una"] = rng.integers(0, 2 ** 32, n, dtype=np.uint64)
+    ka["hiwat"] = rng.integers(0, 2 ** 20, n)
+    ka["scale"] = rng.integers(0, 9, n)
+    return ka
+
+
+def test_rsp_replay_reference_vs_restatement(port):
+    """The response replay over the reference's own in_cksum / udp_cksum and
+    over the restatement: outcomes, counters, replies sent and every byte of
+    both rings equal; every reply carries checksums that verify."""
+    R = oracle.reference()
+    if R is None:
+        pytest.skip("reference build absent")
+    rng = np.random.default_rng(81)
+    frames = rxcorpus.rsp_corpus(rng, R, 600)
+    buf, desc, tx_base, tx_stride = rxcorpus.pool(frames, 700)
+    ka = keepalives(rng, 20)
+    a = rsp_replay(port, R.fn_pointers(), buf.copy(), desc, tx_base, tx_stride, 700, 1, 1, ka)
+    b_buf = buf.copy()
+    b = rsp_replay(port, port.fn_pointers(), b_buf, desc, tx_base, tx_stride, 700, 1, 1, ka)
+    for x, y in zip(a[:4], b[:4]):
+        assert np.array_equal(np.asarray(x), np.asarray(y))
+    txs = b[2]
+    assert txs[1] == 0 and txs[0] == txs[2:].sum()
+    assert min(txs[2:]) > 0, txs                      # RSTs, ICMP errors, echo replies, keepalives
+    assert sum(1 for r in b[0] if r == P.R_NOTOURS) > 0
+    # each reply's checksums verify (zero the field, recompute, compare)
+    for j in range(int(txs[0])):
+        ip = b_buf[tx_base + j * tx_stride + 14:]
+        hl = (int(ip[0]) & 15) * 4
+        tot = int(ip[2]) << 8 | int(ip[3])
+        h = ip[:hl].copy()
+        stored = h[10:12].copy()
+        h[10:12] = 0
+        assert np.frombuffer(np.uint16(port.in_cksum(h, 0, hl)).tobytes(), np.uint8).tolist() == stored.tolist()
+        pkt = ip[:tot].copy()
+        if pkt[9] == 6:
+            st = pkt[hl + 16:hl + 18].copy()
+            pkt[hl + 16:hl + 18] = 0
+            assert np.uint16(port.udp_cksum(pkt, 0, tot - hl)).tobytes() == st.tobytes(), j
+        else:
+            assert pkt[9] == 1
+            st = pkt[hl + 2:hl + 4].copy()
+            pkt[hl + 2:hl + 4] = 0
+            assert np.uint16(port.in_cksum(pkt, hl, tot - hl)).tobytes() == st.tobytes(), j
+
+
+def test_rsp_replay_ring_full_uses_pkt_body(port):
+    """With the transmit ring full the replies are built in pkt_body
+    (netmap_init_tx_packet, netmap.c:74-83): same bytes either way."""
+    rng = np.random.default_rng(82)
+    frames = rxcorpus.rsp_corpus(rng, port, 120)
+    buf, desc, tx_base, tx_stride = rxcorpus.pool(frames, 130)
+    fns = port.fn_pointers()
+    full = rsp_replay(port, fns, buf.copy(), desc, tx_base, tx_stride, 130, 2, 2)
+    part_buf = buf.copy()
+    part = rsp_replay(port, fns, part_buf, desc, tx_base, tx_stride, 16, 2, 2)
+    assert part[2][0] == 16 and part[2][1] == full[2][0] - 16
+    assert np.array_equal(full[0], part[0]) and np.array_equal(full[1], part[1])
+    # the packets past the ring equal the ring-built ones of the full replay
+    full_buf = buf.copy()
+    rsp_replay(port, fns, full_buf, desc, tx_base, tx_stride, 130, 2, 2)
+    for j in range(16, int(full[2][0])):
+        want = full_buf[tx_base + j * tx_stride:tx_base + j * tx_stride + 1514]
+        got = part[4][(j - 16) * 2048:(j - 16) * 2048 + 1514]
+        ln = 14 + (int(want[16]) << 8 | int(want[17]))
+        assert np.array_equal(want[:ln], got[:ln]), j

@@ -1,0 +1,54 @@
+# Round 5 GPU steps: bash tools/gpu_r5.sh OUTDIR step [step ...]
+#   tests   — the whole -m gpu suite (slow ones included)
+#   quick   — the burst / window tests only
+#   txburst — tools/txburst 0.2 (all burst rows, pipelined included)
+#   bench   — python bench.py (default N=1 line)
+#   stress  — tools/reg_stress.py 60 plain
+# Each step has its own time limit; the script stops at the first failure.
+cd $GRAFT_REPO_ROOT
+O=gpurun_out/$1
+shift
+mkdir -p $O
+rocminfo 2>/dev/null | grep -m2 -E "Marketing" > $O/info.txt || true
+run() { # name seconds cmd...
+	local name=$1 secs=$2; shift 2
+	timeout -k 10 $secs "$@" > $O/$name.log 2>&1
+	local rc=$?
+	echo "$name rc=$rc"; tail -3 $O/$name.log
+	return $rc
+}
+for step in "$@"; do
+	case $step in
+	tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread || exit 1 ;;
+	cycles) for i in 1 2 3; do run pytest_cycles$i 300 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread -k "not reregister or reregister" || true; done ;;
+	testsk) run pytest_gpu 900 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread || true ;;
+	quick) run pytest_quick 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "burst or window or pipelined or rx_post or tx_" || exit 1 ;;
+	txburst) run txburst 400 tools/txburst 0.2 || exit 1 ;;
+	txloop) run txloop 400 tools/txloop 0.2 || exit 1 ;;
+	txloop128) TXLOOP_LEN=128 run txloop128 400 tools/txloop 0.2 || exit 1 ;;
+	txlens) # con-gen's typical frames (54-130 B): 128 B beside 64 B
+		TXBURST_LENS=128,64 run txburst_128 400 tools/txburst 0.2 || exit 1 ;;
+	txstack) # the same rows with 150 us of other stack work between bursts
+		TXBURST_STACK_US=150 run txburst_stack150 400 tools/txburst 0.2 || exit 1 ;;
+	txkstore) # lab: the kernel stores the posted fills' fields (CGCK_STORE) instead of the host
+		LD_LIBRARY_PATH=$PWD/tools/labso CGCK_TX_KSTORE=1 run txburst_kstore 400 tools/txburst 0.2 || exit 1 ;;
+	txtouch) # the TX rows with each frame's line written by the core before the clock starts
+		TXBURST_PRETOUCH=1 run txburst_pretouch 400 tools/txburst 0.2 || exit 1 ;;
+	bench) run bench 600 python -u bench.py || exit 1 ;;
+	smoke) run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" || exit 1 ;;
+	bench2) run bench_n2 600 python -u bench.py --gpus 2 --allow-shared-devices --steps 5 --warmup 2 --no-burst || exit 1 ;;
+	stress) run stress 110 python -u tools/reg_stress.py 60 plain || exit 1 ;;
+	stressm) for m in heap plain lock mmap; do run stress_$m 110 python -u tools/reg_stress.py 40 $m || exit 1; done ;;
+	stress3) run stress_r3 110 python -u tools/reg_stress.py 30 plain tools/r3lib/libcgck.so || exit 1
+		run stress_new 110 python -u tools/reg_stress.py 30 plain || exit 1 ;;
+	lpwab) # lpw on each IMIX layout, full kernel vs its DMA rounds alone (lab build)
+		for w in imixp imix ring; do
+			for k in 1 2; do
+				CGCK_LIB=con-gen_amd/libcgck_lab.so run lpw_${w}_full$k 120 python -u tools/one_workload.py $w --launches 10 || exit 1
+				CGCK_LIB=con-gen_amd/libcgck_lab.so CGCK_LPW_NOCONS=1 run lpw_${w}_rounds$k 120 python -u tools/one_workload.py $w --launches 10 || exit 1
+			done
+		done ;;
+	prof) bash tools/gpu_prof_layouts.sh $(basename $O)/prof || exit 1 ;;
+	*) echo "unknown step $step"; exit 2 ;;
+	esac
+done

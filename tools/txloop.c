@@ -1,0 +1,416 @@
+/*
+ * txloop — con-gen's worker loop at the checksum boundary, through the C-ABI
+ * from C, the way thread_process (con-gen.c:484-538) would run it with both
+ * windows open across the whole iteration:
+ *
+ *   cgck_tx_complete()                 the previous iteration's fill, before
+ *   io_tx()                            the kick (con-gen.c:493)
+ *   cgck_tx_begin()
+ *   io_rx: cgck_rx_post(burst k)       the frames that just arrived;
+ *          cgck_rx_begin_posted()      the window over burst k - 1: per frame
+ *          ip_input -> tcp_input       the stack's verify calls (field saved,
+ *                                      zeroed, restored) and, in the "reply"
+ *                                      mix, the segment it sends back built
+ *                                      in a transmit slot (tcp_respond's
+ *                                      tcp_cksum + ip_output's ip_cksum,
+ *                                      tcp_subr.c:93-123), queued by the TX
+ *                                      window; cgck_rx_end()
+ *   the rest of the stack's work       a spin of `ns` per frame (README.md:6:
+ *                                      ~4 Mpps a core, ~250 ns a frame), or a
+ *                                      fixed 50 us per burst
+ *   bsd_flush: cgck_tx_post()
+ *
+ * The reference row runs the same loop with the reference's own in_cksum /
+ * udp_cksum (oracle/_ref/libref_cksum.so, subr.c:186-223) called in place.
+ * The synchronous row opens the RX window with cgck_rx_begin and flushes with
+ * cgck_tx_flush in the same iteration.  Per (mix, budget, burst, form) one
+ * JSON line: the worker thread's microseconds in the checksum path per
+ * iteration (everything but the spin), the part of it spent waiting for the
+ * GPU (RX window open + TX completion), and the post-to-verdict latency of a
+ * burst (its post to the end of its window: one loop period, or the GPU's
+ * time when that is longer).  Each run checks itself: every window flags
+ * exactly the frames it corrupted, and sampled replies carry the reference's
+ * checksums.
+ *
+ * "lone" rows: one burst posted and, nothing arriving after it, drained at
+ * once by the next iteration (the drain rule, include/cgck.h): the latency
+ * from its post to its window's end.
+ *
+ *   tools/txloop [seconds per cell, default 0.2]
+ *   TXLOOP_LEN=64  TXLOOP_BURSTS=1,2,4,8,16,32,64,256,2048  TXLOOP_NS=0,250
+ */
+#include <dlfcn.h>
+#include <libgen.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/mman.h>
+#include <time.h>
+#include <unistd.h>
+
+#include "cgck.h"
+
+#define SLOT 2048
+#define L3 14
+#define MAXB 2048
+#define MAXIT 200000
+
+typedef uint16_t (*in_fn)(void *, int);
+typedef uint16_t (*udp_fn)(struct ip *, int);
+
+static double now(void)
+{
+	struct timespec ts;
+	clock_gettime(CLOCK_MONOTONIC, &ts);
+	return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+
+static int cmpd(const void *a, const void *b)
+{
+	const double x = *(const double *)a, y = *(const double *)b;
+	return x < y ? -1 : x > y;
+}
+
+/* sorts t; the p-th percentile */
+static double pct(double *t, int n, int p)
+{
+	if (n <= 0)
+		return 0;
+	qsort(t, n, sizeof(double), cmpd);
+	return t[(long)n * p / 100 < n ? (long)n * p / 100 : n - 1];
+}
+
+static void spin(double sec)
+{
+	for (const double s0 = now(); now() - s0 < sec;)
+		;
+}
+
+static void make_packet(uint8_t *ip, int len, uint64_t *s)
+{
+	for (int i = 0; i < len; i++) {
+		*s ^= *s << 13;
+		*s ^= *s >> 7;
+		*s ^= *s << 17;
+		ip[i] = (uint8_t)*s;
+	}
+	ip[0] = 0x45;
+	ip[1] = 0;
+	ip[2] = (uint8_t)(len >> 8);
+	ip[3] = (uint8_t)len;
+	ip[9] = 6;
+	ip[10] = ip[11] = 0;
+	ip[36] = ip[37] = 0;
+}
+
+/* the stack's verify of one received TCP/IPv4 frame (ip_input.c:45-58,
+ * tcp_input.c:75-85, fields restored as gbtcp/inet.c does): bad checks */
+static inline int verify(uint8_t *ip, int len, in_fn fin, udp_fn fudp)
+{
+	uint16_t saved, v;
+	int bad = 0;
+	memcpy(&saved, ip + 10, 2);
+	ip[10] = ip[11] = 0;
+	v = fin(ip, 20);
+	bad += v != saved;
+	memcpy(ip + 10, &saved, 2);
+	memcpy(&saved, ip + 36, 2);
+	ip[36] = ip[37] = 0;
+	v = fudp((struct ip *)ip, len - 20);
+	bad += v != saved;
+	memcpy(ip + 36, &saved, 2);
+	return bad;
+}
+
+/* tcp_respond(NULL, ip, th, ...) into a transmit slot (tcp_subr.c:93-123):
+ * the template from the received header, the two checksum calls */
+static inline void reply(uint8_t *tx, const uint8_t *rx, in_fn fin, udp_fn fudp)
+{
+	uint16_t v;
+	memcpy(tx, rx, 40);
+	tx[2] = 0;
+	tx[3] = 40;
+	memcpy(tx + 12, rx + 16, 4);
+	memcpy(tx + 16, rx + 12, 4);
+	memcpy(tx + 20, rx + 22, 2);
+	memcpy(tx + 22, rx + 20, 2);
+	tx[32] = 0x50;
+	tx[33] = 0x14; /* RST | ACK */
+	tx[36] = tx[37] = 0;
+	v = fudp((struct ip *)tx, 20);
+	memcpy(tx + 36, &v, 2);
+	tx[10] = tx[11] = 0;
+	v = fin(tx, 20);
+	memcpy(tx + 10, &v, 2);
+}
+
+struct cell {
+	double *worker, *wait, *lat;
+	int it, bad_rx, bad_tx_checked, bad_tx;
+};
+
+static in_fn ref_in;
+static udp_fn ref_udp;
+
+/* replies of slots [0, R) checked against the reference's values */
+static int check_replies(const uint8_t *txh, int R)
+{
+	int bad = 0;
+	const int idx[3] = {0, R / 2, R - 1};
+	for (int j = 0; j < 3; j++) {
+		uint8_t c[64];
+		memcpy(c, txh + (size_t)idx[j] * SLOT + L3, 40);
+		uint16_t s_ip, s_tcp, v;
+		memcpy(&s_ip, c + 10, 2);
+		memcpy(&s_tcp, c + 36, 2);
+		c[36] = c[37] = 0;
+		v = ref_udp((struct ip *)c, 20);
+		bad += v != s_tcp;
+		memcpy(c + 36, &v, 2);
+		c[10] = c[11] = 0;
+		bad += ref_in(c, 20) != s_ip;
+	}
+	return bad;
+}
+
+int main(int argc, char **argv)
+{
+	const double budget = argc > 1 ? atof(argv[1]) : 0.2;
+	const int len = getenv("TXLOOP_LEN") ? atoi(getenv("TXLOOP_LEN")) : 64;
+	int bursts[16] = {1, 2, 4, 8, 16, 32, 64, 256, 2048}, nb = 9;
+	double nsl[8] = {0, 250};
+	int nns = 2;
+	if (getenv("TXLOOP_BURSTS")) {
+		nb = 0;
+		for (char *e = getenv("TXLOOP_BURSTS"); *e && nb < 16;) {
+			const int v = (int)strtol(e, &e, 10);
+			if (v >= 1 && v <= MAXB)
+				bursts[nb++] = v;
+			while (*e == ',')
+				e++;
+		}
+	}
+	if (getenv("TXLOOP_NS")) {
+		nns = 0;
+		for (char *e = getenv("TXLOOP_NS"); *e && nns < 7;) {
+			nsl[nns++] = strtod(e, &e);
+			while (*e == ',')
+				e++;
+		}
+	}
+	if (len < 40 || len > 1500)
+		return 2;
+	{
+		char exe[4096];
+		const ssize_t k = readlink("/proc/self/exe", exe, sizeof(exe) - 64);
+		if (k > 0) {
+			exe[k] = 0;
+			char path[4200];
+			snprintf(path, sizeof(path), "%s/../oracle/_ref/libref_cksum.so", dirname(exe));
+			void *h = dlopen(path, RTLD_NOW | RTLD_LOCAL);
+			if (h) {
+				ref_in = (in_fn)dlsym(h, "in_cksum");
+				ref_udp = (udp_fn)dlsym(h, "udp_cksum");
+			}
+		}
+	}
+	if (!ref_in || !ref_udp) {
+		fprintf(stderr, "txloop: oracle/_ref/libref_cksum.so not found (make -C oracle ref)\n");
+		return 1;
+	}
+	/* one pool, as a netmap pool holds both rings: two receive halves
+	 * (bursts k and k - 1), two transmit halves (fills k and k - 1) */
+	const size_t half = (size_t)MAXB * SLOT, pool_bytes = 4 * half;
+	uint8_t *pool = mmap(NULL, pool_bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+	cgck_desc_t *desc = malloc(sizeof(cgck_desc_t) * MAXB);
+	uint32_t *out = malloc(4 * MAXB);
+	struct cell c;
+	c.worker = malloc(sizeof(double) * MAXIT);
+	c.wait = malloc(sizeof(double) * MAXIT);
+	c.lat = malloc(sizeof(double) * MAXIT);
+	double *tpost = malloc(sizeof(double) * (MAXIT + 64));
+	if (pool == MAP_FAILED || !desc || !out || !c.worker || !c.wait || !c.lat || !tpost) {
+		fprintf(stderr, "txloop: out of memory\n");
+		return 1;
+	}
+	uint8_t *rxh[2] = {pool, pool + half}, *txh[2] = {pool + 2 * half, pool + 3 * half};
+	uint64_t s = 0x9E3779B97F4A7C15ull;
+	for (int i = 0; i < MAXB; i++) {
+		make_packet(rxh[0] + (size_t)i * SLOT + L3, len, &s);
+		desc[i].frame_off = (uint64_t)i * SLOT;
+		desc[i].l3_off = L3;
+		desc[i].ip_len = (uint16_t)len;
+	}
+	for (int i = 0; i < MAXB; i++) { /* the sender's fill (reference functions) */
+		uint8_t *ip = rxh[0] + (size_t)i * SLOT + L3;
+		uint16_t v = ref_udp((struct ip *)ip, len - 20);
+		memcpy(ip + 36, &v, 2);
+		v = ref_in(ip, 20);
+		memcpy(ip + 10, &v, 2);
+	}
+	for (int i = 0; i < MAXB; i += 64) /* every 64th frame corrupted */
+		rxh[0][(size_t)i * SLOT + L3 + len - 1] ^= 0x5A;
+	memcpy(rxh[1], rxh[0], half);
+	if (cgck_host_register(pool, pool_bytes) || cgck_burst_open(NULL, MAXB, (size_t)MAXB * 1536, 0)) {
+		fprintf(stderr, "txloop: setup failed: %s\n", cgck_last_error());
+		return 1;
+	}
+	in_fn lib_in = (in_fn)in_cksum;
+	udp_fn lib_udp = (udp_fn)udp_cksum;
+	static const char *forms[3] = {"reference", "pipelined", "sync"};
+	for (int mix = 0; mix < 2; mix++) {
+		for (int bud = 0; bud <= nns; bud++) {
+			const double ns = bud < nns ? nsl[bud] : 0, fixed_us = bud < nns ? 0 : 50;
+			for (int bi = 0; bi < nb; bi++) {
+				const int R = bursts[bi];
+				const double other = (R * ns + fixed_us * 1000) * 1e-9;
+				const int expect = (R + 63) / 64;
+				for (int form = 0; form < 3; form++) {
+					c.it = c.bad_rx = c.bad_tx = c.bad_tx_checked = 0;
+					int k = 0;
+					const double t0 = now();
+					while (c.it < MAXIT && now() - t0 < budget) {
+						const int rec = k >= 20;
+						double a = now(), w = 0, lat = 0;
+						int bad = 0;
+						uint8_t *tx = txh[k & 1];
+						if (form == 0) {
+							uint8_t *rx = rxh[k & 1];
+							for (int i = 0; i < R; i++) {
+								uint8_t *ip = rx + (size_t)i * SLOT + L3;
+								bad += verify(ip, len, ref_in, ref_udp);
+								if (mix)
+									reply(tx + (size_t)i * SLOT + L3, ip, ref_in, ref_udp);
+							}
+							lat = now() - a;
+						} else if (form == 1) {
+							double w0 = now();
+							const int done = cgck_tx_complete(); /* fill k - 1 */
+							w += now() - w0;
+							if (done < 0)
+								goto fail;
+							if (mix && k > 0 && done == 2 * R) {
+								c.bad_tx += check_replies(txh[(k + 1) & 1], R);
+								c.bad_tx_checked++;
+							}
+							cgck_tx_begin();
+							tpost[k] = now();
+							if (cgck_rx_post(rxh[k & 1], 2 * half, desc, R) != R)
+								goto fail;
+							if (k > 0) {
+								uint8_t *rx = rxh[(k + 1) & 1];
+								w0 = now();
+								if (cgck_rx_begin_posted() != R)
+									goto fail;
+								w += now() - w0;
+								for (int i = 0; i < R; i++) {
+									uint8_t *ip = rx + (size_t)i * SLOT + L3;
+									bad += verify(ip, len, lib_in, lib_udp);
+									if (mix)
+										reply(tx + (size_t)i * SLOT + L3, ip, lib_in, lib_udp);
+								}
+								if (cgck_rx_end() != 2 * R)
+									goto fail;
+								lat = now() - tpost[k - 1];
+							} else {
+								bad = expect;
+							}
+						} else {
+							uint8_t *rx = rxh[k & 1];
+							cgck_tx_begin();
+							double w0 = now();
+							if (cgck_rx_begin(rx, 2 * half, desc, R) != R)
+								goto fail;
+							w += now() - w0;
+							for (int i = 0; i < R; i++) {
+								uint8_t *ip = rx + (size_t)i * SLOT + L3;
+								bad += verify(ip, len, lib_in, lib_udp);
+								if (mix)
+									reply(tx + (size_t)i * SLOT + L3, ip, lib_in, lib_udp);
+							}
+							if (cgck_rx_end() != 2 * R)
+								goto fail;
+							lat = now() - a;
+						}
+						const double a_spin = now();
+						spin(other);
+						const double spun = now() - a_spin;
+						if (form == 1) {
+							if (cgck_tx_post() < 0)
+								goto fail;
+						} else if (form == 2) {
+							const double w0 = now();
+							if (cgck_tx_flush() != (mix ? 2 * R : 0))
+								goto fail;
+							w += now() - w0;
+							if (mix) {
+								c.bad_tx += check_replies(tx, R);
+								c.bad_tx_checked++;
+							}
+						}
+						c.bad_rx += bad != expect;
+						if (rec) {
+							c.worker[c.it] = now() - a - spun;
+							c.wait[c.it] = w;
+							c.lat[c.it] = lat;
+							c.it++;
+						}
+						k++;
+					}
+					if (form == 1) { /* drain: the last burst and fill */
+						if (cgck_rx_begin_posted() >= 0)
+							cgck_rx_end();
+						cgck_tx_post();
+						cgck_tx_complete();
+						cgck_tx_complete();
+					}
+					const int n = c.it;
+					const double wm = pct(c.worker, n, 50) * 1e6, w90 = pct(c.worker, n, 90) * 1e6;
+					const double wt = pct(c.wait, n, 50) * 1e6;
+					const double lm = pct(c.lat, n, 50) * 1e6, l90 = pct(c.lat, n, 90) * 1e6;
+					printf("{\"mode\": \"loop\", \"form\": \"%s\", \"mix\": \"%s\", \"pkt_len\": %d, "
+					       "\"burst\": %d, \"stack_ns_per_frame\": %.0f, \"stack_us_fixed\": %.0f, "
+					       "\"iters\": %d, \"us_worker\": %.3f, \"us_worker_p90\": %.3f, \"us_wait\": %.3f, "
+					       "\"us_latency\": %.3f, \"us_latency_p90\": %.3f, \"exact\": %s}\n",
+					       forms[form], mix ? "rx+reply" : "rx", len, R, ns, fixed_us, n, wm, w90, wt, lm,
+					       l90, c.bad_rx == 0 && c.bad_tx == 0 ? "true" : "false");
+					fflush(stdout);
+				}
+			}
+		}
+	}
+	/* the drain rule alone: one burst, nothing after it */
+	for (int bi = 0; bi < nb; bi++) {
+		const int R = bursts[bi];
+		int n = 0, bad = 0;
+		const double t0 = now();
+		while (n < MAXIT && now() - t0 < budget) {
+			const double a = now();
+			if (cgck_rx_post(rxh[0], 2 * half, desc, R) != R || cgck_rx_pending() != 1)
+				goto fail;
+			if (cgck_rx_begin_posted() != R) /* the next iteration: nothing arrived, drain */
+				goto fail;
+			int b = 0;
+			for (int i = 0; i < R; i++)
+				b += verify(rxh[0] + (size_t)i * SLOT + L3, len, lib_in, lib_udp);
+			if (cgck_rx_end() != 2 * R)
+				goto fail;
+			bad += b != (R + 63) / 64;
+			c.lat[n++] = now() - a;
+			spin(20e-6); /* a quiet spell */
+		}
+		const double lm = pct(c.lat, n, 50) * 1e6, l90 = pct(c.lat, n, 90) * 1e6;
+		printf("{\"mode\": \"lone\", \"pkt_len\": %d, \"burst\": %d, \"iters\": %d, \"us_latency\": %.3f, "
+		       "\"us_latency_p90\": %.3f, \"exact\": %s}\n",
+		       len, R, n, lm, l90, bad == 0 ? "true" : "false");
+		fflush(stdout);
+	}
+	cgck_burst_close(NULL);
+	cgck_host_unregister(pool);
+	cgck_thread_release();
+	return 0;
+fail:
+	fprintf(stderr, "txloop: %s\n", cgck_last_error());
+	return 1;
+}
