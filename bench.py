@@ -671,6 +671,8 @@ def roofline(n, size, ev_ms, kernel, traffic_key, extra_bytes=0, live=None):
         traffic, src = load_traffic(traffic_key, kernel), TRAFFIC_SOURCE
     return {"bound": "hbm", "achieved": ach / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
             "frac": ach / HBM_PEAK, "traffic": traffic, "kernel": kernel,
+            # the same launch in HBM bytes (PMC): what the memory system moved per second
+            "hbm_frac": traffic / (ev_ms * 1e-3) / HBM_PEAK if traffic else None,
             "algorithmic_bytes_per_launch": algo, "kernel_ms_hip_events": ev_ms,
             "traffic_over_algorithmic": traffic / algo if traffic else None, "traffic_source": src}
 
@@ -727,7 +729,10 @@ def main():
             cpu_r = cpu_rss(min(3.0, args.cpu_seconds))
     live = {}
     if dist.rank == 0 and dist.world == 1 and not args.no_pmc:
-        live = pmc_traffic_live({k: res[k]["kernel"] for k in ("1500", "64", "imix") if k in res})
+        kern = {k: res[k]["kernel"] for k in ("1500", "64", "imix") if k in res}
+        if "imix" in res:
+            kern["ring"] = res["imix"]["ring"]["kernel"]
+        live = pmc_traffic_live(kern)
     dist.barrier()
 
     if dist.rank == 0:
@@ -769,6 +774,15 @@ def main():
                         "roofline_imix": roofline(n, 0, r["ev"], r["kernel"], "imix", r["bytes"] + 12 * n,
                                                   live=live),
                         "imix_without_layout_hint": r["unhinted"], "imix_ring": r["ring"]})
+            rg = r["ring"]
+            if live.get("ring"):
+                # ring slots cost whole lines: a frame at +14 reads 128 B for 64 B, 640 B for
+                # 576 B, 1536 B for 1500 B (1.174x the IMIX cycle), so the ring's HBM bytes are
+                # its PMC traffic, not the algorithmic bytes
+                rg["traffic"] = live["ring"]
+                rg["traffic_over_algorithmic"] = live["ring"] / (r["bytes"] + 16 * n)
+                rg["hbm_frac"] = live["ring"] / (rg["kernel_ms"] * 1e-3) / HBM_PEAK
+                rg["traffic_source"] = TRAFFIC_LIVE
         out["parity"] = parity
         if cpu:
             out["cpu_baseline"] = cpu

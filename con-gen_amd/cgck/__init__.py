@@ -69,7 +69,7 @@ EXPORTS = (
     "cgck_rx_begin", "cgck_rx_end", "cgck_window_stats", "cgck_ctx_last_kernel", "cgck_set_desc_layout",
     "cgck_ctx_set_kernel", "cgck_synth_imix_ring", "cgck_burst_request", "cgck_host_device_ptr",
     "cgck_rx_post", "cgck_rx_begin_posted", "cgck_tx_post", "cgck_tx_complete",
-    "cgck_rx_pending", "cgck_rx_ready",
+    "cgck_rx_pending", "cgck_rx_ready", "cgck_tx_pending", "cgck_tx_ready",
 )
 # Descriptor layout hint (cgck_set_desc_layout)
 LAYOUT_ANY = 0
@@ -294,6 +294,16 @@ def rx_ready():
     """cgck_rx_ready: 1 when the oldest posted burst's values are in, 0 while
     the GPU still computes it (no wait)."""
     return _check(load().cgck_rx_ready(), "cgck_rx_ready")
+
+
+def tx_pending():
+    """cgck_tx_pending: fills posted and not yet completed."""
+    return _check(load().cgck_tx_pending(), "cgck_tx_pending")
+
+
+def tx_ready():
+    """cgck_tx_ready: 1 when the oldest posted fill's values are in (no wait)."""
+    return _check(load().cgck_tx_ready(), "cgck_tx_ready")
 
 
 def window_stats():

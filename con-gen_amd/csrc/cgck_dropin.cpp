@@ -107,27 +107,96 @@ struct TxEntry {
 	int16_t fo; // -1: IP header entry (field ip+10); else L4 field offset after the header
 };
 
-// One receive burst: its descriptors and the kernel's values and meta words
-// (kFlagRx), and, when it was left posted on the burst server, the request.
+// cgck_rx_begin's burst: its descriptors and the kernel's values and meta
+// words (kFlagRx).
 struct RxBurst {
 	const uint8_t *base = nullptr;
 	uint64_t n = 0;
 	std::vector<cgck_desc_t> d;
 	std::vector<uint32_t> o, m;
-	BurstPending pend{};
 };
 
-// One TX flush: the queued fields, the descriptors of the in-place batch (or
-// the staged copies' values), and the posted request (cgck_tx_post).
+// The posted (pipelined) windows keep a queue per thread and kind: receive
+// bursts (cgck_rx_post) and TX fills (cgck_tx_post), up to kPostQ each,
+// opened / completed oldest first.  At most one burst-server request per
+// queue is in flight; what is posted while it is in flight waits and goes
+// out with everything else posted meanwhile as ONE request once it is back.
+// So a loop posting small bursts faster than the GPU answers one (a busy
+// worker at a handful of frames per poll) pays one mailbox round trip per
+// GPU service time, not per burst, and never waits for the GPU while older
+// bursts are still to be processed; a lone burst goes out at once.
+constexpr unsigned kPostQ = 64;
+
+// One server request carrying the descriptors of one or more posted items.
+struct PostReq {
+	std::vector<cgck_desc_t> d;
+	std::vector<uint32_t> o, m; // values, meta words (RX)
+	BurstPending pend{};
+	unsigned items = 0; // posted items it carries, not yet consumed
+	bool done = false;  // o / m hold its values (or rc its failure)
+	int rc = 0;
+	char msg[192] = {0};
+};
+
+// One posted item: a receive burst or a TX fill.  Its n descriptors index
+// [base, base + bytes); `own`: no request (nothing to compute, or a staged
+// TX fill computed at its post into vals).
+struct PostItem {
+	const uint8_t *base = nullptr;
+	size_t bytes = 0;
+	uint32_t flags = 0;
+	uint64_t n = 0;
+	size_t pkt_bytes = 0; // 16-byte-rounded packet bytes (the server's caps)
+	uint32_t max_len = 0;
+	std::vector<cgck_desc_t> d;
+	std::vector<uint32_t> vals;
+	int req = -1;     // request slot, -1: not sent yet
+	uint32_t off = 0; // its first descriptor in the request
+	bool own = false;
+};
+
+struct PostQueue {
+	PostItem it[kPostQ];
+	PostReq rq[kPostQ]; // each carries >= 1 item: never more live than items
+	unsigned head = 0, count = 0, sent = 0; // oldest item; items posted; of them sent (oldest first)
+	unsigned rhead = 0, rcount = 0;
+	int inflight = -1; // the request in flight
+	bool meta = false; // requests return meta words (RX)
+
+	PostItem &at(unsigned k) { return it[(head + k) % kPostQ]; }
+	PostItem &oldest() { return it[head]; }
+	unsigned next_slot() const { return (head + count) % kPostQ; }
+	PostItem &push()
+	{
+		PostItem &x = it[next_slot()];
+		count++;
+		x.req = -1;
+		x.off = 0;
+		x.own = false;
+		x.n = 0;
+		x.pkt_bytes = 0;
+		x.max_len = 0;
+		return x;
+	}
+	bool done(const PostItem &x) const { return x.own || (x.req >= 0 && rq[x.req].done); }
+	int rc_of(const PostItem &x) const { return x.own ? 0 : rq[x.req].rc; }
+	const char *msg_of(const PostItem &x) const { return x.own ? "" : rq[x.req].msg; }
+	const uint32_t *values(const PostItem &x) const { return x.own ? x.vals.data() : rq[x.req].o.data() + x.off; }
+	const uint32_t *metas(const PostItem &x) const { return x.own ? nullptr : rq[x.req].m.data() + x.off; }
+	void send(cgck_ctx *c);
+	void pump(cgck_ctx *c, bool wait);
+	int settle(cgck_ctx *c, bool wait);
+	void pop();
+};
+
+// TX fill bookkeeping beside its PostItem (same slot): the queued fields,
+// and for each the value (descriptor) it takes.
 struct TxFill {
 	std::vector<TxEntry> q;
-	std::vector<cgck_desc_t> d;
-	std::vector<uint32_t> o, idx; // idx: the value (descriptor) of each queued entry
-	BurstPending pend{};
-	bool stored = false; // the kernel wrote the fields in place (CGCK_STORE): nothing left to write
-	bool fast = false;   // posted in the fast form: o[k] is descriptor k's values, hs its spans
-	bool icmp = false;   // holds ICMP messages (their L4 value without the pseudo-header)
-	int n = 0;           // the fields it stands for (q is empty in the fast form)
+	std::vector<uint32_t> idx; // entry i's value: values[idx[i]]
+	bool fast = false;  // fast form: descriptor k's values, hs[k] its spans
+	bool icmp = false;  // holds ICMP messages (their L4 value without the pseudo-header)
+	int n = 0;          // the fields it stands for (q is empty in the fast form)
 	std::vector<uint32_t> hs;
 	uint8_t *lo = nullptr;
 };
@@ -142,8 +211,9 @@ struct ThreadState {
 	bool tx_map = false;             // txidx built (the first call below tx_max)
 	PtrMap txidx; // (ip << 1 | is_l4) -> txq index
 	TxFill txs;       // cgck_tx_flush's batch
-	TxFill txp[2];    // posted fills (cgck_tx_post), oldest at txp_head
-	unsigned txp_head = 0, txp_count = 0;
+	PostItem txs_item;
+	PostQueue txpq;   // posted fills (cgck_tx_post)
+	TxFill txf[kPostQ]; // their bookkeeping, slot for slot
 	// The window in its fast form, while every call is at or above the
 	// highest header so far and inside one registered range (txd_ok): no
 	// txq entries, only one descriptor per packet, its header and segment
@@ -179,8 +249,7 @@ struct ThreadState {
 	bool rx_iv_built = false;
 	std::vector<std::pair<uintptr_t, uintptr_t>> rx_iv;
 	RxBurst rxs;      // cgck_rx_begin's burst
-	RxBurst rxp[2];   // posted bursts (cgck_rx_post), oldest at rxp_head
-	unsigned rxp_head = 0, rxp_count = 0;
+	PostQueue rxpq;   // posted bursts (cgck_rx_post)
 	uint64_t rx_served0 = 0; // stats[0] at rx_begin
 	uint64_t stats[4] = {0, 0, 0, 0};
 	// the registered range of the last TX-window hit, valid while g_reg_gen
@@ -651,39 +720,134 @@ namespace {
 
 constexpr uint32_t kRxFlags = CGCK_IP | CGCK_L4 | CGCK_ZERO_FIELDS | kFlagL4Auto | kFlagRx;
 
-// Fill a burst's descriptor copy and output arrays for n frames.
-void rx_fill(RxBurst &r, const void *base, const cgck_desc_t *desc, uint64_t n)
+// Send the items posted and not sent yet, oldest first, as one request: as
+// many as share the first one's range and flags and fit the burst server
+// (its max_pkts and max_bytes; without a server the request is a launch,
+// computed at once).  Items computed at their post are stepped over.
+void PostQueue::send(cgck_ctx *c)
 {
-	r.base = (const uint8_t *)base;
-	r.n = n;
-	r.d.assign(desc, desc + n);
-	r.o.resize(n ? n : 1);
-	r.m.resize(n ? n : 1);
+	while (sent < count && at(sent).own)
+		sent++;
+	if (sent == count)
+		return;
+	const PostItem &f = at(sent);
+	const uint64_t cap_n = c->bbox ? c->bmax : UINT64_MAX;
+	const size_t cap_b = c->bbox ? c->bmax_bytes : SIZE_MAX;
+	uint64_t n = 0;
+	size_t pb = 0;
+	uint32_t ml = 0;
+	unsigned k = sent;
+	for (; k < count; k++) {
+		const PostItem &x = at(k);
+		if (x.own || x.base != f.base || x.bytes != f.bytes || x.flags != f.flags)
+			break;
+		if (k > sent && (n + x.n > cap_n || pb + x.pkt_bytes > cap_b))
+			break;
+		n += x.n;
+		pb += x.pkt_bytes;
+		ml = x.max_len > ml ? x.max_len : ml;
+	}
+	const int ri = (int)((rhead + rcount) % kPostQ);
+	rcount++;
+	PostReq &r = rq[ri];
+	r.d.clear();
+	for (unsigned j = sent; j < k; j++) {
+		PostItem &x = at(j);
+		x.req = ri;
+		x.off = (uint32_t)r.d.size();
+		r.d.insert(r.d.end(), x.d.begin(), x.d.end());
+	}
+	r.o.resize(n);
+	if (meta)
+		r.m.resize(n);
+	r.items = k - sent;
+	r.done = false;
+	r.rc = 0;
+	r.msg[0] = 0;
+	sent = k;
+	const DescSummary sum = {ml, pb};
+	const int rc = desc_host_post(c, const_cast<uint8_t *>(f.base), f.bytes, r.d.data(), n, f.flags, r.o.data(),
+				      nullptr, meta ? r.m.data() : nullptr, &r.pend, &sum);
+	if (rc < 0) {
+		r.rc = rc;
+		snprintf(r.msg, sizeof(r.msg), "%s", err_text());
+		r.done = true;
+	} else if (rc == 1) {
+		inflight = ri;
+	} else {
+		r.done = true;
+	}
+}
+
+// Collect the request in flight once it is back (wait: wait for it), then
+// send what was posted meanwhile.
+void PostQueue::pump(cgck_ctx *c, bool wait)
+{
+	if (inflight >= 0) {
+		PostReq &r = rq[inflight];
+		if (!wait && !burst_ready(c, &r.pend))
+			return;
+		r.rc = r.pend.seq ? burst_collect(c, &r.pend) : r.pend.rc;
+		if (r.rc)
+			snprintf(r.msg, sizeof(r.msg), "%s", err_text());
+		r.done = true;
+		inflight = -1;
+	}
+	if (sent < count)
+		send(c);
+}
+
+// Are the oldest item's values in (1), or not yet (0)?  wait: until they are.
+int PostQueue::settle(cgck_ctx *c, bool wait)
+{
+	pump(c, false);
+	while (!done(oldest())) {
+		if (!wait)
+			return 0;
+		pump(c, true);
+	}
+	return 1;
+}
+
+// The oldest item consumed; requests all of whose items are consumed free.
+void PostQueue::pop()
+{
+	PostItem &x = oldest();
+	if (x.req >= 0)
+		rq[x.req].items--;
+	head = (head + 1) % kPostQ;
+	count--;
+	if (sent)
+		sent--;
+	while (rcount && rq[rhead].done && rq[rhead].items == 0) {
+		rhead = (rhead + 1) % kPostQ;
+		rcount--;
+	}
 }
 
 // Open the window over a computed burst; returns the frames it answers for.
-int rx_open_on(ThreadState &t, const RxBurst &r, bool posted)
+int rx_open_on(ThreadState &t, const uint8_t *base, uint64_t n, const cgck_desc_t *d, const uint32_t *o,
+	       const uint32_t *m, bool posted)
 {
-	uint64_t m = 0;
-	for (uint64_t i = 0; i < r.n; i++)
-		m += r.m[i] != 0;
-	t.rxd = r.d.data();
-	t.rxo = r.o.data();
-	t.rxm = r.m.data();
-	t.rx_base = r.base;
-	t.rx_n = r.n;
+	uint64_t k = 0;
+	for (uint64_t i = 0; i < n; i++)
+		k += m[i] != 0;
+	t.rxd = d;
+	t.rxo = o;
+	t.rxm = m;
+	t.rx_base = base;
+	t.rx_n = n;
 	t.rx_cur = 0;
 	t.rx_map = false;
 	t.rx_iv_built = false;
 	t.rx_open = true;
 	t.rx_posted = posted;
 	t.rx_served0 = t.stats[0];
-	return (int)m;
+	return (int)k;
 }
 
-int rx_check(ThreadState &t, const void *base, const cgck_desc_t *desc, uint64_t n, const char *who)
+int rx_check(const void *base, const cgck_desc_t *desc, uint64_t n, const char *who)
 {
-	(void)t;
 	if (n && (!base || !desc))
 		return set_err(-EINVAL, "%s: NULL base or descriptors", who);
 	if (n > 0xffffffffull / 2)
@@ -698,7 +862,7 @@ extern "C" int cgck_rx_begin(void *base, size_t bytes, const cgck_desc_t *desc, 
 	ThreadState &t = tstate();
 	if (t.rx_open)
 		return set_err(-EBUSY, "cgck_rx_begin: an RX window is already open on this thread");
-	int rc = rx_check(t, base, desc, n, "cgck_rx_begin");
+	int rc = rx_check(base, desc, n, "cgck_rx_begin");
 	if (rc)
 		return rc;
 	cgck_ctx *c = thread_ctx();
@@ -711,60 +875,78 @@ extern "C" int cgck_rx_begin(void *base, size_t bytes, const cgck_desc_t *desc, 
 	// drop rules of ip_input.c:28-44, 76, tcp_input.c:67, udp_usrreq.c:65,
 	// ip_icmp.c:177, gbtcp/inet.c:282-314), so no header is parsed here.
 	// desc_host checks every descriptor against [base, base + bytes).
-	rx_fill(t.rxs, base, desc, n);
-	if (n && (rc = desc_host(c, base, bytes, t.rxs.d.data(), n, kRxFlags, t.rxs.o.data(), nullptr,
-				 t.rxs.m.data()))) {
+	RxBurst &r = t.rxs;
+	r.base = (const uint8_t *)base;
+	r.n = n;
+	r.d.assign(desc, desc + n);
+	r.o.resize(n ? n : 1);
+	r.m.resize(n ? n : 1);
+	if (n && (rc = desc_host(c, base, bytes, r.d.data(), n, kRxFlags, r.o.data(), nullptr, r.m.data()))) {
 		char msg[256];
 		snprintf(msg, sizeof(msg), "%s", err_text());
 		return set_err(rc, "cgck_rx_begin: %s", msg);
 	}
-	return rx_open_on(t, t.rxs, false);
+	return rx_open_on(t, r.base, n, r.d.data(), r.o.data(), r.m.data(), false);
 }
 
 // Pipelined form: post burst k and return; the window over it opens at a
-// later cgck_rx_begin_posted, while the stack has worked on burst k - 1.
+// later cgck_rx_begin_posted, while the stack has worked on older bursts.
+// The descriptors are checked here, so a bad one fails its own post.
 extern "C" int cgck_rx_post(void *base, size_t bytes, const cgck_desc_t *desc, uint64_t n)
 {
 	ThreadState &t = tstate();
-	if (t.rxp_count == 2)
-		return set_err(-EBUSY, "cgck_rx_post: two bursts already posted and not yet opened");
-	int rc = rx_check(t, base, desc, n, "cgck_rx_post");
+	PostQueue &q = t.rxpq;
+	if (q.count == kPostQ)
+		return set_err(-EBUSY, "cgck_rx_post: %u bursts already posted and not yet opened", kPostQ);
+	int rc = rx_check(base, desc, n, "cgck_rx_post");
 	if (rc)
 		return rc;
 	cgck_ctx *c = thread_ctx();
 	if (!c)
 		return -ENODEV;
-	RxBurst &r = t.rxp[(t.rxp_head + t.rxp_count) & 1];
-	rx_fill(r, base, desc, n);
-	r.pend.seq = 0;
-	r.pend.rc = 0;
-	if (n && (rc = desc_host_post(c, base, bytes, r.d.data(), n, kRxFlags, r.o.data(), nullptr, r.m.data(),
-				      &r.pend)) < 0) {
-		char msg[256];
-		snprintf(msg, sizeof(msg), "%s", err_text());
-		return set_err(rc, "cgck_rx_post: %s", msg);
+	size_t pb = 0;
+	uint32_t ml = 0;
+	for (uint64_t i = 0; i < n; i++) {
+		const uint64_t end = desc[i].frame_off + desc[i].l3_off + desc[i].ip_len;
+		if (end > bytes || end < desc[i].frame_off)
+			return set_err(-EINVAL, "cgck_rx_post: descriptor %llu reaches past the %zu bytes given",
+				       (unsigned long long)i, bytes);
+		ml = desc[i].ip_len > ml ? desc[i].ip_len : ml;
+		pb += ((size_t)desc[i].ip_len + 15) & ~(size_t)15;
 	}
-	t.rxp_count++;
+	q.meta = true;
+	PostItem &x = q.push();
+	x.base = (const uint8_t *)base;
+	x.bytes = bytes;
+	x.flags = kRxFlags;
+	x.n = n;
+	x.d.assign(desc, desc + n);
+	x.pkt_bytes = pb;
+	x.max_len = ml;
+	x.own = n == 0;
+	x.vals.clear();
+	q.pump(c, false);
 	return (int)n;
 }
 
 extern "C" int cgck_rx_begin_posted(void)
 {
 	ThreadState &t = tstate();
+	PostQueue &q = t.rxpq;
 	if (t.rx_open)
 		return set_err(-EBUSY, "cgck_rx_begin_posted: an RX window is already open on this thread");
-	if (t.rxp_count == 0)
+	if (q.count == 0)
 		return set_err(-ENOENT, "cgck_rx_begin_posted: no burst posted");
-	RxBurst &r = t.rxp[t.rxp_head];
-	int rc = r.pend.seq ? burst_collect(t.ctx, &r.pend) : r.pend.rc;
-	if (rc) {
-		t.rxp_head ^= 1;
-		t.rxp_count--;
-		char msg[256];
-		snprintf(msg, sizeof(msg), "%s", err_text());
+	q.settle(t.ctx, true);
+	const PostItem &x = q.oldest();
+	if (const int rc = q.rc_of(x)) {
+		char msg[200];
+		snprintf(msg, sizeof(msg), "%s", q.msg_of(x));
+		q.pop();
 		return set_err(rc, "cgck_rx_begin_posted: %s", msg);
 	}
-	return rx_open_on(t, r, true);
+	static const uint32_t none = 0;
+	return rx_open_on(t, x.base, x.n, x.d.data(), x.n ? q.values(x) : &none, x.n ? q.metas(x) : &none, true);
 }
 
 // The drain rule's two questions (include/cgck.h): is a burst still posted,
@@ -772,16 +954,15 @@ extern "C" int cgck_rx_begin_posted(void)
 extern "C" int cgck_rx_pending(void)
 {
 	const ThreadState *t = t_st;
-	return t ? (int)t->rxp_count : 0;
+	return t ? (int)t->rxpq.count : 0;
 }
 
 extern "C" int cgck_rx_ready(void)
 {
-	const ThreadState *t = t_st;
-	if (!t || t->rxp_count == 0)
+	ThreadState *t = t_st;
+	if (!t || t->rxpq.count == 0)
 		return set_err(-ENOENT, "cgck_rx_ready: no burst posted");
-	const RxBurst &r = t->rxp[t->rxp_head];
-	return r.pend.seq ? burst_ready(t->ctx, &r.pend) : 1;
+	return t->rxpq.settle(t->ctx, false);
 }
 
 extern "C" int cgck_rx_end(void)
@@ -794,8 +975,7 @@ extern "C" int cgck_rx_end(void)
 	t.rx_map = false;
 	if (t.rx_posted) {
 		t.rx_posted = false;
-		t.rxp_head ^= 1;
-		t.rxp_count--;
+		t.rxpq.pop();
 	}
 	return (int)(t.stats[0] - t.rx_served0);
 }
@@ -836,32 +1016,21 @@ constexpr uint32_t kTxFlags = CGCK_IP | CGCK_L4 | CGCK_ZERO_FIELDS;
 // kFlagL4Auto and the group kernel is slower on small frames.
 inline uint32_t tx_flags(const TxFill &f) { return kTxFlags | (f.icmp ? kFlagL4Auto : 0u); }
 
-// Posted fills return values and the completion writes the fields on the
-// host (see cgck_tx_post); the lab build's $CGCK_TX_KSTORE has the kernel
-// store them instead (CGCK_STORE), for the A/B.
-inline bool tx_kstore()
-{
-	static const bool k = CGCK_ENV("CGCK_TX_KSTORE") != nullptr;
-	return k;
-}
-
-// Compute the values of f.q: when every entry lies in one registered range
-// (the transport's pool) the batch is described in place, as cgck_desc_host
-// of that range — the burst server when one is open on this context and the
-// flush fits it (left posted when pend is given: returns 1), else a launch;
+// Describe the entries of f.q for the kernel, into x.  When every entry lies
+// in one registered range (the transport's pool) the batch is described in
+// place, as cgck_desc_host of that range (returns 1: x is to be computed);
 // otherwise each region is staged 16-byte aligned in pinned memory and
-// launched (computed at once: 0).  f.idx[i] is entry i's value in f.o.
-int tx_compute(cgck_ctx *c, TxFill &f, bool post)
+// computed at once into x.vals (returns 0).  f.idx[i] is entry i's value.
+int tx_build(cgck_ctx *c, TxFill &f, PostItem &x)
 {
 	const std::vector<TxEntry> &q = f.q;
 	const uint64_t n = q.size();
-	const uint32_t flags = tx_flags(f);
+	x.flags = tx_flags(f);
 	HIP_TRY(hipSetDevice(c->device));
 	RegRange reg{nullptr, nullptr, nullptr};
 	bool inplace = reg_find(q[0].ip, q[0].span, &reg);
 	for (uint64_t i = 1; inplace && i < n; i++)
 		inplace = q[i].ip >= reg.lo && q[i].ip + q[i].span <= reg.hi;
-	int rc;
 	// One descriptor per packet: a packet's header entry and its segment
 	// entry (queued one after the other by the finalisers, ip_output.c:61-64
 	// after tcp_output.c:416-418) share it — it covers the segment, and the
@@ -869,41 +1038,35 @@ int tx_compute(cgck_ctx *c, TxFill &f, bool post)
 	// the queue checked equals the header call's length) and the segment's
 	// L4 checksum from one read of the frame.
 	f.idx.resize(n);
-	f.stored = false;
 	if (inplace) {
-		f.d.resize(n);
+		x.d.resize(n);
 		uint64_t m = 0;
-		bool l4_alone = false; // a packet with its segment queued but not its header
 		for (uint64_t i = 0; i < n; i++) {
 			if (i > 0 && q[i].ip == q[i - 1].ip && (q[i].fo < 0) != (q[i - 1].fo < 0) && f.idx[i - 1] == m - 1 &&
 			    (i < 2 || f.idx[i - 2] != m - 1)) {
 				f.idx[i] = (uint32_t)(m - 1);
-				if (q[i].span > f.d[m - 1].ip_len)
-					f.d[m - 1].ip_len = (uint16_t)q[i].span;
+				if (q[i].span > x.d[m - 1].ip_len)
+					x.d[m - 1].ip_len = (uint16_t)q[i].span;
 				continue;
 			}
-			if (q[i].fo >= 0 && !(i + 1 < n && q[i + 1].ip == q[i].ip && q[i + 1].fo < 0))
-				l4_alone = true;
 			f.idx[i] = (uint32_t)m;
-			f.d[m].frame_off = (uint64_t)(q[i].ip - reg.lo);
-			f.d[m].l3_off = 0;
-			f.d[m].ip_len = (uint16_t)q[i].span;
+			x.d[m].frame_off = (uint64_t)(q[i].ip - reg.lo);
+			x.d[m].l3_off = 0;
+			x.d[m].ip_len = (uint16_t)q[i].span;
 			m++;
 		}
-		f.o.resize(m);
-		if (post) {
-			// Posted: completing the fill writes the fields from the values
-			// (tx_write).  Lab ($CGCK_TX_KSTORE): when every packet's header
-			// is queued (alone, or with its segment), the kernel stores them
-			// (CGCK_STORE: ip+10, and the L4 field of a descriptor that
-			// covers the segment; a header-only descriptor covers
-			// ip_hl * 4 bytes, so no L4 field fits in it and none is stored).
-			f.stored = tx_kstore() && !l4_alone;
-			return desc_host_post(c, reg.lo, (size_t)(reg.hi - reg.lo), f.d.data(), m,
-					      flags | (f.stored ? CGCK_STORE : 0u), f.stored ? nullptr : f.o.data(), nullptr,
-					      nullptr, &f.pend);
+		x.d.resize(m);
+		x.base = reg.lo;
+		x.bytes = (size_t)(reg.hi - reg.lo);
+		x.n = m;
+		x.pkt_bytes = 0;
+		x.max_len = 0;
+		for (const cgck_desc_t &e : x.d) {
+			x.pkt_bytes += ((size_t)e.ip_len + 15) & ~(size_t)15;
+			x.max_len = e.ip_len > x.max_len ? e.ip_len : x.max_len;
 		}
-		return desc_host(c, reg.lo, (size_t)(reg.hi - reg.lo), f.d.data(), m, flags, f.o.data(), nullptr);
+		x.own = false;
+		return 1;
 	}
 	for (uint64_t i = 0; i < n; i++)
 		f.idx[i] = (uint32_t)i;
@@ -912,6 +1075,7 @@ int tx_compute(cgck_ctx *c, TxFill &f, bool post)
 		bytes += (e.span + 15) & ~(size_t)15;
 	const size_t d_off = (bytes + 15) & ~(size_t)15;
 	const size_t o_off = (d_off + 12 * n + 15) & ~(size_t)15;
+	int rc;
 	if ((rc = grow_host((void **)&c->h_stage, &c->h_stage_cap, o_off + 4 * n)))
 		return rc;
 	uint8_t *h = c->h_stage;
@@ -925,23 +1089,26 @@ int tx_compute(cgck_ctx *c, TxFill &f, bool post)
 		d[i].ip_len = (uint16_t)q[i].span;
 		at += (q[i].span + 15) & ~(size_t)15;
 	}
-	KParams p = {h, d, n, 0, 0, 0, flags, o, nullptr, nullptr, 0, nullptr};
+	KParams p = {h, d, n, 0, 0, 0, x.flags, o, nullptr, nullptr, 0, nullptr};
 	if ((rc = run(c, p, 1500, c->stream)))
 		return rc;
 	HIP_TRY(hipStreamSynchronize(c->stream));
-	f.o.assign(o, o + n);
+	x.vals.assign(o, o + n);
+	x.d.clear();
+	x.n = 0;
+	x.own = true;
 	return 0;
 }
 
 // Write every queued field from the computed values; returns their count.
-int tx_write(TxFill &f)
+int tx_write(TxFill &f, const uint32_t *vals)
 {
 	const std::vector<TxEntry> &q = f.q;
 	const uint64_t n = q.size();
 	for (uint64_t i = 0; i < n; i++) {
 		uint16_t v;
 		uint8_t *dst;
-		const uint32_t r = f.o[f.idx[i]];
+		const uint32_t r = vals[f.idx[i]];
 		if (q[i].fo < 0) {
 			v = (uint16_t)r;
 			dst = q[i].ip + 10;
@@ -955,16 +1122,15 @@ int tx_write(TxFill &f)
 	return (int)n;
 }
 
-// The fields of a fill posted in the fast form, from descriptor k's values:
-// its header's (ip+10) when the header was queued, its segment's when the
-// segment was (at ip_hl * 4 + 16 for TCP, + 6 for UDP, read from the packet
-// as the call read them).
-int tx_write_fast(TxFill &f)
+// The fields of a fill in the fast form, from descriptor k's values: its
+// header's (ip+10) when the header was queued, its segment's when the
+// segment was (at ip_hl * 4 + 16 for TCP, + 6 for UDP, + 2 for ICMP, read
+// from the packet as the call read them).
+int tx_write_fast(const TxFill &f, const PostItem &x, const uint32_t *vals)
 {
-	const size_t m = f.d.size();
-	for (size_t k = 0; k < m; k++) {
-		uint8_t *ip = f.lo + f.d[k].frame_off;
-		const uint32_t r = f.o[k], hs = f.hs[k];
+	for (size_t k = 0; k < x.n; k++) {
+		uint8_t *ip = f.lo + x.d[k].frame_off;
+		const uint32_t r = vals[k], hs = f.hs[k];
 		if (hs & 0xffff) {
 			const uint16_t v = (uint16_t)(r >> 16);
 			memcpy(ip + (ip[0] & 15) * 4 + l4_fo(ip), &v, 2);
@@ -977,14 +1143,39 @@ int tx_write_fast(TxFill &f)
 	return f.n;
 }
 
-// Close the window and move its queue into f.
-void tx_take(ThreadState &t, TxFill &f)
+// Close the window into f and x: the fast form's descriptors as they are
+// (every packet's header among them), else the entry queue (returns 1), or
+// nothing queued (0).
+int tx_take(ThreadState &t, TxFill &f, PostItem &x)
 {
+	txd_close(t);
+	const bool fast = t.txd_ok && t.txd_noip == 0 && !t.txd_fast.empty();
+	if (t.txd_ok && !fast)
+		txd_spill(t);
 	t.tx_open = false;
 	t.tx_map = false;
 	f.icmp = t.tx_icmp;
+	f.fast = fast;
 	f.q.swap(t.txq);
 	t.txq.clear();
+	x.own = false;
+	x.vals.clear();
+	if (fast) {
+		x.d.swap(t.txd_fast);
+		f.hs.swap(t.txd_hs);
+		f.lo = const_cast<uint8_t *>(t.txd_lo);
+		f.n = (int)t.txd_calls;
+		x.base = t.txd_lo;
+		x.bytes = (size_t)(t.txd_hi - t.txd_lo);
+		x.n = x.d.size();
+		x.pkt_bytes = t.txd_bytes;
+		x.max_len = t.txd_max;
+		x.flags = tx_flags(f);
+		return 1;
+	}
+	f.n = (int)f.q.size();
+	x.n = 0;
+	return f.n ? 1 : 0;
 }
 
 } // namespace
@@ -994,56 +1185,45 @@ extern "C" int cgck_tx_flush(void)
 	ThreadState &t = tstate();
 	if (!t.tx_open)
 		return set_err(-EINVAL, "cgck_tx_flush: no open window on this thread");
-	txd_close(t);
-	if (t.txd_ok && t.txd_noip == 0 && !t.txd_fast.empty()) {
-		// the fast form: its descriptors as they are, the fields written from
-		// the values (as cgck_tx_post + cgck_tx_complete, waited for at once)
-		TxFill &f = t.txs;
-		tx_take(t, f);
-		cgck_ctx *c = thread_ctx();
-		if (!c)
-			return -ENODEV;
-		f.d.swap(t.txd_fast);
-		f.hs.swap(t.txd_hs);
-		f.lo = const_cast<uint8_t *>(t.txd_lo);
-		f.n = (int)t.txd_calls;
-		f.o.resize(f.d.size());
-		const DescSummary sum = {t.txd_max, t.txd_bytes};
-		int rc = desc_host_post(c, (void *)t.txd_lo, (size_t)(t.txd_hi - t.txd_lo), f.d.data(), f.d.size(),
-					tx_flags(f), f.o.data(), nullptr, nullptr, &f.pend, &sum);
-		if (rc >= 0)
-			rc = f.pend.seq ? burst_collect(c, &f.pend) : f.pend.rc;
-		f.q.clear();
-		return rc < 0 ? rc : tx_write_fast(f);
-	}
-	if (t.txd_ok)
-		txd_spill(t);
-	tx_take(t, t.txs);
-	if (t.txs.q.empty())
+	TxFill &f = t.txs;
+	PostItem &x = t.txs_item;
+	if (!tx_take(t, f, x))
 		return 0;
 	cgck_ctx *c = thread_ctx();
 	if (!c)
 		return -ENODEV;
-	int rc = tx_compute(c, t.txs, false);
+	int rc = f.fast ? 1 : tx_build(c, f, x);
+	if (rc == 1) {
+		// in place: one request (or launch) over the pool, waited for here
+		x.vals.resize(x.n);
+		BurstPending pend{};
+		const DescSummary sum = {x.max_len, x.pkt_bytes};
+		rc = desc_host_post(c, const_cast<uint8_t *>(x.base), x.bytes, x.d.data(), x.n, x.flags, x.vals.data(),
+				    nullptr, nullptr, &pend, &sum);
+		if (rc >= 0)
+			rc = pend.seq ? burst_collect(c, &pend) : pend.rc;
+	}
 	if (rc < 0) {
-		t.txs.q.clear();
+		f.q.clear();
 		return rc;
 	}
-	return tx_write(t.txs);
+	return f.fast ? tx_write_fast(f, x, x.vals.data()) : tx_write(f, x.vals.data());
 }
 
 // Pipelined form: post the window's fill and return; cgck_tx_complete
 // (before the transport hands these slots to the NIC) waits for it and
-// writes the fields.
+// writes the fields.  Fills posted while an earlier one is still on the
+// GPU go out together once it is back (PostQueue).
 extern "C" int cgck_tx_post(void)
 {
 	ThreadState &t = tstate();
 	if (!t.tx_open)
 		return set_err(-EINVAL, "cgck_tx_post: no open window on this thread");
-	if (t.txp_count == 2) {
-		// A third fill: the oldest completes first (its fields are written
-		// now, before the kick that was to wait for them — final values
-		// either way), so no queued field is dropped.
+	PostQueue &q = t.txpq;
+	if (q.count == kPostQ) {
+		// The queue is full: the oldest fill completes first (its fields
+		// are written now, before the kick that was to wait for them —
+		// final values either way), so no queued field is dropped.
 		const int rc = cgck_tx_complete();
 		if (rc < 0) {
 			t.tx_open = false;
@@ -1053,75 +1233,57 @@ extern "C" int cgck_tx_post(void)
 			return set_err(rc, "cgck_tx_post: completing the oldest fill: %s", msg);
 		}
 	}
-	TxFill &f = t.txp[(t.txp_head + t.txp_count) & 1];
-	txd_close(t);
-	// the descriptors built as the calls came, when every packet's header is
-	// among them: the kernel stores every field (CGCK_STORE)
-	const bool fast = t.txd_ok && t.txd_noip == 0 && !t.txd_fast.empty();
-	if (t.txd_ok && !fast)
-		txd_spill(t);
-	const int n = fast ? (int)t.txd_calls : (int)t.txq.size();
-	tx_take(t, f);
-	f.pend.seq = 0;
-	f.pend.rc = 0;
-	f.n = n;
-	f.fast = false;
-	if (n) {
-		cgck_ctx *c = thread_ctx();
-		if (!c)
-			return -ENODEV;
-		int rc;
-		if (fast) {
-			// The kernel returns each descriptor's two values and the
-			// completion writes the fields (tx_write_fast): a ring line
-			// the GPU stores into leaves the worker's caches, so the stack's
-			// next writes to that slot miss (kernel
-			// stores 3.9 against 3.7 us at 256 x 64 B, and 27-55 against 25
-			// at 2048).
-			const bool kstore = tx_kstore();
-			f.d.swap(t.txd_fast);
-			f.hs.swap(t.txd_hs);
-			f.lo = const_cast<uint8_t *>(t.txd_lo);
-			f.stored = kstore;
-			f.fast = !kstore;
-			if (f.fast)
-				f.o.resize(f.d.size());
-			const DescSummary sum = {t.txd_max, t.txd_bytes};
-			rc = desc_host_post(c, (void *)t.txd_lo, (size_t)(t.txd_hi - t.txd_lo), f.d.data(), f.d.size(),
-					    tx_flags(f) | (kstore ? CGCK_STORE : 0u), kstore ? nullptr : f.o.data(), nullptr, nullptr,
-					    &f.pend, &sum);
-		} else {
-			rc = tx_compute(c, f, true);
-		}
-		if (rc < 0) {
-			f.q.clear();
-			return rc;
-		}
+	cgck_ctx *c = thread_ctx();
+	if (!c)
+		return -ENODEV;
+	TxFill &f = t.txf[q.next_slot()];
+	PostItem &x = q.push();
+	int rc = tx_take(t, f, x);
+	if (rc == 0) {
+		x.own = true; // nothing queued: complete as it stands
+	} else if (!f.fast && (rc = tx_build(c, f, x)) < 0) {
+		// computed at once and failed: the fill leaves the queue unwritten
+		q.count--;
+		f.q.clear();
+		return rc;
 	}
-	t.txp_count++;
-	return n;
+	q.pump(c, false);
+	return f.n;
 }
 
 extern "C" int cgck_tx_complete(void)
 {
 	ThreadState &t = tstate();
-	if (t.txp_count == 0)
+	PostQueue &q = t.txpq;
+	if (q.count == 0)
 		return 0;
-	TxFill &f = t.txp[t.txp_head];
-	t.txp_head ^= 1;
-	t.txp_count--;
-	const int rc = f.pend.seq ? burst_collect(t.ctx, &f.pend) : f.pend.rc;
-	if (rc < 0) {
+	q.settle(t.ctx, true);
+	const PostItem &x = q.oldest();
+	TxFill &f = t.txf[q.head];
+	if (const int rc = q.rc_of(x)) {
+		char msg[200];
+		snprintf(msg, sizeof(msg), "%s", q.msg_of(x));
 		f.q.clear();
-		return rc;
+		q.pop();
+		return set_err(rc, "cgck_tx_complete: %s", msg);
 	}
-	if (f.stored) { // the kernel wrote them
-		f.q.clear();
-		return f.n;
-	}
-	if (f.fast)
-		return tx_write_fast(f);
-	return tx_write(f);
+	const int n = f.n == 0 ? 0 : f.fast ? tx_write_fast(f, x, q.values(x)) : tx_write(f, q.values(x));
+	q.pop();
+	return n;
+}
+
+extern "C" int cgck_tx_pending(void)
+{
+	const ThreadState *t = t_st;
+	return t ? (int)t->txpq.count : 0;
+}
+
+extern "C" int cgck_tx_ready(void)
+{
+	ThreadState *t = t_st;
+	if (!t || t->txpq.count == 0)
+		return set_err(-ENOENT, "cgck_tx_ready: no fill posted");
+	return t->txpq.settle(t->ctx, false);
 }
 
 // --------------------------------------------------------------------------

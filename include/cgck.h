@@ -207,19 +207,24 @@ void cgck_set_error_handler(cgck_error_fn fn, void *arg);
 int cgck_rx_begin(void *base, size_t bytes, const cgck_desc_t *desc, uint64_t n);
 int cgck_rx_end(void);
 
-/* Pipelined RX window: one burst in flight while the stack works.  The
+/* Pipelined RX window: bursts in flight while the stack works.  The
  * transport posts burst k as it arrives (cgck_rx_post returns at once, the
  * burst server computing it meanwhile), then opens the window over the
  * oldest posted burst — k - 1, whose values are in by then — with
  * cgck_rx_begin_posted, runs the stack over it and closes it with
  * cgck_rx_end as above.  The ring keeps a posted burst's frames unchanged
  * until its window closes (netmap's head and DPDK's mbuf free come after
- * the stack's processing: netmap.c:116-126, dpdk.c:255-263).  At most two
- * bursts are posted and not yet opened (-EBUSY).  Without an open burst
- * server, or when a burst does not fit it, cgck_rx_post computes the burst
- * at once.  cgck_rx_post returns the frames posted; cgck_rx_begin_posted
- * the frames the window answers for (as cgck_rx_begin), -ENOENT when
- * nothing is posted. */
+ * the stack's processing: netmap.c:116-126, dpdk.c:255-263).  Up to 64
+ * bursts may be posted and not yet opened (-EBUSY beyond).  One request per
+ * thread is on the burst server at a time: the bursts posted while it is
+ * there go out together, as one request, when it is back, so a loop that
+ * posts small bursts faster than one request's round trip pays one round
+ * trip per round trip, not per burst.  Without an open burst server, or
+ * when a burst does not fit it, cgck_rx_post computes the burst at once.
+ * cgck_rx_post returns the frames posted (-EINVAL: a descriptor reaches
+ * past `bytes`); cgck_rx_begin_posted the frames the window answers for
+ * (as cgck_rx_begin), -ENOENT when nothing is posted.  Posted fills
+ * (cgck_tx_post) coalesce the same way. */
 int cgck_rx_post(void *base, size_t bytes, const cgck_desc_t *desc, uint64_t n);
 int cgck_rx_begin_posted(void);
 
@@ -263,10 +268,20 @@ int cgck_tx_flush(void);
  * slots.  The transport calls
  * it before it hands those slots to the NIC — at the next loop's kick
  * (con-gen.c:493), so the GPU computes burst k while the stack builds burst
- * k + 1.  At most two fills are posted and not yet completed: a third
+ * k + 1.  Up to 64 fills may be posted and not yet completed: one more
  * cgck_tx_post completes the oldest first (its fields are written then). */
 int cgck_tx_post(void);
 int cgck_tx_complete(void);
+
+/* Without waiting: fills posted and not yet completed (cgck_tx_pending),
+ * and whether the oldest one's values are in (cgck_tx_ready: 1, so
+ * cgck_tx_complete will not wait; 0 while the GPU computes it; -ENOENT
+ * when none is posted).  A transport that holds each fill's slots back from
+ * the NIC until its completion (netmap: `head` stops at the fill's first
+ * slot; DPDK: its mbufs stay out of rte_eth_tx_burst) can complete fills as
+ * they come back instead of waiting at every kick. */
+int cgck_tx_pending(void);
+int cgck_tx_ready(void);
 
 /* Per-thread window counters since the thread's first call:
  * [0] drop-in calls answered by an RX window, [1] calls inside an RX window

@@ -814,3 +814,54 @@ def test_dropin_concurrent_threads(engine, golden_basic, server):
     for t in ts:
         t.join(timeout=120)
     assert not errors, errors[:5]
+
+
+def thp_ring(nbytes):
+    """A ring in an anonymous mapping advised MADV_HUGEPAGE, 2 MiB aligned
+    and never written yet: (owner, view).  The pages come in on the first
+    write after cgck_host_register — the trigger DESIGN.md §0 named for the
+    round-3/4 wrong-address reads."""
+    import mmap
+    al = 2 << 20
+    size = (nbytes + al - 1) // al * al
+    m = mmap.mmap(-1, size + al, flags=mmap.MAP_PRIVATE | mmap.MAP_ANONYMOUS)
+    whole = np.frombuffer(m, np.uint8)
+    start = (-whole.ctypes.data) % al
+    m.madvise(mmap.MADV_HUGEPAGE, start, size)
+    return m, whole[start:start + size]
+
+
+@pytest.mark.parametrize("cycle", range(3))
+def test_thp_ring_first_touch_after_register(engine, port, cycle):
+    """a ring advised MADV_HUGEPAGE, registered before
+    any of its pages exist, then written for the first time; GEN, FILL and
+    VERIFY through a 32-workgroup server (4096 packets, every index, byte
+    and verdict checked), then once more after the frames are rewritten in
+    place.  The smaps entry (AnonHugePages) and the THP counters of the
+    request go into the failure message."""
+    L = cgck.load()
+    rng = np.random.default_rng(7700 + cycle)
+    npk = 4096
+    buf, desc = random_batch(rng, npk, 600 if cycle % 2 else 1500)
+    raw, ring = thp_ring(len(buf))
+    vm0 = memdiag.vmstat()
+    assert L.cgck_host_register(ring.ctypes.data, ring.nbytes) == 0
+    engine.burst_open(max_pkts=4096, max_bytes=8 << 20)
+    try:
+        for rep in range(2):
+            for flags in (cgck.GEN_BOTH, cgck.FILL_BOTH, cgck.VERIFY_BSD):
+                ref = buf.copy()
+                exp, ever = port.batch_desc(ref, desc.view(np.uint8), len(desc), flags)
+                ring[:len(buf)] = buf                         # rep 0: the first touch of every page
+                got = ring[:len(buf)]
+                out = np.zeros(npk, np.uint32)
+                ver = np.zeros(npk, np.uint8)
+                vm = memdiag.vmstat()
+                engine.desc_host(got, desc, flags, out, ver)
+                check_burst(out, exp, ver, ever, got, ref,
+                            f"THP cycle {cycle} rep {rep} flags {flags} {memdiag.vma_info(ring.ctypes.data, 4096)} "
+                            f"thp since register {memdiag.vmstat_delta(vm0, memdiag.vmstat())}",
+                            4096, ring, desc, vm)
+    finally:
+        engine.burst_close()
+        assert L.cgck_host_unregister(ring.ctypes.data) == 0

@@ -354,17 +354,19 @@ def test_rx_pipelined_replay(port, nframes, server):
 def test_rx_post_limits(port):
     rng = np.random.default_rng(77)
     buf, desc = rxcorpus.ring(rxcorpus.corpus(rng, port, 16, clean=True))
-    rings = [buf.copy() for _ in range(3)]
-    assert cgck.rx_post(rings[0], desc) == 16
-    assert cgck.rx_post(rings[1], desc) == 16
+    rings = [buf.copy() for _ in range(65)]
+    for k in range(64):
+        assert cgck.rx_post(rings[k], desc) == 16
+    assert cgck.rx_pending() == 64
     with pytest.raises(cgck.CgckError, match="already posted"):
-        cgck.rx_post(rings[2], desc)
+        cgck.rx_post(rings[64], desc)
     assert cgck.rx_begin_posted() == 16
     with pytest.raises(cgck.CgckError, match="already open"):
         cgck.rx_begin_posted()
     assert cgck.rx_end() == 0
-    assert cgck.rx_begin_posted() == 16
-    assert cgck.rx_end() == 0
+    for k in range(63):
+        assert cgck.rx_begin_posted() == 16
+        assert cgck.rx_end() == 0
     bad = desc.copy()
     bad[3]["ip_len"] = 60000
     with pytest.raises(cgck.CgckError, match="reaches past"):
@@ -920,3 +922,103 @@ def test_rsp_iteration_tx_window(port, mode, ring):
         assert d[3] == 0 and d[2] == tx_calls, (d, tx_calls)
     else:
         assert d[3] == 2 * B.nlocal and d[2] == 2 * B.used, (d, B.used, B.nlocal)
+
+
+# ---------------------------------------------------------------------------
+# Coalesced posting: bursts and fills posted while an earlier request is on
+# the burst server go out together as one request when it is back
+# ---------------------------------------------------------------------------
+
+@pytest.mark.parametrize("server", [False, True])
+def test_rx_coalesced_small_bursts(port, server):
+    """Sixty bursts of 1..6 frames over one registered pool, posted and
+    opened on a random schedule (up to 40 outstanding), with a synchronous
+    drop-in call now and then (it takes a server slot): every burst's
+    window replays bit-exact, oldest first, and cgck_rx_ready never says
+    ready for a burst whose values are not in."""
+    R = referee(port)
+    L = cgck.load()
+    rng = np.random.default_rng(7100 + server)
+    sizes = [int(rng.integers(1, 7)) for _ in range(60)]
+    frames = rxcorpus.corpus(rng, R, sum(sizes), clean=True)
+    buf, desc_all = rxcorpus.ring(frames)
+    raw, pool, size = rxcorpus.registered_copy(buf)
+    assert L.cgck_host_register(pool.ctypes.data, size) == 0
+    got = pool[:len(buf)]
+    descs, at = [], 0
+    for s in sizes:
+        descs.append(desc_all[at:at + s].copy())
+        at += s
+    if server:
+        cgck.burst_open(max_pkts=1024, max_bytes=4 << 20)
+    other = np.arange(64, dtype=np.uint8)
+    posted = opened = 0
+    try:
+        while opened < len(sizes):
+            k = int(rng.integers(0, 4))
+            for _ in range(k):
+                if posted < len(sizes) and posted - opened < 40:
+                    assert cgck.rx_post(got, descs[posted]) == sizes[posted]
+                    posted += 1
+            if rng.random() < 0.1:
+                assert cgck.in_cksum(other, 3, 41) == R.in_cksum(other, 3, 41)
+            if posted > opened and rng.random() < 0.5:
+                r = cgck.rx_ready()
+                assert r in (0, 1)
+                cell = FLAGS[(opened * 5) % len(FLAGS)]
+                replay_posted(port, R, buf, descs[opened], got, cell)
+                opened += 1
+            assert cgck.rx_pending() == posted - opened
+    finally:
+        if server:
+            cgck.burst_close()
+        L.cgck_host_unregister(pool.ctypes.data)
+
+
+@pytest.mark.parametrize("server", [False, True])
+def test_tx_coalesced_fills(port, server):
+    """Forty small fills posted back to back with none completed (a
+    transport holding each fill's slots back until it completes), then
+    completed as cgck_tx_ready reports them in: every field equals the
+    reference's, fills complete in post order, and a fill's slots keep the
+    stack's zeros until then."""
+    rng = np.random.default_rng(7200 + server)
+    raw, ring, size = rxcorpus.registered_copy(np.zeros(200 * 2048, np.uint8))
+    slots = ring[:200 * 2048].reshape(200, 2048)
+    L = cgck.load()
+    assert L.cgck_host_register(ring.ctypes.data, size) == 0
+    if server:
+        cgck.burst_open(max_pkts=1024, max_bytes=4 << 20)
+    try:
+        fills, at = [], 0
+        for k in range(40):
+            want = []
+            cgck.tx_begin()
+            for i in range(at, at + int(rng.integers(1, 6))):
+                ln = int(rng.integers(40, 600))
+                pkt = tcp_pkt(rng, ln)
+                slots[i, 14:14 + ln] = pkt
+                want.append((i, ln, expected(port, pkt, 16)))
+                tx_calls(slots[i], ln, 16)
+            at += len(want)
+            assert cgck.tx_post() == 2 * len(want)
+            fills.append(want)
+        assert cgck.tx_pending() == 40
+        import time
+        t0 = time.monotonic()
+        done = 0
+        while done < 40:
+            if cgck.tx_ready() == 1 or time.monotonic() - t0 > 1.0:
+                assert cgck.tx_complete() == 2 * len(fills[done])
+                for i, ln, ref in fills[done]:
+                    assert np.array_equal(slots[i, 14:14 + ln], ref), (done, i)
+                done += 1
+                if done < 40:                   # the next fill's fields are still the zeros
+                    i, ln, _ = fills[done][0]
+                    if cgck.tx_ready() == 0:
+                        assert not slots[i, 14 + 10:14 + 12].any()
+        assert cgck.tx_pending() == 0 and cgck.tx_complete() == 0
+    finally:
+        if server:
+            cgck.burst_close()
+        L.cgck_host_unregister(ring.ctypes.data)

@@ -11,6 +11,16 @@ header at +14 as in netmap):
   * zcopy — the kernel reads the pinned host buffer directly over the
             fabric (no staging copy), outputs to device memory, D2H 4 B/pkt.
 
+  * registered — the ring in a mapping of its own, registered once with
+            cgck_host_register (a transport's pool): one cgck_desc_host over
+            all of it (descriptors up, the launch path's kernel reading the
+            frames in place, 4 B/packet back to host memory);
+  * server_2048 — the same ring in 2048-frame bursts, one synchronous
+            cgck_desc_host each through the thread's burst server;
+  * pipelined_2048 — the RX window's pipelined form over those bursts
+            (cgck_rx_post burst k, cgck_rx_begin_posted / cgck_rx_end burst
+            k - 1; no stack calls): the sustained burst rate of one worker.
+
 Prints one JSON line; numbers go to DESIGN.md (never bench.py's value).
 """
 import json
@@ -99,7 +109,71 @@ def run(layout, n, chunk, reps):
                     "parity": bool(np.array_equal(outs, ref))}
     for b in bufs + obufs + [o]:
         b.free()
+    # --- registered ring memory, cgck_desc_host (the product's host-resident path) ---
+    import mmap
+    size = (nbytes + 4095) // 4096 * 4096
+    mm = mmap.mmap(-1, size, flags=mmap.MAP_PRIVATE | mmap.MAP_ANONYMOUS)
+    ring = np.frombuffer(mm, np.uint8)
+    import ctypes
+    ctypes.memmove(ring.ctypes.data, host, nbytes)
     L.cgck_host_free(host)
+    cgck._check(L.cgck_host_register(ring.ctypes.data, size), "cgck_host_register")
+    desc = np.zeros(n, cgck.DESC_DTYPE)
+    desc["frame_off"] = np.arange(n, dtype=np.uint64) * stride
+    desc["l3_off"] = l3
+    desc["ip_len"] = ln
+    ctx = e0.ctx
+    gen = cgck.GEN_BOTH
+
+    def desc_host(lo, m):
+        cgck._check(L.cgck_desc_host(ctx, ring.ctypes.data, size, desc[lo:].ctypes.data, m, gen,
+                                     outs[lo:].ctypes.data, None), "cgck_desc_host")
+
+    outs[:] = 0
+    best = None
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        desc_host(0, n)
+        dt = time.perf_counter() - t0
+        best = dt if best is None else min(best, dt)
+    res["registered"] = {"mpkt_s": n / best / 1e6, "wire_gb_s": n * ln / best / 1e9,
+                         "parity": bool(np.array_equal(outs, ref))}
+    B = 2048
+    cgck._check(L.cgck_burst_open(ctx, B, B * 1536, 0), "cgck_burst_open")
+    outs[:] = 0
+    best = None
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        for lo in range(0, n, B):
+            desc_host(lo, min(B, n - lo))
+        dt = time.perf_counter() - t0
+        best = dt if best is None else min(best, dt)
+    res["server_2048"] = {"mpkt_s": n / best / 1e6, "wire_gb_s": n * ln / best / 1e9,
+                          "us_per_burst": best / ((n + B - 1) // B) * 1e6,
+                          "parity": bool(np.array_equal(outs, ref))}
+    L.cgck_burst_close(ctx)
+    # the RX window's pipelined form on this thread's own context and server
+    cgck.burst_open(max_pkts=B, max_bytes=B * 1536)
+    best = None
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        k = 0
+        for lo in range(0, n, B):
+            cgck._check(L.cgck_rx_post(ring.ctypes.data, size, desc[lo:].ctypes.data, min(B, n - lo)), "rx_post")
+            if k:
+                cgck._check(L.cgck_rx_begin_posted(), "rx_begin_posted")
+                L.cgck_rx_end()
+            k += 1
+        cgck._check(L.cgck_rx_begin_posted(), "rx_begin_posted")
+        L.cgck_rx_end()
+        dt = time.perf_counter() - t0
+        best = dt if best is None else min(best, dt)
+    res["pipelined_2048"] = {"mpkt_s": n / best / 1e6, "wire_gb_s": n * ln / best / 1e9,
+                             "us_per_burst": best / ((n + B - 1) // B) * 1e6}
+    cgck.burst_close()
+    cgck.thread_release()
+    L.cgck_host_unregister(ring.ctypes.data)
+    del ring
     return res
 
 

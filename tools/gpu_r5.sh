@@ -25,6 +25,8 @@ for step in "$@"; do
 	quick) run pytest_quick 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "burst or window or pipelined or rx_post or tx_" || exit 1 ;;
 	txburst) run txburst 400 tools/txburst 0.2 || exit 1 ;;
 	txloop) run txloop 400 tools/txloop 0.2 || exit 1 ;;
+	e2e) run e2e 300 python -u tools/e2e.py || exit 1 ;;
+	rss) run rss_steady 200 python -u tools/rss_steady.py || exit 1 ;;
 	txloop128) TXLOOP_LEN=128 run txloop128 400 tools/txloop 0.2 || exit 1 ;;
 	txlens) # con-gen's typical frames (54-130 B): 128 B beside 64 B
 		TXBURST_LENS=128,64 run txburst_128 400 tools/txburst 0.2 || exit 1 ;;

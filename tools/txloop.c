@@ -147,7 +147,7 @@ static inline void reply(uint8_t *tx, const uint8_t *rx, in_fn fin, udp_fn fudp)
 
 struct cell {
 	double *worker, *wait, *lat;
-	int it, bad_rx, bad_tx_checked, bad_tx;
+	int it, itl, bad_rx, bad_tx_checked, bad_tx;
 };
 
 static in_fn ref_in;
@@ -172,6 +172,41 @@ static int check_replies(const uint8_t *txh, int R)
 		bad += ref_in(c, 20) != s_ip;
 	}
 	return bad;
+}
+
+/* the coalesced form's posted fills: their first reply slot and count */
+struct fills {
+	long start[64], cnt[64];
+	int h, n;
+	long cursor, busy; /* next free slot; slots of posted fills */
+};
+
+static void fill_push(struct fills *f, long cnt)
+{
+	const int i = (f->h + f->n) % 64;
+	f->start[i] = f->cursor;
+	f->cnt[i] = cnt;
+	f->n++;
+	f->cursor += cnt;
+	f->busy += cnt;
+}
+
+/* complete the oldest fill (waits if it is not back); its first reply checked */
+static int fill_done(struct fills *f, int mix, const uint8_t *tx0, struct cell *c)
+{
+	const int done = cgck_tx_complete();
+	if (done < 0)
+		return done;
+	const long cnt = f->cnt[f->h];
+	if (mix && cnt > 0) {
+		c->bad_tx += done != 2 * cnt;
+		c->bad_tx += check_replies(tx0 + (size_t)(f->start[f->h] % (2 * MAXB)) * SLOT, 1);
+		c->bad_tx_checked++;
+	}
+	f->busy -= cnt;
+	f->h = (f->h + 1) % 64;
+	f->n--;
+	return 0;
 }
 
 int main(int argc, char **argv)
@@ -258,7 +293,7 @@ int main(int argc, char **argv)
 	}
 	in_fn lib_in = (in_fn)in_cksum;
 	udp_fn lib_udp = (udp_fn)udp_cksum;
-	static const char *forms[3] = {"reference", "pipelined", "sync"};
+	static const char *forms[4] = {"reference", "pipelined", "sync", "coalesced"};
 	for (int mix = 0; mix < 2; mix++) {
 		for (int bud = 0; bud <= nns; bud++) {
 			const double ns = bud < nns ? nsl[bud] : 0, fixed_us = bud < nns ? 0 : 50;
@@ -266,9 +301,12 @@ int main(int argc, char **argv)
 				const int R = bursts[bi];
 				const double other = (R * ns + fixed_us * 1000) * 1e-9;
 				const int expect = (R + 63) / 64;
-				for (int form = 0; form < 3; form++) {
-					c.it = c.bad_rx = c.bad_tx = c.bad_tx_checked = 0;
+				for (int form = 0; form < 4; form++) {
+					c.it = c.itl = c.bad_rx = c.bad_tx = c.bad_tx_checked = 0;
 					int k = 0;
+					long copened = 0; /* coalesced form: bursts opened */
+					struct fills cf;
+					memset(&cf, 0, sizeof(cf));
 					const double t0 = now();
 					while (c.it < MAXIT && now() - t0 < budget) {
 						const int rec = k >= 20;
@@ -316,6 +354,58 @@ int main(int argc, char **argv)
 							} else {
 								bad = expect;
 							}
+						} else if (form == 3) {
+							/* the kick releases the fills that are back
+							 * (no wait unless 48 are outstanding); burst k
+							 * is posted; every burst whose values are in
+							 * is processed, oldest first (no wait unless
+							 * 48 are outstanding).  Replies go to a rolling
+							 * cursor over both transmit halves; a fill's
+							 * slots are reused only after it completed. */
+							double w0 = now();
+							while (cf.n > 0 && (cgck_tx_ready() == 1 || cf.n >= 48)) {
+								if (fill_done(&cf, mix, txh[0], &c) < 0)
+									goto fail;
+							}
+							w += now() - w0;
+							cgck_tx_begin();
+							tpost[k % 64] = now();
+							if (cgck_rx_post(rxh[k & 1], 2 * half, desc, R) != R)
+								goto fail;
+							int got = 0;
+							long cur = 0; /* this iteration's reply slots */
+							for (;;) {
+								const int pend = cgck_rx_pending();
+								const int rdy = pend ? cgck_rx_ready() : 0;
+								if (!pend || (rdy != 1 && pend < 48) || cur + R > 2 * MAXB)
+									break;
+								w0 = now();
+								while (cf.n > 0 && cf.busy + cur + R > 2 * MAXB)
+									if (fill_done(&cf, mix, txh[0], &c) < 0)
+										goto fail;
+								if (cgck_rx_begin_posted() != R)
+									goto fail;
+								w += now() - w0;
+								uint8_t *rx = rxh[copened & 1];
+								for (int i = 0; i < R; i++) {
+									uint8_t *ip = rx + (size_t)i * SLOT + L3;
+									bad += verify(ip, len, lib_in, lib_udp);
+									if (mix)
+										reply(txh[0] + (size_t)((cf.cursor + cur + i) % (2 * MAXB)) * SLOT +
+											      L3,
+										      ip, lib_in, lib_udp);
+								}
+								if (mix)
+									cur += R;
+								if (cgck_rx_end() != 2 * R)
+									goto fail;
+								lat += now() - tpost[copened % 64];
+								copened++;
+								got++;
+							}
+							bad = got ? (bad == got * expect ? expect : -1) : expect;
+							lat = got ? lat / got : 0;
+							fill_push(&cf, cur);
 						} else {
 							uint8_t *rx = rxh[k & 1];
 							cgck_tx_begin();
@@ -336,7 +426,7 @@ int main(int argc, char **argv)
 						const double a_spin = now();
 						spin(other);
 						const double spun = now() - a_spin;
-						if (form == 1) {
+						if (form == 1 || form == 3) {
 							if (cgck_tx_post() < 0)
 								goto fail;
 						} else if (form == 2) {
@@ -353,22 +443,23 @@ int main(int argc, char **argv)
 						if (rec) {
 							c.worker[c.it] = now() - a - spun;
 							c.wait[c.it] = w;
-							c.lat[c.it] = lat;
 							c.it++;
+							if (lat > 0) /* (the coalesced form: iterations that opened bursts) */
+								c.lat[c.itl++] = lat;
 						}
 						k++;
 					}
-					if (form == 1) { /* drain: the last burst and fill */
-						if (cgck_rx_begin_posted() >= 0)
+					if (form == 1 || form == 3) { /* drain: the bursts and fills left */
+						while (cgck_rx_pending() > 0 && cgck_rx_begin_posted() >= 0)
 							cgck_rx_end();
-						cgck_tx_post();
-						cgck_tx_complete();
-						cgck_tx_complete();
+						while (cgck_tx_pending() > 0)
+							cgck_tx_complete();
+						memset(&cf, 0, sizeof(cf));
 					}
 					const int n = c.it;
 					const double wm = pct(c.worker, n, 50) * 1e6, w90 = pct(c.worker, n, 90) * 1e6;
 					const double wt = pct(c.wait, n, 50) * 1e6;
-					const double lm = pct(c.lat, n, 50) * 1e6, l90 = pct(c.lat, n, 90) * 1e6;
+					const double lm = pct(c.lat, c.itl, 50) * 1e6, l90 = pct(c.lat, c.itl, 90) * 1e6;
 					printf("{\"mode\": \"loop\", \"form\": \"%s\", \"mix\": \"%s\", \"pkt_len\": %d, "
 					       "\"burst\": %d, \"stack_ns_per_frame\": %.0f, \"stack_us_fixed\": %.0f, "
 					       "\"iters\": %d, \"us_worker\": %.3f, \"us_worker_p90\": %.3f, \"us_wait\": %.3f, "
