@@ -363,6 +363,64 @@ def bench_burst():
     return [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
 
 
+def bench_loop():
+    """con-gen's worker loop at the checksum boundary (tools/txloop.c): both
+    windows open across the iteration, bursts of 1..2048 64 B frames, the
+    rest of the stack's work as 0 or 250 ns a frame or 50 us a burst; per
+    form (the reference's own functions, pipelined, coalesced, synchronous)
+    the worker's us per iteration, its wait and the post-to-verdict latency.
+    Host-resident: never `value`.  Returns all rows."""
+    import subprocess
+    exe = os.path.join(ROOT, "tools", "txloop")
+    if not os.path.exists(exe):
+        return None
+    r = subprocess.run([exe, "0.1"], capture_output=True, text=True, timeout=300)
+    if r.returncode != 0:
+        return {"error": r.stderr.strip()[-300:]}
+    return [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+
+
+LOOP_FORMS = ("reference", "pipelined", "coalesced", "sync")
+
+
+def loop_summary(rows):
+    """Per (mix, stack budget): [burst, us per iteration of each form
+    (LOOP_FORMS), the pipelined form's wait, the pipelined and coalesced
+    forms' post-to-verdict latency]; per (mix, budget, form) the crossover
+    burst (the smallest from which the form costs the worker less than the
+    reference loop at every larger measured burst, None if never); the drain
+    rule's lone-burst latency per burst."""
+    if not isinstance(rows, list):
+        return rows
+    loop = [r for r in rows if r.get("mode") == "loop"]
+    by = {(r["mix"], r["stack_ns_per_frame"], r["stack_us_fixed"], r["form"], r["burst"]): r for r in loop}
+    cells = sorted({(r["mix"], r["stack_ns_per_frame"], r["stack_us_fixed"]) for r in loop})
+    bursts = sorted({r["burst"] for r in loop})
+    out = {"unit": "us per loop iteration (worker thread, checksum path only)",
+           "cols": ["burst"] + [f"{f}_us" for f in LOOP_FORMS] + ["pipelined_wait_us", "pipelined_latency_us",
+                                                                  "coalesced_latency_us"],
+           "rows": {}, "crossover": {}, "exact": all(r.get("exact") for r in rows if "exact" in r)}
+    for mix, ns, fx in cells:
+        key = f"{mix}@{'%gus/burst' % fx if fx else '%gns/frame' % ns}"
+        tab = []
+        for b in bursts:
+            g = lambda f, c="us_worker": by.get((mix, ns, fx, f, b), {}).get(c)
+            tab.append([b] + [g(f) for f in LOOP_FORMS] + [g("pipelined", "us_wait"), g("pipelined", "us_latency"),
+                                                         g("coalesced", "us_latency")])
+        out["rows"][key] = tab
+        cross = {}
+        for fi, f in enumerate(LOOP_FORMS[1:], 2):
+            first = None
+            for row in reversed(tab):
+                if row[1] is None or row[fi] is None or not row[fi] < row[1]:
+                    break
+                first = row[0]
+            cross[f] = first
+        out["crossover"][key] = cross
+    out["lone_latency_us"] = {r["burst"]: r["us_latency"] for r in rows if r.get("mode") == "lone"}
+    return out
+
+
 BURST_COLS = ["pkt_len", "burst", "rx_window_launch_us", "rx_window_server_us", "rx_window_pipelined_us",
               "tx_fill_launch_us", "tx_fill_server_us", "tx_fill_pipelined_us", "rx_ref_loop_us", "tx_ref_loop_us",
               "cpu_ref_us"]
@@ -715,9 +773,10 @@ def main():
                            "pci_bus": torch.cuda.get_device_properties(dev).pci_bus_id
                            if hasattr(torch.cuda.get_device_properties(dev), "pci_bus_id") else None})
 
-    burst = None
+    burst = loop = None
     if dist.rank == 0 and dist.world == 1 and not args.no_burst and args.only is None:
         burst = bench_burst()
+        loop = bench_loop()
     cpu = cpu_r = cpu_64 = cpu_b = None
     if dist.rank == 0 and dist.world == 1 and not args.no_cpu:
         if burst:
@@ -809,7 +868,7 @@ def main():
             try:
                 os.makedirs(os.path.dirname(path), exist_ok=True)
                 with open(path, "w") as f:
-                    json.dump({"rows": burst, "cpu_baseline": cpu_b}, f, indent=0)
+                    json.dump({"rows": burst, "cpu_baseline": cpu_b, "loop_rows": loop}, f, indent=0)
             except OSError:
                 path = None
             extra["burst"] = {"what": "us per burst, 2048 B ring slots registered with cgck_host_register, "
@@ -819,7 +878,8 @@ def main():
                                       "cpu_ref = the reference in_cksum+udp_cksum per packet, 1 core",
                               "cols": BURST_COLS, "rows": burst_summary(burst, cpu_b),
                               "crossover_burst": burst_crossover(burst, cpu_b),
-                              "all_rows": path and "gpurun_out/bench_burst.json"}
+                              "all_rows": path and "gpurun_out/bench_burst.json",
+                              "loop": loop_summary(loop)}
         if extra:
             out["extra"] = extra
         if "value" not in out:   # --only 64 / imix / rss profiling runs

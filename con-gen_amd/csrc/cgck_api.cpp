@@ -607,14 +607,22 @@ int cgck::burst_collect(cgck_ctx *c, BurstPending *p)
 	return rc;
 }
 
-int cgck::burst_ready(const cgck_ctx *c, const BurstPending *p)
+int cgck::burst_ready(cgck_ctx *c, const BurstPending *p)
 {
 	if (!p->seq)
 		return 1;
 	const uint32_t W = burst_wgs(p->n, c->bwgs, c->bper);
 	for (uint32_t j = 0; j < W; j++)
-		if ((int32_t)(__atomic_load_n(&c->bbox->done[j], __ATOMIC_ACQUIRE) - p->seq) < 0)
+		if ((int32_t)(__atomic_load_n(&c->bbox->done[j], __ATOMIC_ACQUIRE) - p->seq) < 0) {
+			// not served yet: a server that idled out between the post and
+			// its last poll is relaunched here, as burst_wait would, so a
+			// caller that only ever asks does not wait forever
+			if (!burst_all_alive(c)) {
+				std::shared_lock<std::shared_mutex> map_lk(g_map_mu);
+				(void)burst_restart(c);
+			}
 			return 0;
+		}
 	return 1;
 }
 

@@ -123,7 +123,7 @@ int desc_host_post(cgck_ctx *c, void *base, size_t bytes, const cgck_desc_t *des
 int burst_collect(cgck_ctx *c, BurstPending *pend);
 // Without waiting: is the posted request's every slice served (1), or not
 // yet (0)?  A request that was computed at once (seq 0) is ready.
-int burst_ready(const cgck_ctx *c, const BurstPending *pend);
+int burst_ready(cgck_ctx *c, const BurstPending *pend);
 
 // Staging path of one region for the drop-in symbols (burst server when open,
 // else a launch on the context stream and a synchronisation).

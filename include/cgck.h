@@ -246,16 +246,25 @@ int cgck_rx_ready(void);
 
 /* Deferred TX fill.  Between begin and flush, the
  * drop-in in_cksum/udp_cksum calls of THIS thread that target an IPv4
- * header (len == ip_hl*4) or a TCP/UDP segment lying inside memory
- * registered with cgck_host_register (the transport's ring or mempool,
- * whose slots stay owned by the stack until the kick) return 0 and are
- * queued; a second call for the same header or segment replaces the first.
- * Calls on any other memory (a stack-local struct packet, pkt_body) are
- * computed synchronously, as outside the window.  The flush computes the
+ * header (len == ip_hl*4), a TCP/UDP segment, or an ICMP message right
+ * after a 20-byte header of protocol 1 (icmp_send, ip_icmp.c:68-80) lying
+ * inside memory registered with cgck_host_register (the transport's ring or
+ * mempool, whose slots stay owned by the stack until the kick) return 0 and
+ * are queued; a second call for the same header or segment replaces the
+ * first.  Calls on any other memory (a stack-local struct packet, pkt_body)
+ * are computed synchronously, as outside the window.  The flush computes the
  * queue in one launch and writes each result into its field (ip+10; TCP +16
- * / UDP +6 after the header); it must run before the transport hands the
- * slots to the NIC.  Returns the number of fields written, or a negative
- * errno. */
+ * / UDP +6 / ICMP +2 after the header); it must run before the transport
+ * hands the slots to the NIC.  Returns the number of fields written, or a
+ * negative errno.
+ *
+ * The window may stay open for the whole loop iteration,
+ * so the replies the stack builds while it processes a burst (tcp_respond,
+ * icmp_error, echo replies) and check_timers' keepalives are queued too.
+ * A call about a frame of the open RX window is never queued (it is the
+ * stack verifying what it received).  A received frame must therefore be
+ * processed inside an RX window whenever the TX window is open: its verify
+ * calls outside one would look like a transmit call and be queued. */
 int cgck_tx_begin(void);
 int cgck_tx_flush(void);
 

@@ -26,6 +26,12 @@ for step in "$@"; do
 	txburst) run txburst 400 tools/txburst 0.2 || exit 1 ;;
 	txloop) run txloop 400 tools/txloop 0.2 || exit 1 ;;
 	e2e) run e2e 300 python -u tools/e2e.py || exit 1 ;;
+	lpdab) # lab lpd variants against the product kernel, one process each (64 B)
+		for cfg in "64 6 2" "64 5 2" "32 8 5" "64 6 5" "16 8 2"; do
+			set -- $cfg
+			CGCK_LPD_C=$1 CGCK_LPD_WPC=$2 CGCK_LPD_SP=$3 run lpdab_c$1_w$2_sp$3 120 python -u tools/ab_inproc.py \
+				--libs con-gen_amd/libcgck.so,con-gen_amd/libcgck_lab.so --workloads 64 --rounds 5 || exit 1
+		done ;;
 	rss) run rss_steady 200 python -u tools/rss_steady.py || exit 1 ;;
 	txloop128) TXLOOP_LEN=128 run txloop128 400 tools/txloop 0.2 || exit 1 ;;
 	txlens) # con-gen's typical frames (54-130 B): 128 B beside 64 B
