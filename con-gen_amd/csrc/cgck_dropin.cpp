@@ -248,6 +248,8 @@ struct ThreadState {
 	// first TX-window call of the window (rx_owns)
 	bool rx_iv_built = false;
 	std::vector<std::pair<uintptr_t, uintptr_t>> rx_iv;
+	bool rx_span_built = false;
+	uintptr_t rx_lo = 0, rx_hi = 0;
 	RxBurst rxs;      // cgck_rx_begin's burst
 	PostQueue rxpq;   // posted bursts (cgck_rx_post)
 	uint64_t rx_served0 = 0; // stats[0] at rx_begin
@@ -338,6 +340,29 @@ __attribute__((noinline)) bool rx_find_slow(ThreadState &t, const uint8_t *p, ui
 	return true;
 }
 
+// [rx_lo, rx_hi): the bytes the burst's frames span, computed on the first
+// call the cursor probe does not answer (most bursts never need it).
+__attribute__((noinline)) void rx_span(ThreadState &t)
+{
+	uintptr_t lo = UINTPTR_MAX, hi = 0;
+	for (size_t i = 0; i < t.rx_n; i++) {
+		const uintptr_t a = (uintptr_t)(t.rx_base + t.rxd[i].frame_off);
+		const uintptr_t e = a + t.rxd[i].l3_off + t.rxd[i].ip_len;
+		lo = a < lo ? a : lo;
+		hi = e > hi ? e : hi;
+	}
+	t.rx_lo = lo;
+	t.rx_hi = hi;
+	t.rx_span_built = true;
+}
+
+inline bool rx_in_span(ThreadState &t, const uint8_t *p)
+{
+	if (!t.rx_span_built)
+		rx_span(t);
+	return (uintptr_t)p >= t.rx_lo && (uintptr_t)p < t.rx_hi;
+}
+
 // The header of the cursor frame or of the next one (the stack's next call
 // is almost always one of the two) without leaving the caller; everything
 // else (ICMP messages, skipped frames, the map) in rx_find_slow.
@@ -355,6 +380,11 @@ inline bool rx_find(ThreadState &t, const uint8_t *p, uint32_t *v)
 			return true;
 		}
 	}
+	// Off the cursor: a call outside the burst's address span (a reply the
+	// stack builds in a transmit slot while the window is open) is no frame
+	// of the burst, and needs neither the map nor rx_owns
+	if (!rx_in_span(t, p))
+		return false;
 	return rx_find_slow(t, p, v);
 }
 
@@ -373,6 +403,8 @@ inline int l4_fo(const uint8_t *ip) { return ip[9] == 6 ? 16 : ip[9] == 17 ? 6 :
 // that asks (a burst that draws no reply never pays for it).
 __attribute__((noinline)) bool rx_owns(ThreadState &t, const uint8_t *p)
 {
+	if (!rx_in_span(t, p))
+		return false;
 	if (!t.rx_iv_built) {
 		t.rx_iv.resize(t.rx_n);
 		bool sorted = true;
@@ -840,6 +872,7 @@ int rx_open_on(ThreadState &t, const uint8_t *base, uint64_t n, const cgck_desc_
 	t.rx_cur = 0;
 	t.rx_map = false;
 	t.rx_iv_built = false;
+	t.rx_span_built = false;
 	t.rx_open = true;
 	t.rx_posted = posted;
 	t.rx_served0 = t.stats[0];

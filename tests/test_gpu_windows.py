@@ -753,35 +753,37 @@ def test_posted_burst_survives_unregister(port):
 
 
 @pytest.mark.parametrize("server", [False, True])
-def test_tx_third_post_completes_oldest(port, server):
-    """Two fills posted and a third window closed: cgck_tx_post completes the
+def test_tx_post_beyond_queue_completes_oldest(port, server):
+    """64 fills posted and a 65th window closed: cgck_tx_post completes the
     oldest first (its fields written), so no queued field is dropped."""
     rng = np.random.default_rng(5400 + server)
-    raw, ring, size = rxcorpus.registered_copy(np.zeros(96 * 2048, np.uint8))
-    slots = ring[:96 * 2048].reshape(96, 2048)
+    raw, ring, size = rxcorpus.registered_copy(np.zeros(130 * 2048, np.uint8))
+    slots = ring[:130 * 2048].reshape(130, 2048)
     L = cgck.load()
     assert L.cgck_host_register(ring.ctypes.data, size) == 0
     if server:
         cgck.burst_open(max_pkts=1024, max_bytes=4 << 20)
     try:
-        bursts = []
-        for k in range(3):
+        fills = []
+        for k in range(65):
             want = []
             cgck.tx_begin()
-            for i in range(k * 32, k * 32 + 32):
+            for i in range(2 * k, 2 * k + 2):
                 ln = int(rng.integers(40, 1501))
                 pkt = tcp_pkt(rng, ln)
                 slots[i, 14:14 + ln] = pkt
                 want.append((i, ln, expected(port, pkt, 16)))
                 tx_calls(slots[i], ln, 16)
-            assert cgck.tx_post() == 64
-            bursts.append(want)
-        for i, ln, ref in bursts[0]:                     # written by the third post
+            assert cgck.tx_post() == 4
+            fills.append(want)
+        assert cgck.tx_pending() == 64
+        for i, ln, ref in fills[0]:                      # written by the 65th post
             assert np.array_equal(slots[i, 14:14 + ln], ref), (0, i)
-        assert cgck.tx_complete() == 64 and cgck.tx_complete() == 64 and cgck.tx_complete() == 0
-        for k in (1, 2):
-            for i, ln, ref in bursts[k]:
+        for k in range(1, 65):
+            assert cgck.tx_complete() == 4
+            for i, ln, ref in fills[k]:
                 assert np.array_equal(slots[i, 14:14 + ln], ref), (k, i)
+        assert cgck.tx_complete() == 0
     finally:
         if server:
             cgck.burst_close()
@@ -815,7 +817,7 @@ class Iteration:
     def __init__(self, port, fns, pool, tx_base, tx_stride, cap):
         self.port, self.fns, self.pool = port, fns, pool
         self.tx_base, self.tx_stride, self.cap = tx_base, tx_stride, cap
-        self.local = np.zeros(2048 * 256, np.uint8)
+        self.local = np.zeros(2048 * 1200, np.uint8)   # room for every reply (the ring full from the start)
         self.used = self.nlocal = 0
         self.ip_id = 4242
         self.sent = np.zeros(4, np.int64)
@@ -860,7 +862,7 @@ def test_rsp_iteration_tx_window(port, mode, ring):
     bursts = [rxcorpus.rsp_corpus(rng, R, 60 + 70 * k) for k in range(nb)]
     frames = [f for b in bursts for f in b]
     kas = [ka_records(rng, 6) for _ in range(nb)]
-    cap = 2000 if ring == "room" else 40
+    cap = 1200 if ring == "room" else 40             # transmit slots (rxcorpus.pool(frames, 1200))
     buf, desc_all, tx_base, tx_stride = rxcorpus.pool(frames, 1200)
     descs, at = [], 0
     for b in bursts:
@@ -914,6 +916,7 @@ def test_rsp_iteration_tx_window(port, mode, ring):
         L.cgck_host_unregister(got.ctypes.data)
     d = [y - x for x, y in zip(s0, s1)]
     assert A.used == B.used and A.nlocal == B.nlocal and np.array_equal(A.sent, B.sent)
+    assert A.used + A.nlocal <= 1200
     assert min(A.sent) > 0, A.sent
     assert np.array_equal(ref, got), np.nonzero(ref != got)[0][:16]
     assert np.array_equal(A.local[:A.nlocal * 2048], B.local[:B.nlocal * 2048])
@@ -952,6 +955,7 @@ def test_rx_coalesced_small_bursts(port, server):
     if server:
         cgck.burst_open(max_pkts=1024, max_bytes=4 << 20)
     other = np.arange(64, dtype=np.uint8)
+    ref = buf.copy()                                # the reference replay's ring, burst after burst
     posted = opened = 0
     try:
         while opened < len(sizes):
@@ -965,8 +969,16 @@ def test_rx_coalesced_small_bursts(port, server):
             if posted > opened and rng.random() < 0.5:
                 r = cgck.rx_ready()
                 assert r in (0, 1)
-                cell = FLAGS[(opened * 5) % len(FLAGS)]
-                replay_posted(port, R, buf, descs[opened], got, cell)
+                stack, ip_in, tcp_in = cell = FLAGS[(opened * 5) % len(FLAGS)]
+                d = descs[opened]
+                a = port.replay_rx(*R.fn_pointers(), ref, d.view(np.uint8), len(d), stack, ip_in, tcp_in)
+                cgck.rx_begin_posted()
+                try:
+                    b = port.replay_rx(*cgck.fn_pointers(), got, d.view(np.uint8), len(d), stack, ip_in, tcp_in)
+                finally:
+                    cgck.rx_end()
+                assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]), (opened, cell, a, b)
+                assert np.array_equal(ref, got), (opened, cell)   # the ring as the reference left it
                 opened += 1
             assert cgck.rx_pending() == posted - opened
     finally:

@@ -123,7 +123,7 @@ def run(layout, n, chunk, reps):
     desc["l3_off"] = l3
     desc["ip_len"] = ln
     ctx = e0.ctx
-    gen = cgck.GEN_BOTH
+    gen = cgck.FILL_BOTH & ~cgck.STORE   # the same flags as the copy / zcopy modes
 
     def desc_host(lo, m):
         cgck._check(L.cgck_desc_host(ctx, ring.ctypes.data, size, desc[lo:].ctypes.data, m, gen,

@@ -287,6 +287,15 @@ int main(int argc, char **argv)
 	for (int i = 0; i < MAXB; i += 64) /* every 64th frame corrupted */
 		rxh[0][(size_t)i * SLOT + L3 + len - 1] ^= 0x5A;
 	memcpy(rxh[1], rxh[0], half);
+	/* every post names the whole pool, as a transport's does (one base, the
+	 * frames by offset), so bursts posted back to back can share a request */
+	cgck_desc_t *descs[2] = {desc, malloc(sizeof(cgck_desc_t) * MAXB)};
+	if (!descs[1])
+		return 1;
+	for (int i = 0; i < MAXB; i++) {
+		descs[1][i] = desc[i];
+		descs[1][i].frame_off += half;
+	}
 	if (cgck_host_register(pool, pool_bytes) || cgck_burst_open(NULL, MAXB, (size_t)MAXB * 1536, 0)) {
 		fprintf(stderr, "txloop: setup failed: %s\n", cgck_last_error());
 		return 1;
@@ -334,7 +343,7 @@ int main(int argc, char **argv)
 							}
 							cgck_tx_begin();
 							tpost[k] = now();
-							if (cgck_rx_post(rxh[k & 1], 2 * half, desc, R) != R)
+							if (cgck_rx_post(pool, pool_bytes, descs[k & 1], R) != R)
 								goto fail;
 							if (k > 0) {
 								uint8_t *rx = rxh[(k + 1) & 1];
@@ -370,7 +379,7 @@ int main(int argc, char **argv)
 							w += now() - w0;
 							cgck_tx_begin();
 							tpost[k % 64] = now();
-							if (cgck_rx_post(rxh[k & 1], 2 * half, desc, R) != R)
+							if (cgck_rx_post(pool, pool_bytes, descs[k & 1], R) != R)
 								goto fail;
 							int got = 0;
 							long cur = 0; /* this iteration's reply slots */
@@ -410,7 +419,7 @@ int main(int argc, char **argv)
 							uint8_t *rx = rxh[k & 1];
 							cgck_tx_begin();
 							double w0 = now();
-							if (cgck_rx_begin(rx, 2 * half, desc, R) != R)
+							if (cgck_rx_begin(pool, pool_bytes, descs[k & 1], R) != R)
 								goto fail;
 							w += now() - w0;
 							for (int i = 0; i < R; i++) {
@@ -478,7 +487,7 @@ int main(int argc, char **argv)
 		const double t0 = now();
 		while (n < MAXIT && now() - t0 < budget) {
 			const double a = now();
-			if (cgck_rx_post(rxh[0], 2 * half, desc, R) != R || cgck_rx_pending() != 1)
+			if (cgck_rx_post(pool, pool_bytes, descs[0], R) != R || cgck_rx_pending() != 1)
 				goto fail;
 			if (cgck_rx_begin_posted() != R) /* the next iteration: nothing arrived, drain */
 				goto fail;
