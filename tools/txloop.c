@@ -148,6 +148,8 @@ static inline void reply(uint8_t *tx, const uint8_t *rx, in_fn fin, udp_fn fudp)
 struct cell {
 	double *worker, *wait, *lat;
 	int it, itl, bad_rx, bad_tx_checked, bad_tx;
+	double total; /* worker seconds over the recorded iterations */
+	long bursts;  /* bursts they processed */
 };
 
 static in_fn ref_in;
@@ -176,19 +178,22 @@ static int check_replies(const uint8_t *txh, int R)
 
 /* the coalesced form's posted fills: their first reply slot and count */
 struct fills {
-	long start[64], cnt[64];
+	long start[64], cnt[64], nrep[64];
 	int h, n;
-	long cursor, busy; /* next free slot; slots of posted fills */
+	long cursor, busy; /* next free slot; slots held by posted fills */
 };
 
-static void fill_push(struct fills *f, long cnt)
+/* a fill of `nrep` replies from cursor + gap (gap: the ring's tail skipped,
+ * so a fill's slots never wrap and the window keeps its address order) */
+static void fill_push(struct fills *f, long gap, long nrep)
 {
 	const int i = (f->h + f->n) % 64;
-	f->start[i] = f->cursor;
-	f->cnt[i] = cnt;
+	f->start[i] = f->cursor + gap;
+	f->cnt[i] = gap + nrep;
+	f->nrep[i] = nrep;
 	f->n++;
-	f->cursor += cnt;
-	f->busy += cnt;
+	f->cursor += gap + nrep;
+	f->busy += gap + nrep;
 }
 
 /* complete the oldest fill (waits if it is not back); its first reply checked */
@@ -197,9 +202,9 @@ static int fill_done(struct fills *f, int mix, const uint8_t *tx0, struct cell *
 	const int done = cgck_tx_complete();
 	if (done < 0)
 		return done;
-	const long cnt = f->cnt[f->h];
-	if (mix && cnt > 0) {
-		c->bad_tx += done != 2 * cnt;
+	const long cnt = f->cnt[f->h], nrep = f->nrep[f->h];
+	if (mix && nrep > 0) {
+		c->bad_tx += done != 2 * nrep;
 		c->bad_tx += check_replies(tx0 + (size_t)(f->start[f->h] % (2 * MAXB)) * SLOT, 1);
 		c->bad_tx_checked++;
 	}
@@ -312,6 +317,8 @@ int main(int argc, char **argv)
 				const int expect = (R + 63) / 64;
 				for (int form = 0; form < 4; form++) {
 					c.it = c.itl = c.bad_rx = c.bad_tx = c.bad_tx_checked = 0;
+					c.total = 0;
+					c.bursts = 0;
 					int k = 0;
 					long copened = 0; /* coalesced form: bursts opened */
 					struct fills cf;
@@ -320,6 +327,7 @@ int main(int argc, char **argv)
 					while (c.it < MAXIT && now() - t0 < budget) {
 						const int rec = k >= 20;
 						double a = now(), w = 0, lat = 0;
+						int nburst = form == 1 ? k > 0 : 1; /* bursts this iteration processed */
 						int bad = 0;
 						uint8_t *tx = txh[k & 1];
 						if (form == 0) {
@@ -383,13 +391,16 @@ int main(int argc, char **argv)
 								goto fail;
 							int got = 0;
 							long cur = 0; /* this iteration's reply slots */
+							const long at = cf.cursor % (2 * MAXB);
+							const long gap = mix && at + R > 2 * MAXB ? 2 * MAXB - at : 0;
+							const long room = 2 * MAXB - (at + gap) % (2 * MAXB);
 							for (;;) {
 								const int pend = cgck_rx_pending();
 								const int rdy = pend ? cgck_rx_ready() : 0;
-								if (!pend || (rdy != 1 && pend < 48) || cur + R > 2 * MAXB)
+								if (!pend || (rdy != 1 && pend < 48) || (mix && cur + R > room))
 									break;
 								w0 = now();
-								while (cf.n > 0 && cf.busy + cur + R > 2 * MAXB)
+								while (cf.n > 0 && cf.busy + gap + cur + R > 2 * MAXB)
 									if (fill_done(&cf, mix, txh[0], &c) < 0)
 										goto fail;
 								if (cgck_rx_begin_posted() != R)
@@ -400,7 +411,8 @@ int main(int argc, char **argv)
 									uint8_t *ip = rx + (size_t)i * SLOT + L3;
 									bad += verify(ip, len, lib_in, lib_udp);
 									if (mix)
-										reply(txh[0] + (size_t)((cf.cursor + cur + i) % (2 * MAXB)) * SLOT +
+										reply(txh[0] + (size_t)((cf.cursor + gap + cur + i) % (2 * MAXB)) *
+												       SLOT +
 											      L3,
 										      ip, lib_in, lib_udp);
 								}
@@ -414,7 +426,8 @@ int main(int argc, char **argv)
 							}
 							bad = got ? (bad == got * expect ? expect : -1) : expect;
 							lat = got ? lat / got : 0;
-							fill_push(&cf, cur);
+							nburst = got;
+							fill_push(&cf, cur ? gap : 0, cur);
 						} else {
 							uint8_t *rx = rxh[k & 1];
 							cgck_tx_begin();
@@ -450,6 +463,8 @@ int main(int argc, char **argv)
 						}
 						c.bad_rx += bad != expect;
 						if (rec) {
+							c.total += now() - a - spun;
+							c.bursts += nburst;
 							c.worker[c.it] = now() - a - spun;
 							c.wait[c.it] = w;
 							c.it++;
@@ -471,9 +486,10 @@ int main(int argc, char **argv)
 					const double lm = pct(c.lat, c.itl, 50) * 1e6, l90 = pct(c.lat, c.itl, 90) * 1e6;
 					printf("{\"mode\": \"loop\", \"form\": \"%s\", \"mix\": \"%s\", \"pkt_len\": %d, "
 					       "\"burst\": %d, \"stack_ns_per_frame\": %.0f, \"stack_us_fixed\": %.0f, "
-					       "\"iters\": %d, \"us_worker\": %.3f, \"us_worker_p90\": %.3f, \"us_wait\": %.3f, "
+					       "\"iters\": %d, \"us_per_burst\": %.3f, \"us_worker\": %.3f, \"us_worker_p90\": %.3f, \"us_wait\": %.3f, "
 					       "\"us_latency\": %.3f, \"us_latency_p90\": %.3f, \"exact\": %s}\n",
-					       forms[form], mix ? "rx+reply" : "rx", len, R, ns, fixed_us, n, wm, w90, wt, lm,
+					       forms[form], mix ? "rx+reply" : "rx", len, R, ns, fixed_us, n,
+					       c.bursts ? c.total / c.bursts * 1e6 : 0.0, wm, w90, wt, lm,
 					       l90, c.bad_rx == 0 && c.bad_tx == 0 ? "true" : "false");
 					fflush(stdout);
 				}
