@@ -25,6 +25,8 @@ for step in "$@"; do
 	quick) run pytest_quick 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "burst or window or pipelined or rx_post or tx_" || exit 1 ;;
 	txburst) run txburst 400 tools/txburst 0.2 || exit 1 ;;
 	txloop) run txloop 400 tools/txloop 0.2 || exit 1 ;;
+	split) TXLOOP_SPLIT=1 run txloop_split 60 tools/txloop 0.5 || exit 1
+		TXLOOP_SPLIT=2 run txloop_split_reply 60 tools/txloop 0.5 || exit 1 ;;
 	e2e) run e2e 300 python -u tools/e2e.py || exit 1 ;;
 	lpdab) # lab lpd variants against the product kernel, one process each (64 B)
 		for cfg in "64 6 2" "64 5 2" "32 8 5" "64 6 5" "16 8 2"; do

@@ -154,10 +154,12 @@ struct cell {
 
 static in_fn ref_in;
 static udp_fn ref_udp;
+static double g_check; /* seconds spent checking replies (kept out of the worker's time) */
 
 /* replies of slots [0, R) checked against the reference's values */
 static int check_replies(const uint8_t *txh, int R)
 {
+	const double t0 = now();
 	int bad = 0;
 	const int idx[3] = {0, R / 2, R - 1};
 	for (int j = 0; j < 3; j++) {
@@ -173,6 +175,7 @@ static int check_replies(const uint8_t *txh, int R)
 		c[10] = c[11] = 0;
 		bad += ref_in(c, 20) != s_ip;
 	}
+	g_check += now() - t0;
 	return bad;
 }
 
@@ -307,6 +310,60 @@ int main(int argc, char **argv)
 	}
 	in_fn lib_in = (in_fn)in_cksum;
 	udp_fn lib_udp = (udp_fn)udp_cksum;
+	/* where a small burst's fixed cost goes: the coalesced loop at one frame
+	 * a burst and 250 ns of stack work a frame, each call timed (mean ns) */
+	if (getenv("TXLOOP_SPLIT")) {
+		const int R = 1, split_reply = atoi(getenv("TXLOOP_SPLIT")) == 2;
+		double acc[10] = {0};
+		long cnt[10] = {0}, k = 0, opened = 0;
+		static const char *nm[10] = {"tx_ready+complete", "tx_begin", "rx_post", "rx_pending+ready",
+					     "rx_begin_posted", "verify (+reply) calls", "rx_end", "tx_post", "spin", "iteration"};
+		const double t0 = now();
+		while (now() - t0 < budget * 4) {
+			double a = now(), b;
+			const double it0 = a;
+			while (cgck_tx_pending() > 0 && cgck_tx_ready() == 1)
+				cgck_tx_complete();
+			b = now(); acc[0] += b - a; cnt[0]++; a = b;
+			cgck_tx_begin();
+			b = now(); acc[1] += b - a; cnt[1]++; a = b;
+			cgck_rx_post(pool, pool_bytes, descs[k & 1], R);
+			b = now(); acc[2] += b - a; cnt[2]++; a = b;
+			for (;;) {
+				const int pend = cgck_rx_pending();
+				const int rdy = pend ? cgck_rx_ready() : 0;
+				b = now(); acc[3] += b - a; cnt[3]++; a = b;
+				if (!pend || (rdy != 1 && pend < 48))
+					break;
+				cgck_rx_begin_posted();
+				b = now(); acc[4] += b - a; cnt[4]++; a = b;
+				verify(rxh[opened & 1] + L3, len, lib_in, lib_udp);
+				if (split_reply)
+					reply(txh[k & 1] + L3, rxh[opened & 1] + L3, lib_in, lib_udp);
+				b = now(); acc[5] += b - a; cnt[5]++; a = b;
+				cgck_rx_end();
+				b = now(); acc[6] += b - a; cnt[6]++; a = b;
+				opened++;
+			}
+			cgck_tx_post();
+			b = now(); acc[7] += b - a; cnt[7]++; a = b;
+			spin(250e-9);
+			b = now(); acc[8] += b - a; cnt[8]++;
+			acc[9] += b - it0;
+			cnt[9]++;
+			k++;
+		}
+		while (cgck_rx_pending() > 0 && cgck_rx_begin_posted() >= 0)
+			cgck_rx_end();
+		while (cgck_tx_pending() > 0)
+			cgck_tx_complete();
+		printf("{\"mode\": \"split\", \"reply\": %d, \"burst\": 1, \"iterations\": %ld, \"bursts_opened\": %ld",
+		       split_reply, k, opened);
+		for (int i = 0; i < 10; i++)
+			printf(", \"%s_ns\": %.1f", nm[i], cnt[i] ? acc[i] / cnt[i] * 1e9 : 0.0);
+		printf("}\n");
+		return 0;
+	}
 	static const char *forms[4] = {"reference", "pipelined", "sync", "coalesced"};
 	for (int mix = 0; mix < 2; mix++) {
 		for (int bud = 0; bud <= nns; bud++) {
@@ -326,6 +383,7 @@ int main(int argc, char **argv)
 					const double t0 = now();
 					while (c.it < MAXIT && now() - t0 < budget) {
 						const int rec = k >= 20;
+						g_check = 0;
 						double a = now(), w = 0, lat = 0;
 						int nburst = form == 1 ? k > 0 : 1; /* bursts this iteration processed */
 						int bad = 0;
@@ -463,9 +521,9 @@ int main(int argc, char **argv)
 						}
 						c.bad_rx += bad != expect;
 						if (rec) {
-							c.total += now() - a - spun;
+							c.total += now() - a - spun - g_check;
 							c.bursts += nburst;
-							c.worker[c.it] = now() - a - spun;
+							c.worker[c.it] = now() - a - spun - g_check;
 							c.wait[c.it] = w;
 							c.it++;
 							if (lat > 0) /* (the coalesced form: iterations that opened bursts) */
