@@ -642,7 +642,7 @@ static int burst_slot_free(cgck_ctx *c, uint8_t **block)
 // Post the request whose descriptors (and, for base_dev == nullptr, packet
 // bytes) are in the next block; returns its seq.
 static int burst_post(cgck_ctx *c, const uint8_t *base_dev, uint64_t range, uint64_t n, uint32_t flags,
-		      uint32_t max_len, const BurstLayout &L, uint32_t *seq_out)
+		      uint32_t max_len, const BurstLayout &L, uint32_t *seq_out, const DescSplit *split = nullptr)
 {
 	std::shared_lock<std::shared_mutex> map_lk(g_map_mu);
 	BurstBox *b = c->bbox;
@@ -656,6 +656,8 @@ static int burst_post(cgck_ctx *c, const uint8_t *base_dev, uint64_t range, uint
 	r->range = base_dev ? range : 0;
 	r->d_off = (uint32_t)L.d_off;
 	r->p_off = (uint32_t)L.p_off;
+	r->n1 = split ? split->n1 : 0;
+	r->flags2 = split ? split->flags2 : 0;
 	c->bseq = seq;
 #if CGCK_LAB
 	t_lab_host[0] = (uint64_t)(now_s() * 1e9);
@@ -724,10 +726,12 @@ static void *registered_ptr(void *p, size_t bytes)
 // per-descriptor pass is skipped.
 static int desc_host_impl(cgck_ctx *c, void *base, size_t bytes, const cgck_desc_t *desc, uint64_t n, uint32_t flags,
 			  uint32_t *out, uint8_t *verdict, uint32_t *meta, BurstPending *pend,
-			  const DescSummary *sum = nullptr)
+			  const DescSummary *sum = nullptr, const DescSplit *split = nullptr)
 {
 	if (n == 0)
 		return 0;
+	if (split && (split->n1 == 0 || split->n1 >= n))
+		split = nullptr;
 	if (!base || !desc)
 		return set_err(-EINVAL, "cgck_desc_host: NULL base or descriptors");
 	size_t pkt_bytes = sum ? sum->pkt_bytes : 0;
@@ -784,7 +788,8 @@ static int desc_host_impl(cgck_ctx *c, void *base, size_t bytes, const cgck_desc
 			}
 		}
 		uint32_t seq;
-		if ((rc = burst_post(c, in_place ? (const uint8_t *)dev_base : nullptr, bytes, n, flags, max_len, L, &seq)))
+		if ((rc = burst_post(c, in_place ? (const uint8_t *)dev_base : nullptr, bytes, n, flags, max_len, L, &seq,
+				     split)))
 			return rc;
 		BurstPending now;
 		BurstPending *q = pend ? pend : &now;
@@ -800,6 +805,15 @@ static int desc_host_impl(cgck_ctx *c, void *base, size_t bytes, const cgck_desc
 			return 1;
 		}
 		return burst_collect(c, &now);
+	}
+	if (split) {
+		// a two-part request the server cannot take: each part computed at
+		// once on its own (the launch path takes one flag set)
+		const uint32_t n1 = split->n1;
+		if ((rc = desc_host_impl(c, base, bytes, desc, n1, flags, out, verdict, meta, nullptr)))
+			return rc;
+		return desc_host_impl(c, base, bytes, desc + n1, n - n1, split->flags2, out ? out + n1 : nullptr,
+				      verdict ? verdict + n1 : nullptr, nullptr, nullptr);
 	}
 	if (dev_base || pkt_bytes <= kStageBytes) {
 		// pinned staging: [packets (staged case)] | descriptors | out | meta | verdict
@@ -888,11 +902,12 @@ int cgck::desc_host(cgck_ctx *c, void *base, size_t bytes, const cgck_desc_t *de
 }
 
 int cgck::desc_host_post(cgck_ctx *c, void *base, size_t bytes, const cgck_desc_t *desc, uint64_t n, uint32_t flags,
-			 uint32_t *out, uint8_t *verdict, uint32_t *meta, BurstPending *pend, const DescSummary *sum)
+			 uint32_t *out, uint8_t *verdict, uint32_t *meta, BurstPending *pend, const DescSummary *sum,
+			 const DescSplit *split)
 {
 	pend->seq = 0;
 	pend->rc = 0;
-	return desc_host_impl(c, base, bytes, desc, n, flags, out, verdict, meta, pend, sum);
+	return desc_host_impl(c, base, bytes, desc, n, flags, out, verdict, meta, pend, sum, split);
 }
 
 extern "C" int cgck_desc_host(cgck_ctx_t *c, void *base, size_t bytes, const cgck_desc_t *desc,

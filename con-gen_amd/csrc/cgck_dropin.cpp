@@ -155,16 +155,15 @@ struct PostItem {
 	bool own = false;
 };
 
+// One kind's posted items (receive bursts or TX fills), oldest first; the
+// requests that carry them belong to the thread's Poster.
 struct PostQueue {
 	PostItem it[kPostQ];
-	PostReq rq[kPostQ]; // each carries >= 1 item: never more live than items
 	unsigned head = 0, count = 0, sent = 0; // oldest item; items posted; of them sent (oldest first)
-	unsigned rhead = 0, rcount = 0;
-	int inflight = -1; // the request in flight
-	bool meta = false; // requests return meta words (RX)
 
 	PostItem &at(unsigned k) { return it[(head + k) % kPostQ]; }
 	PostItem &oldest() { return it[head]; }
+	const PostItem &oldest() const { return it[head]; }
 	unsigned next_slot() const { return (head + count) % kPostQ; }
 	PostItem &push()
 	{
@@ -178,15 +177,32 @@ struct PostQueue {
 		x.max_len = 0;
 		return x;
 	}
+};
+
+// The thread's two queues and the burst-server requests that carry them.
+// One request per kind is in flight; what is posted meanwhile goes out when
+// it is back.  When both kinds have items waiting over the same registered
+// range, they go out as ONE two-part request (BurstReq.n1: the receive
+// frames, then the fill's packets, each with its own flags), so a loop that
+// posts a burst and a fill every iteration pays one mailbox round trip for
+// both.
+enum { kRx = 0, kTx = 1 };
+struct Poster {
+	PostQueue q[2];
+	PostReq rq[2 * kPostQ]; // each carries >= 1 item: never more live than items
+	unsigned rhead = 0, rcount = 0;
+	int inflight[2] = {-1, -1}; // the request carrying each kind's sent items (one, when fused)
+
 	bool done(const PostItem &x) const { return x.own || (x.req >= 0 && rq[x.req].done); }
 	int rc_of(const PostItem &x) const { return x.own ? 0 : rq[x.req].rc; }
 	const char *msg_of(const PostItem &x) const { return x.own ? "" : rq[x.req].msg; }
 	const uint32_t *values(const PostItem &x) const { return x.own ? x.vals.data() : rq[x.req].o.data() + x.off; }
 	const uint32_t *metas(const PostItem &x) const { return x.own ? nullptr : rq[x.req].m.data() + x.off; }
 	void send(cgck_ctx *c);
-	void pump(cgck_ctx *c, bool wait);
-	int settle(cgck_ctx *c, bool wait);
-	void pop();
+	void collect(cgck_ctx *c, int ri);
+	void pump(cgck_ctx *c, int kind, bool wait);
+	int settle(cgck_ctx *c, int kind, bool wait);
+	void pop(int kind);
 };
 
 // TX fill bookkeeping beside its PostItem (same slot): the queued fields,
@@ -212,8 +228,7 @@ struct ThreadState {
 	PtrMap txidx; // (ip << 1 | is_l4) -> txq index
 	TxFill txs;       // cgck_tx_flush's batch
 	PostItem txs_item;
-	PostQueue txpq;   // posted fills (cgck_tx_post)
-	TxFill txf[kPostQ]; // their bookkeeping, slot for slot
+	TxFill txf[kPostQ]; // the posted fills' bookkeeping, slot for slot with post.q[kTx]
 	// The window in its fast form, while every call is at or above the
 	// highest header so far and inside one registered range (txd_ok): no
 	// txq entries, only one descriptor per packet, its header and segment
@@ -251,7 +266,7 @@ struct ThreadState {
 	bool rx_span_built = false;
 	uintptr_t rx_lo = 0, rx_hi = 0;
 	RxBurst rxs;      // cgck_rx_begin's burst
-	PostQueue rxpq;   // posted bursts (cgck_rx_post)
+	Poster post;      // posted bursts (cgck_rx_post) and fills (cgck_tx_post)
 	uint64_t rx_served0 = 0; // stats[0] at rx_begin
 	uint64_t stats[4] = {0, 0, 0, 0};
 	// the registered range of the last TX-window hit, valid while g_reg_gen
@@ -752,107 +767,156 @@ namespace {
 
 constexpr uint32_t kRxFlags = CGCK_IP | CGCK_L4 | CGCK_ZERO_FIELDS | kFlagL4Auto | kFlagRx;
 
-// Send the items posted and not sent yet, oldest first, as one request: as
-// many as share the first one's range and flags and fit the burst server
-// (its max_pkts and max_bytes; without a server the request is a launch,
-// computed at once).  Items computed at their post are stepped over.
-void PostQueue::send(cgck_ctx *c)
-{
-	while (sent < count && at(sent).own)
-		sent++;
-	if (sent == count)
-		return;
-	const PostItem &f = at(sent);
-	const uint64_t cap_n = c->bbox ? c->bmax : UINT64_MAX;
-	const size_t cap_b = c->bbox ? c->bmax_bytes : SIZE_MAX;
-	uint64_t n = 0;
+// The unsent items of one kind that go out together: as many as share the
+// first one's range and flags and fit what is left of the server's caps
+// (without a server the request is a launch, computed at once).  Items
+// computed at their post are stepped over.
+struct Group {
+	unsigned s = 0, e = 0; // items [s, e) of the queue (from its oldest)
+	uint64_t n = 0;        // descriptors
 	size_t pb = 0;
 	uint32_t ml = 0;
-	unsigned k = sent;
-	for (; k < count; k++) {
-		const PostItem &x = at(k);
-		if (x.own || x.base != f.base || x.bytes != f.bytes || x.flags != f.flags)
+	const PostItem *f = nullptr;
+};
+
+static Group gather(PostQueue &q, uint64_t cap_n, size_t cap_b)
+{
+	Group g;
+	while (q.sent < q.count && q.at(q.sent).own)
+		q.sent++;
+	g.s = g.e = q.sent;
+	if (q.sent == q.count)
+		return g;
+	g.f = &q.at(q.sent);
+	for (unsigned k = q.sent; k < q.count; k++) {
+		const PostItem &x = q.at(k);
+		if (x.own || x.base != g.f->base || x.bytes != g.f->bytes || x.flags != g.f->flags)
 			break;
-		if (k > sent && (n + x.n > cap_n || pb + x.pkt_bytes > cap_b))
+		if (k > q.sent && (g.n + x.n > cap_n || g.pb + x.pkt_bytes > cap_b))
 			break;
-		n += x.n;
-		pb += x.pkt_bytes;
-		ml = x.max_len > ml ? x.max_len : ml;
+		g.n += x.n;
+		g.pb += x.pkt_bytes;
+		g.ml = x.max_len > g.ml ? x.max_len : g.ml;
+		g.e = k + 1;
 	}
-	const int ri = (int)((rhead + rcount) % kPostQ);
-	rcount++;
-	PostReq &r = rq[ri];
-	r.d.clear();
-	for (unsigned j = sent; j < k; j++) {
-		PostItem &x = at(j);
-		x.req = ri;
-		x.off = (uint32_t)r.d.size();
-		r.d.insert(r.d.end(), x.d.begin(), x.d.end());
-	}
-	r.o.resize(n);
-	if (meta)
+	return g;
+}
+
+// Send what each kind with nothing in flight has waiting: both kinds as one
+// two-part request when they share the range (the receive frames first, so
+// their meta words come back too), else one request each.
+void Poster::send(cgck_ctx *c)
+{
+	const uint64_t cap_n = c->bbox ? c->bmax : UINT64_MAX;
+	const size_t cap_b = c->bbox ? c->bmax_bytes : SIZE_MAX;
+	Group g[2];
+	for (int k = 0; k < 2; k++)
+		if (inflight[k] < 0)
+			g[k] = gather(q[k], cap_n, cap_b);
+	// one request when both fit the server together (else one each)
+	const bool fuse = g[kRx].f && g[kTx].f && c->bbox && g[kRx].f->base == g[kTx].f->base &&
+			  g[kRx].f->bytes == g[kTx].f->bytes && g[kRx].n + g[kTx].n <= cap_n &&
+			  g[kRx].pb + g[kTx].pb <= cap_b;
+	for (int k = 0; k < 2; k++) {
+		if (!g[k].f || (fuse && k == kTx))
+			continue;
+		const int parts = fuse ? 2 : 1;
+		const int ri = (int)((rhead + rcount) % (2 * kPostQ));
+		rcount++;
+		PostReq &r = rq[ri];
+		r.d.clear();
+		r.items = 0;
+		for (int pk = k; pk < k + parts; pk++) {
+			PostQueue &qq = q[pk];
+			for (unsigned j = g[pk].s; j < g[pk].e; j++) {
+				PostItem &x = qq.at(j);
+				if (x.own)
+					continue;
+				x.req = ri;
+				x.off = (uint32_t)r.d.size();
+				r.d.insert(r.d.end(), x.d.begin(), x.d.end());
+				r.items++;
+			}
+			qq.sent = g[pk].e;
+			inflight[pk] = ri;
+		}
+		const uint64_t n = r.d.size();
+		r.o.resize(n);
 		r.m.resize(n);
-	r.items = k - sent;
-	r.done = false;
-	r.rc = 0;
-	r.msg[0] = 0;
-	sent = k;
-	const DescSummary sum = {ml, pb};
-	const int rc = desc_host_post(c, const_cast<uint8_t *>(f.base), f.bytes, r.d.data(), n, f.flags, r.o.data(),
-				      nullptr, meta ? r.m.data() : nullptr, &r.pend, &sum);
-	if (rc < 0) {
-		r.rc = rc;
-		snprintf(r.msg, sizeof(r.msg), "%s", err_text());
-		r.done = true;
-	} else if (rc == 1) {
-		inflight = ri;
-	} else {
-		r.done = true;
+		r.done = false;
+		r.rc = 0;
+		r.msg[0] = 0;
+		const DescSummary sum = {g[k].ml > g[kTx].ml || !fuse ? g[k].ml : g[kTx].ml,
+					 g[k].pb + (fuse ? g[kTx].pb : 0)};
+		const DescSplit split = {(uint32_t)g[kRx].n, fuse ? g[kTx].f->flags : 0u};
+		const int rc = desc_host_post(c, const_cast<uint8_t *>(g[k].f->base), g[k].f->bytes, r.d.data(), n,
+					      g[k].f->flags, r.o.data(), nullptr, k == kRx ? r.m.data() : nullptr, &r.pend,
+					      &sum, fuse ? &split : nullptr);
+		if (rc < 0) {
+			r.rc = rc;
+			snprintf(r.msg, sizeof(r.msg), "%s", err_text());
+			r.done = true;
+		} else if (rc == 0) {
+			r.done = true;
+		}
+		if (r.done)
+			for (int pk = k; pk < k + parts; pk++)
+				inflight[pk] = -1;
 	}
 }
 
-// Collect the request in flight once it is back (wait: wait for it), then
-// send what was posted meanwhile.
-void PostQueue::pump(cgck_ctx *c, bool wait)
+// Collect request ri (waiting for it if it is not back).
+void Poster::collect(cgck_ctx *c, int ri)
 {
-	if (inflight >= 0) {
-		PostReq &r = rq[inflight];
-		if (!wait && !burst_ready(c, &r.pend))
-			return;
-		r.rc = r.pend.seq ? burst_collect(c, &r.pend) : r.pend.rc;
-		if (r.rc)
-			snprintf(r.msg, sizeof(r.msg), "%s", err_text());
-		r.done = true;
-		inflight = -1;
+	PostReq &r = rq[ri];
+	r.rc = r.pend.seq ? burst_collect(c, &r.pend) : r.pend.rc;
+	if (r.rc)
+		snprintf(r.msg, sizeof(r.msg), "%s", err_text());
+	r.done = true;
+	for (int k = 0; k < 2; k++)
+		if (inflight[k] == ri)
+			inflight[k] = -1;
+}
+
+// Collect the requests in flight that are back (wait: also `kind`'s, once
+// it is back), then send what was posted meanwhile.
+void Poster::pump(cgck_ctx *c, int kind, bool wait)
+{
+	for (int k = 0; k < 2; k++) {
+		const int ri = inflight[k];
+		if (ri >= 0 && ((wait && k == kind) || burst_ready(c, &rq[ri].pend)))
+			collect(c, ri);
 	}
-	if (sent < count)
+	if (q[kRx].sent < q[kRx].count || q[kTx].sent < q[kTx].count)
 		send(c);
 }
 
 // Are the oldest item's values in (1), or not yet (0)?  wait: until they are.
-int PostQueue::settle(cgck_ctx *c, bool wait)
+int Poster::settle(cgck_ctx *c, int kind, bool wait)
 {
-	pump(c, false);
-	while (!done(oldest())) {
+	pump(c, kind, false);
+	while (!done(q[kind].oldest())) {
 		if (!wait)
 			return 0;
-		pump(c, true);
+		pump(c, kind, true);
 	}
 	return 1;
 }
 
-// The oldest item consumed; requests all of whose items are consumed free.
-void PostQueue::pop()
+// The oldest item of a kind consumed; requests all of whose items are
+// consumed free, oldest first.
+void Poster::pop(int kind)
 {
-	PostItem &x = oldest();
+	PostQueue &qq = q[kind];
+	PostItem &x = qq.oldest();
 	if (x.req >= 0)
 		rq[x.req].items--;
-	head = (head + 1) % kPostQ;
-	count--;
-	if (sent)
-		sent--;
+	qq.head = (qq.head + 1) % kPostQ;
+	qq.count--;
+	if (qq.sent)
+		qq.sent--;
 	while (rcount && rq[rhead].done && rq[rhead].items == 0) {
-		rhead = (rhead + 1) % kPostQ;
+		rhead = (rhead + 1) % (2 * kPostQ);
 		rcount--;
 	}
 }
@@ -928,7 +992,7 @@ extern "C" int cgck_rx_begin(void *base, size_t bytes, const cgck_desc_t *desc, 
 extern "C" int cgck_rx_post(void *base, size_t bytes, const cgck_desc_t *desc, uint64_t n)
 {
 	ThreadState &t = tstate();
-	PostQueue &q = t.rxpq;
+	PostQueue &q = t.post.q[kRx];
 	if (q.count == kPostQ)
 		return set_err(-EBUSY, "cgck_rx_post: %u bursts already posted and not yet opened", kPostQ);
 	int rc = rx_check(base, desc, n, "cgck_rx_post");
@@ -947,7 +1011,6 @@ extern "C" int cgck_rx_post(void *base, size_t bytes, const cgck_desc_t *desc, u
 		ml = desc[i].ip_len > ml ? desc[i].ip_len : ml;
 		pb += ((size_t)desc[i].ip_len + 15) & ~(size_t)15;
 	}
-	q.meta = true;
 	PostItem &x = q.push();
 	x.base = (const uint8_t *)base;
 	x.bytes = bytes;
@@ -958,28 +1021,28 @@ extern "C" int cgck_rx_post(void *base, size_t bytes, const cgck_desc_t *desc, u
 	x.max_len = ml;
 	x.own = n == 0;
 	x.vals.clear();
-	q.pump(c, false);
+	t.post.pump(c, kRx, false);
 	return (int)n;
 }
 
 extern "C" int cgck_rx_begin_posted(void)
 {
 	ThreadState &t = tstate();
-	PostQueue &q = t.rxpq;
+	Poster &P = t.post;
 	if (t.rx_open)
 		return set_err(-EBUSY, "cgck_rx_begin_posted: an RX window is already open on this thread");
-	if (q.count == 0)
+	if (P.q[kRx].count == 0)
 		return set_err(-ENOENT, "cgck_rx_begin_posted: no burst posted");
-	q.settle(t.ctx, true);
-	const PostItem &x = q.oldest();
-	if (const int rc = q.rc_of(x)) {
+	P.settle(t.ctx, kRx, true);
+	const PostItem &x = P.q[kRx].oldest();
+	if (const int rc = P.rc_of(x)) {
 		char msg[200];
-		snprintf(msg, sizeof(msg), "%s", q.msg_of(x));
-		q.pop();
+		snprintf(msg, sizeof(msg), "%s", P.msg_of(x));
+		P.pop(kRx);
 		return set_err(rc, "cgck_rx_begin_posted: %s", msg);
 	}
 	static const uint32_t none = 0;
-	return rx_open_on(t, x.base, x.n, x.d.data(), x.n ? q.values(x) : &none, x.n ? q.metas(x) : &none, true);
+	return rx_open_on(t, x.base, x.n, x.d.data(), x.n ? P.values(x) : &none, x.n ? P.metas(x) : &none, true);
 }
 
 // The drain rule's two questions (include/cgck.h): is a burst still posted,
@@ -987,15 +1050,15 @@ extern "C" int cgck_rx_begin_posted(void)
 extern "C" int cgck_rx_pending(void)
 {
 	const ThreadState *t = t_st;
-	return t ? (int)t->rxpq.count : 0;
+	return t ? (int)t->post.q[kRx].count : 0;
 }
 
 extern "C" int cgck_rx_ready(void)
 {
 	ThreadState *t = t_st;
-	if (!t || t->rxpq.count == 0)
+	if (!t || t->post.q[kRx].count == 0)
 		return set_err(-ENOENT, "cgck_rx_ready: no burst posted");
-	return t->rxpq.settle(t->ctx, false);
+	return t->post.settle(t->ctx, kRx, false);
 }
 
 extern "C" int cgck_rx_end(void)
@@ -1008,7 +1071,7 @@ extern "C" int cgck_rx_end(void)
 	t.rx_map = false;
 	if (t.rx_posted) {
 		t.rx_posted = false;
-		t.rxpq.pop();
+		t.post.pop(kRx);
 	}
 	return (int)(t.stats[0] - t.rx_served0);
 }
@@ -1252,7 +1315,7 @@ extern "C" int cgck_tx_post(void)
 	ThreadState &t = tstate();
 	if (!t.tx_open)
 		return set_err(-EINVAL, "cgck_tx_post: no open window on this thread");
-	PostQueue &q = t.txpq;
+	PostQueue &q = t.post.q[kTx];
 	if (q.count == kPostQ) {
 		// The queue is full: the oldest fill completes first (its fields
 		// are written now, before the kick that was to wait for them —
@@ -1280,43 +1343,44 @@ extern "C" int cgck_tx_post(void)
 		f.q.clear();
 		return rc;
 	}
-	q.pump(c, false);
+	t.post.pump(c, kTx, false);
 	return f.n;
 }
 
 extern "C" int cgck_tx_complete(void)
 {
 	ThreadState &t = tstate();
-	PostQueue &q = t.txpq;
+	Poster &P = t.post;
+	PostQueue &q = P.q[kTx];
 	if (q.count == 0)
 		return 0;
-	q.settle(t.ctx, true);
+	P.settle(t.ctx, kTx, true);
 	const PostItem &x = q.oldest();
 	TxFill &f = t.txf[q.head];
-	if (const int rc = q.rc_of(x)) {
+	if (const int rc = P.rc_of(x)) {
 		char msg[200];
-		snprintf(msg, sizeof(msg), "%s", q.msg_of(x));
+		snprintf(msg, sizeof(msg), "%s", P.msg_of(x));
 		f.q.clear();
-		q.pop();
+		P.pop(kTx);
 		return set_err(rc, "cgck_tx_complete: %s", msg);
 	}
-	const int n = f.n == 0 ? 0 : f.fast ? tx_write_fast(f, x, q.values(x)) : tx_write(f, q.values(x));
-	q.pop();
+	const int n = f.n == 0 ? 0 : f.fast ? tx_write_fast(f, x, P.values(x)) : tx_write(f, P.values(x));
+	P.pop(kTx);
 	return n;
 }
 
 extern "C" int cgck_tx_pending(void)
 {
 	const ThreadState *t = t_st;
-	return t ? (int)t->txpq.count : 0;
+	return t ? (int)t->post.q[kTx].count : 0;
 }
 
 extern "C" int cgck_tx_ready(void)
 {
 	ThreadState *t = t_st;
-	if (!t || t->txpq.count == 0)
+	if (!t || t->post.q[kTx].count == 0)
 		return set_err(-ENOENT, "cgck_tx_ready: no fill posted");
-	return t->txpq.settle(t->ctx, false);
+	return t->post.settle(t->ctx, kTx, false);
 }
 
 // --------------------------------------------------------------------------

@@ -272,16 +272,34 @@ __device__ __forceinline__ uint64_t sys_relaxed64(const uint64_t *p)
 // The group body over a request's packets [lo, hi) (block 0 of 1); desc is
 // packet lo's descriptor (in LDS when LDSD).
 template <bool LDSD>
-__device__ __forceinline__ void burst_body(const BurstReq &h, const uint32_t *desc, uint32_t lo, uint32_t hi,
-					   uint32_t *out, uint32_t *meta, uint8_t *verdict, const void *zero,
-					   const uint8_t *base)
+__device__ __forceinline__ void burst_part(const BurstReq &h, uint32_t flags, const uint32_t *desc, uint32_t lo,
+					   uint32_t hi, uint32_t *out, uint32_t *meta, uint8_t *verdict,
+					   const void *zero, const uint8_t *base)
 {
-	KParams p = {base, reinterpret_cast<const cgck_desc_t *>(desc), hi - lo, 0, 0, 0, h.flags,
+	KParams p = {base, reinterpret_cast<const cgck_desc_t *>(desc), hi - lo, 0, 0, 0, flags,
 		     out ? out + lo : nullptr, verdict ? verdict + lo : nullptr, nullptr, 0, zero, meta + lo};
 	if (h.max_len <= 80)
 		cksum_body<4, 2, 4, true, false, LDSD>(p, 0, 1);
 	else
 		cksum_body<16, 6, 4, true, false, LDSD>(p, 0, 1);
+}
+
+// A request may carry two parts (a receive burst's frames, then a TX fill's
+// packets: BurstReq.n1): packets [lo, hi) on either side of n1 run with that
+// part's flags.
+template <bool LDSD>
+__device__ __forceinline__ void burst_body(const BurstReq &h, const uint32_t *desc, uint32_t lo, uint32_t hi,
+					   uint32_t *out, uint32_t *meta, uint8_t *verdict, const void *zero,
+					   const uint8_t *base)
+{
+	const uint32_t n1 = h.n1 < h.n ? h.n1 : 0;
+	if (n1 > lo && n1 < hi) {
+		burst_part<LDSD>(h, h.flags, desc, lo, n1, out, meta, verdict, zero, base);
+		__syncthreads(); // (the body's LDS staging is reused)
+		burst_part<LDSD>(h, h.flags2, desc + 3 * (n1 - lo), n1, hi, out, meta, verdict, zero, base);
+	} else {
+		burst_part<LDSD>(h, n1 && lo >= n1 ? h.flags2 : h.flags, desc, lo, hi, out, meta, verdict, zero, base);
+	}
 }
 
 // A request header the server can serve: the count it was told, inside the

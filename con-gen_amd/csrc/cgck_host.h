@@ -117,9 +117,13 @@ struct DescSummary {
 	uint32_t max_len;
 	size_t pkt_bytes;
 };
+// A request in two parts: descriptors [n1, n) take flags2 (BurstReq.n1).
+struct DescSplit {
+	uint32_t n1, flags2;
+};
 int desc_host_post(cgck_ctx *c, void *base, size_t bytes, const cgck_desc_t *desc, uint64_t n, uint32_t flags,
 		   uint32_t *out, uint8_t *verdict, uint32_t *meta, BurstPending *pend,
-		   const DescSummary *sum = nullptr);
+		   const DescSummary *sum = nullptr, const DescSplit *split = nullptr);
 int burst_collect(cgck_ctx *c, BurstPending *pend);
 // Without waiting: is the posted request's every slice served (1), or not
 // yet (0)?  A request that was computed at once (seq 0) is ready.

@@ -130,7 +130,9 @@ struct BurstReq {
 	uint32_t d_off;   // descriptors: offset in the block
 	uint32_t p_off;   // packet bytes (base == 0): offset in the block
 	uint64_t range;   // base != 0: bytes readable from base; the server refuses a descriptor past it
-	uint32_t pad[6];
+	uint32_t n1;      // 0 < n1 < n: descriptors [n1, n) take flags2 (a receive burst and a TX
+	uint32_t flags2;  // fill sharing one request); 0: every descriptor takes flags
+	uint32_t pad[4];
 };
 static_assert(sizeof(BurstReq) == 64, "one header line");
 constexpr uint32_t kBurstFirst = 8192;

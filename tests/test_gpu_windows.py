@@ -1034,3 +1034,72 @@ def test_tx_coalesced_fills(port, server):
         if server:
             cgck.burst_close()
         L.cgck_host_unregister(ring.ctypes.data)
+
+
+def test_rx_tx_fused_coalesced(port):
+    """Receive bursts and TX fills posted over ONE registered pool on a random
+    schedule, both queues deep: what waits in both queues when the server
+    answers goes out as one two-part request (the frames with the RX flags,
+    the fill's packets with the TX flags).  Every burst replays bit-exact
+    against the reference, every fill's fields equal the reference's, in
+    post order on each side."""
+    R = referee(port)
+    L = cgck.load()
+    rng = np.random.default_rng(7300)
+    sizes = [int(rng.integers(1, 5)) for _ in range(70)]
+    frames = rxcorpus.corpus(rng, R, sum(sizes), clean=True)
+    buf, desc_all, tx_base, tx_stride = rxcorpus.pool(frames, 400)
+    raw, pool, size = rxcorpus.registered_copy(buf)
+    assert L.cgck_host_register(pool.ctypes.data, size) == 0
+    got = pool[:len(buf)]
+    ref = buf.copy()
+    descs, at = [], 0
+    for s in sizes:
+        descs.append(desc_all[at:at + s].copy())
+        at += s
+    slot = lambda j: got[tx_base + j * tx_stride:tx_base + j * tx_stride + 2048]
+    cgck.burst_open(max_pkts=1024, max_bytes=4 << 20)
+    posted = opened = 0
+    fills, completed, next_tx = [], 0, 0
+    try:
+        while opened < len(sizes) or completed < len(fills):
+            if posted < len(sizes) and posted - opened < 60 and rng.random() < 0.6:
+                assert cgck.rx_post(got, descs[posted]) == sizes[posted]
+                posted += 1
+            if next_tx < 380 and len(fills) - completed < 60 and rng.random() < 0.6:
+                want = []
+                cgck.tx_begin()
+                for _ in range(int(rng.integers(1, 4))):
+                    ln = int(rng.integers(40, 600))
+                    pkt = tcp_pkt(rng, ln)
+                    row = slot(next_tx)
+                    row[14:14 + ln] = pkt
+                    want.append((next_tx, ln, expected(port, pkt, 16)))
+                    tx_calls(row, ln, 16)
+                    next_tx += 1
+                assert cgck.tx_post() == 2 * len(want)
+                fills.append(want)
+            if posted > opened and (rng.random() < 0.3 or posted == len(sizes)):
+                stack, ip_in, tcp_in = cell = FLAGS[(opened * 7) % len(FLAGS)]
+                d = descs[opened]
+                a = port.replay_rx(*R.fn_pointers(), ref, d.view(np.uint8), len(d), stack, ip_in, tcp_in)
+                cgck.rx_begin_posted()
+                try:
+                    b = port.replay_rx(*cgck.fn_pointers(), got, d.view(np.uint8), len(d), stack, ip_in, tcp_in)
+                finally:
+                    cgck.rx_end()
+                assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]), (opened, cell)
+                opened += 1
+            if len(fills) > completed and (rng.random() < 0.3 or next_tx >= 380):
+                assert cgck.tx_complete() == 2 * len(fills[completed])
+                for j, ln, r in fills[completed]:
+                    assert np.array_equal(slot(j)[14:14 + ln], r), (completed, j)
+                completed += 1
+        assert cgck.rx_pending() == 0 and cgck.tx_pending() == 0
+        # the receive frames as the reference left them (the transmit slots differ by design)
+        for d in descs:
+            for o, l3, ln in d.tolist():
+                assert np.array_equal(got[o:o + l3 + ln], ref[o:o + l3 + ln])
+    finally:
+        cgck.burst_close()
+        L.cgck_host_unregister(pool.ctypes.data)

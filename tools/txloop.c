@@ -314,7 +314,8 @@ int main(int argc, char **argv)
 	 * a burst and 250 ns of stack work a frame, each call timed (mean ns) */
 	if (getenv("TXLOOP_SPLIT")) {
 		const int R = 1, split_reply = atoi(getenv("TXLOOP_SPLIT")) == 2;
-		double acc[10] = {0};
+		double acc[10] = {0}, slow_t = 0;
+		long slow_n = 0, forced = 0, maxpend = 0;
 		long cnt[10] = {0}, k = 0, opened = 0;
 		static const char *nm[10] = {"tx_ready+complete", "tx_begin", "rx_post", "rx_pending+ready",
 					     "rx_begin_posted", "verify (+reply) calls", "rx_end", "tx_post", "spin", "iteration"};
@@ -335,8 +336,15 @@ int main(int argc, char **argv)
 				b = now(); acc[3] += b - a; cnt[3]++; a = b;
 				if (!pend || (rdy != 1 && pend < 48))
 					break;
+				forced += rdy != 1;
+				maxpend = pend > maxpend ? pend : maxpend;
 				cgck_rx_begin_posted();
-				b = now(); acc[4] += b - a; cnt[4]++; a = b;
+				b = now(); acc[4] += b - a; cnt[4]++;
+				if (b - a > 1e-6) { /* the opens that waited (or collected) */
+					slow_n++;
+					slow_t += b - a;
+				}
+				a = b;
 				verify(rxh[opened & 1] + L3, len, lib_in, lib_udp);
 				if (split_reply)
 					reply(txh[k & 1] + L3, rxh[opened & 1] + L3, lib_in, lib_udp);
@@ -361,6 +369,8 @@ int main(int argc, char **argv)
 		       split_reply, k, opened);
 		for (int i = 0; i < 10; i++)
 			printf(", \"%s_ns\": %.1f", nm[i], cnt[i] ? acc[i] / cnt[i] * 1e9 : 0.0);
+		printf(", \"opens_over_1us\": %ld, \"their_mean_us\": %.2f, \"opens_not_ready\": %ld, \"max_pending\": %ld",
+		       slow_n, slow_n ? slow_t / slow_n * 1e6 : 0.0, forced, maxpend);
 		printf("}\n");
 		return 0;
 	}
