@@ -224,7 +224,8 @@ int cgck_rx_end(void);
  * cgck_rx_post returns the frames posted (-EINVAL: a descriptor reaches
  * past `bytes`); cgck_rx_begin_posted the frames the window answers for
  * (as cgck_rx_begin), -ENOENT when nothing is posted.  Posted fills
- * (cgck_tx_post) coalesce the same way. */
+ * (cgck_tx_post) coalesce the same way, and bursts and fills waiting
+ * together over the same registered range go out as one request. */
 int cgck_rx_post(void *base, size_t bytes, const cgck_desc_t *desc, uint64_t n);
 int cgck_rx_begin_posted(void);
 
