@@ -1220,6 +1220,41 @@ extern "C" int cgck_burst_open(cgck_ctx_t *c, uint32_t max_pkts, size_t max_byte
 }
 
 #if CGCK_LAB
+// Lab (tests/test_gpu_burst_lab.py).  cgck_lab_burst_poke: restart ctx's
+// server as if `seq` were the last request served (a few seqs before the
+// 32-bit wrap).  cgck_lab_burst_stale: with the server running and nothing
+// posted, set the done words of workgroups >= from half the seq space ahead,
+// as a word untouched for 2^31 requests would compare; the next request must
+// refresh them (a workgroup outside a request's slices stores the seq it
+// steps over), or a wider request after it would be reported served before
+// those workgroups wrote anything.
+extern "C" int cgck_lab_burst_poke(cgck_ctx_t *c, uint32_t seq)
+{
+	if (!c || !c->bbox || c->bslot[0] || c->bslot[1])
+		return -EINVAL;
+	std::shared_lock<std::shared_mutex> map_lk(g_map_mu);
+	__atomic_store_n(&c->bbox->stop, 1u, __ATOMIC_RELEASE);
+	const hipError_t e = hipStreamSynchronize(c->bstream);
+	__atomic_store_n(&c->bbox->stop, 0u, __ATOMIC_RELEASE);
+	if (e != hipSuccess)
+		return -EIO;
+	for (uint32_t j = 0; j < kBurstMaxWG; j++)
+		__atomic_store_n(&c->bbox->done[j], seq, __ATOMIC_RELEASE);
+	c->bbox->req[0] = c->bbox->req[1] = 0;
+	c->bbox->refused[0] = c->bbox->refused[1] = 0;
+	c->bseq = c->bdone = seq;
+	return burst_launch(c, seq);
+}
+
+extern "C" int cgck_lab_burst_stale(cgck_ctx_t *c, uint32_t from)
+{
+	if (!c || !c->bbox || c->bslot[0] || c->bslot[1])
+		return -EINVAL;
+	for (uint32_t j = from; j < kBurstMaxWG; j++)
+		__atomic_store_n(&c->bbox->done[j], c->bseq + 0x7ffffff0u, __ATOMIC_RELEASE);
+	return 0;
+}
+
 // Lab: workgroup 0's timestamps of the last request (100 MHz ticks: seen,
 // block read, computed, published; then the compute phase in shader clocks)
 // and the host's view of that request (ns: post, done seen) for

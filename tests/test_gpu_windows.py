@@ -1103,3 +1103,92 @@ def test_rx_tx_fused_coalesced(port):
     finally:
         cgck.burst_close()
         L.cgck_host_unregister(pool.ctypes.data)
+
+
+def test_coalesced_threads_with_mapping_changes(port):
+    """Three worker threads, each with its own pool, burst server and both
+    coalesced queues deep, while the main thread keeps registering and
+    unregistering a range of its own (each change stops every server, after
+    serving what is posted): every burst replays bit-exact and every fill's
+    fields are the reference's on every thread."""
+    import time
+    R = referee(port)
+    L = cgck.load()
+    errs, stop = [], threading.Event()
+
+    def work(t):
+        try:
+            rng = np.random.default_rng(7500 + t)
+            sizes = [int(rng.integers(1, 6)) for _ in range(40)]
+            frames = rxcorpus.corpus(rng, R, sum(sizes), clean=True)
+            buf, desc_all, tx_base, tx_stride = rxcorpus.pool(frames, 200)
+            raw, pool, size = rxcorpus.registered_copy(buf)
+            assert L.cgck_host_register(pool.ctypes.data, size) == 0
+            got, ref = pool[:len(buf)], buf.copy()
+            descs, at = [], 0
+            for s in sizes:
+                descs.append(desc_all[at:at + s].copy())
+                at += s
+            cgck.burst_open(max_pkts=1024, max_bytes=4 << 20)
+            try:
+                fills, nxt = [], 0
+                for k in range(len(sizes)):
+                    assert cgck.rx_post(got, descs[k]) == sizes[k]
+                    want = []
+                    cgck.tx_begin()
+                    for _ in range(2):
+                        ln = int(rng.integers(40, 400))
+                        pkt = tcp_pkt(rng, ln)
+                        row = got[tx_base + nxt * tx_stride:tx_base + nxt * tx_stride + 2048]
+                        row[14:14 + ln] = pkt
+                        want.append((nxt, ln, expected(port, pkt, 16)))
+                        tx_calls(row, ln, 16)
+                        nxt += 1
+                    assert cgck.tx_post() == 4
+                    fills.append(want)
+                    if k % 3 == 2:          # open three bursts, complete three fills
+                        for j in range(k - 2, k + 1):
+                            stack, ip_in, tcp_in = FLAGS[(j * 5 + t) % len(FLAGS)]
+                            d = descs[j]
+                            a = port.replay_rx(*R.fn_pointers(), ref, d.view(np.uint8), len(d), stack, ip_in,
+                                               tcp_in)
+                            cgck.rx_begin_posted()
+                            try:
+                                b = port.replay_rx(*cgck.fn_pointers(), got, d.view(np.uint8), len(d), stack,
+                                                   ip_in, tcp_in)
+                            finally:
+                                cgck.rx_end()
+                            assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]), (t, j)
+                            assert cgck.tx_complete() == 4
+                            for s_, ln, r in fills[j]:
+                                row = got[tx_base + s_ * tx_stride:tx_base + s_ * tx_stride + 2048]
+                                assert np.array_equal(row[14:14 + ln], r), (t, j, s_)
+                    time.sleep(0.0005)
+                while cgck.rx_pending():
+                    cgck.rx_begin_posted()
+                    cgck.rx_end()
+                while cgck.tx_pending():
+                    cgck.tx_complete()
+            finally:
+                cgck.burst_close()
+                L.cgck_host_unregister(pool.ctypes.data)
+        except Exception as e:  # noqa: BLE001 — reported below
+            errs.append(repr(e))
+        finally:
+            cgck.thread_release()
+
+    th = [threading.Thread(target=work, args=(t,)) for t in range(3)]
+    for x in th:
+        x.start()
+    cycles = 0
+    while any(x.is_alive() for x in th):
+        raw, other, size = rxcorpus.registered_copy(np.zeros(16384, np.uint8))
+        assert L.cgck_host_register(other.ctypes.data, size) == 0
+        time.sleep(0.002)
+        assert L.cgck_host_unregister(other.ctypes.data) == 0
+        del other, raw
+        cycles += 1
+    for x in th:
+        x.join()
+    assert not errs, errs
+    assert cycles > 0

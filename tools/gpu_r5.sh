@@ -22,6 +22,10 @@ for step in "$@"; do
 	tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread || exit 1 ;;
 	cycles) for i in 1 2 3; do run pytest_cycles$i 300 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread -k "not reregister or reregister" || true; done ;;
 	testsk) run pytest_gpu 900 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread || true ;;
+	lab) run pytest_lab 300 python -u -m pytest tests/test_gpu_burst_lab.py -m "gpu and lab" -x -v --timeout 120 --timeout-method thread || exit 1
+		# the control: the same test with the done-word refresh switched off must fail
+		CGCK_SERVER_OPTS=16 run pytest_lab_norefresh 300 python -u -m pytest tests/test_gpu_burst_lab.py -m "gpu and lab" -v --timeout 120 --timeout-method thread
+		echo "control (refresh off) rc=$?" ;;
 	quick) run pytest_quick 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "burst or window or pipelined or rx_post or tx_" || exit 1 ;;
 	txburst) run txburst 400 tools/txburst 0.2 || exit 1 ;;
 	txloop) run txloop 400 tools/txloop 0.2 || exit 1 ;;
