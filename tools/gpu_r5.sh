@@ -26,6 +26,8 @@ for step in "$@"; do
 		# the control: the same test with the done-word refresh switched off must fail
 		CGCK_SERVER_OPTS=16 run pytest_lab_norefresh 300 python -u -m pytest tests/test_gpu_burst_lab.py -m "gpu and lab" -v --timeout 120 --timeout-method thread
 		echo "control (refresh off) rc=$?" ;;
+	srvlat) run srvlat_64 120 tools/srvlat 64 || exit 1
+		run srvlat_64_raw 120 tools/srvlat 64 raw || exit 1 ;;
 	quick) run pytest_quick 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "burst or window or pipelined or rx_post or tx_" || exit 1 ;;
 	txburst) run txburst 400 tools/txburst 0.2 || exit 1 ;;
 	txloop) run txloop 400 tools/txloop 0.2 || exit 1 ;;
