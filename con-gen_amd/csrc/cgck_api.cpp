@@ -313,6 +313,8 @@ static double now_s()
 // the one after start_seq.
 #if CGCK_LAB
 static thread_local uint64_t t_lab_host[2]; // cgck_lab_burst_times
+thread_local double t_lab_post[16];         // cgck_lab_post_times (cgck_dropin.cpp), TSC ticks
+#define LAB_TICK(i, t0) (t_lab_post[2 * (i)] += (double)(__builtin_ia32_rdtsc() - (t0)), t_lab_post[2 * (i) + 1] += 1)
 #endif
 
 // Lab A/B bits of the server kernel ($CGCK_SERVER_OPTS; 0 in the product).
@@ -512,7 +514,14 @@ static void burst_done_at(cgck_ctx *c, uint32_t seq)
 // so a workgroup's done word at or past seq means its slice is in.
 static int burst_wait(cgck_ctx *c, uint32_t seq, uint32_t n, uint64_t range)
 {
+#if CGCK_LAB
+	const uint64_t tl0 = __builtin_ia32_rdtsc();
+#endif
 	std::shared_lock<std::shared_mutex> map_lk(g_map_mu);
+#if CGCK_LAB
+	LAB_TICK(4, tl0);
+	const uint64_t tl1 = __builtin_ia32_rdtsc();
+#endif
 	BurstBox *b = c->bbox;
 	const uint32_t W = burst_wgs(n, c->bwgs, c->bper);
 	const double t0 = now_s();
@@ -559,6 +568,7 @@ static int burst_wait(cgck_ctx *c, uint32_t seq, uint32_t n, uint64_t range)
 	}
 #if CGCK_LAB
 	t_lab_host[1] = (uint64_t)(now_s() * 1e9);
+	LAB_TICK(5, tl1);
 #endif
 	burst_done_at(c, seq);
 	if (__atomic_load_n(&b->refused[seq & 1], __ATOMIC_ACQUIRE) == seq)
@@ -595,6 +605,9 @@ int cgck::burst_collect(cgck_ctx *c, BurstPending *p)
 	}
 	int rc = burst_wait(c, seq, p->n, p->range);
 	if (rc == 0) {
+#if CGCK_LAB
+		const uint64_t tc0 = __builtin_ia32_rdtsc();
+#endif
 		const uint8_t *o = burst_resp(c, seq);
 		if (p->out)
 			memcpy(p->out, o, 4 * (size_t)p->n);
@@ -602,6 +615,9 @@ int cgck::burst_collect(cgck_ctx *c, BurstPending *p)
 			memcpy(p->meta, o + burst_meta_off(p->n), 4 * (size_t)p->n);
 		if (p->verdict)
 			memcpy(p->verdict, o + burst_ver_off(p->n), p->n);
+#if CGCK_LAB
+		LAB_TICK(2, tc0);
+#endif
 	}
 	p->rc = rc;
 	return rc;
@@ -1252,6 +1268,36 @@ extern "C" int cgck_lab_burst_stale(cgck_ctx_t *c, uint32_t from)
 		return -EINVAL;
 	for (uint32_t j = from; j < kBurstMaxWG; j++)
 		__atomic_store_n(&c->bbox->done[j], c->bseq + 0x7ffffff0u, __ATOMIC_RELEASE);
+	return 0;
+}
+
+// Lab: what one host load of a BurstBox word costs while the server polls
+// (ns, mean over reps, each load after ~2 us of spin): out[0] the mailbox
+// line (stop, which the leader polls with req), out[1] refused[] (the same
+// line today), out[2] done[0], out[3] alive[0].  NULL: the thread's context.
+extern "C" int cgck_lab_box_probe(cgck_ctx_t *c, int reps, double out[4])
+{
+	if (!c)
+		c = cgck::thread_ctx_if_any();
+	if (!c || !c->bbox || reps <= 0)
+		return -EINVAL;
+	const volatile uint32_t *w[4] = {&c->bbox->stop, &c->bbox->refused[0], &c->bbox->done[0],
+					 (const volatile uint32_t *)&c->bbox->alive[0]};
+	for (int k = 0; k < 4; k++) {
+		double acc = 0;
+		uint32_t sink = 0;
+		for (int i = 0; i < reps; i++) {
+			for (const double s0 = now_s(); now_s() - s0 < 2e-6;)
+				;
+			struct timespec a, b;
+			clock_gettime(CLOCK_MONOTONIC, &a);
+			sink += *w[k];
+			__atomic_thread_fence(__ATOMIC_SEQ_CST);
+			clock_gettime(CLOCK_MONOTONIC, &b);
+			acc += (b.tv_sec - a.tv_sec) * 1e9 + (b.tv_nsec - a.tv_nsec);
+		}
+		out[k] = acc / reps + (sink == 0xdeadbeef ? 1e-9 : 0);
+	}
 	return 0;
 }
 

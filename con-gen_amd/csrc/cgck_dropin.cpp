@@ -23,6 +23,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include <algorithm>
 #include <atomic>
@@ -31,6 +32,10 @@
 #include "cgck_host.h"
 
 using namespace cgck;
+
+#if CGCK_LAB
+extern thread_local double t_lab_post[16]; // cgck_api.cpp: the Poster's phase totals (lab, TSC ticks)
+#endif
 
 namespace {
 
@@ -187,6 +192,20 @@ struct PostQueue {
 // posts a burst and a fill every iteration pays one mailbox round trip for
 // both.
 enum { kRx = 0, kTx = 1 };
+
+#if CGCK_LAB
+// Lab build: where the posted windows' host time goes (tools/txloop split
+// mode reads it through cgck_lab_post_times): ns and calls of burst_ready,
+// of collect (and of its copy out of the response slot, inside burst_collect)
+// and of send.
+static inline double lab_ns() { return (double)__builtin_ia32_rdtsc(); } // TSC ticks (lab)
+#define LAB_T0(v) const double v = lab_ns()
+#define LAB_ADD(i, v) (t_lab_post[2 * (i)] += lab_ns() - (v), t_lab_post[2 * (i) + 1] += 1)
+#else
+#define LAB_T0(v)
+#define LAB_ADD(i, v) ((void)0)
+#endif
+
 struct Poster {
 	PostQueue q[2];
 	PostReq rq[2 * kPostQ]; // each carries >= 1 item: never more live than items
@@ -869,7 +888,9 @@ void Poster::send(cgck_ctx *c)
 void Poster::collect(cgck_ctx *c, int ri)
 {
 	PostReq &r = rq[ri];
+	LAB_T0(t0);
 	r.rc = r.pend.seq ? burst_collect(c, &r.pend) : r.pend.rc;
+	LAB_ADD(1, t0);
 	if (r.rc)
 		snprintf(r.msg, sizeof(r.msg), "%s", err_text());
 	r.done = true;
@@ -884,11 +905,20 @@ void Poster::pump(cgck_ctx *c, int kind, bool wait)
 {
 	for (int k = 0; k < 2; k++) {
 		const int ri = inflight[k];
-		if (ri >= 0 && ((wait && k == kind) || burst_ready(c, &rq[ri].pend)))
+		bool go = ri >= 0 && wait && k == kind;
+		if (ri >= 0 && !go) {
+			LAB_T0(t0);
+			go = burst_ready(c, &rq[ri].pend);
+			LAB_ADD(0, t0);
+		}
+		if (go)
 			collect(c, ri);
 	}
-	if (q[kRx].sent < q[kRx].count || q[kTx].sent < q[kTx].count)
+	if (q[kRx].sent < q[kRx].count || q[kTx].sent < q[kTx].count) {
+		LAB_T0(t0);
 		send(c);
+		LAB_ADD(3, t0);
+	}
 }
 
 // Are the oldest item's values in (1), or not yet (0)?  wait: until they are.
@@ -1047,6 +1077,15 @@ extern "C" int cgck_rx_begin_posted(void)
 
 // The drain rule's two questions (include/cgck.h): is a burst still posted,
 // and would opening the oldest one wait for the GPU?
+#if CGCK_LAB
+// Lab: the Poster's phase totals (TSC ticks, calls) since the last call, zeroed.
+extern "C" void cgck_lab_post_times(double out[16])
+{
+	memcpy(out, t_lab_post, sizeof(t_lab_post));
+	memset(t_lab_post, 0, sizeof(t_lab_post));
+}
+#endif
+
 extern "C" int cgck_rx_pending(void)
 {
 	const ThreadState *t = t_st;

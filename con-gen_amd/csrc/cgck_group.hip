@@ -333,6 +333,21 @@ constexpr uint32_t kSliceLds = 1024;
 // word: one wide request in a suite run was not served in 2 s).
 constexpr uint32_t kBurstExit = 0xffffffffu;
 
+// A workgroup outside a request keeps its done word from lagging the seqs
+// by more than kDoneLag (a word untouched for 2^31 requests would pass the
+// host's serial compare for a later request it has a slice of), but stores
+// only when it lags that far: every store takes the done line out of the
+// host's cache, and the host reads that line at every request (31 refresh
+// stores a request cost the poll loop 150-400 ns of misses a collect,
+// tools/txloop_lab split).  Reading the word does not take the line.
+constexpr uint32_t kDoneLag = 1u << 20;
+
+__device__ __forceinline__ void done_refresh(BurstBox *box, uint32_t j, uint32_t seq)
+{
+	if (seq - sys_relaxed(&box->done[j]) > kDoneLag)
+		__hip_atomic_store(&box->done[j], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __device__ __forceinline__ uint64_t relay_load(const uint64_t *p)
 {
 	return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -407,14 +422,10 @@ __global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const 
 						c = 1, last = want, n = (uint32_t)(r >> 32);
 					else if ((uint32_t)r != 0 && (int32_t)((uint32_t)r - want) > 0) {
 						// not ours: on to the next seq.  Its done word
-						// moves along with it, so done[j] never lags the
-						// host's seqs by more than the two in flight (a
-						// stale word would pass the host's serial compare
-						// once 2^31 requests had gone by without j)
+						// is kept within kDoneLag of it (done_refresh)
 						last = want;
 						if (!(opts & 16)) // lab bit 16: the refresh off (the regression test's control)
-							__hip_atomic_store(&box->done[j], want, __ATOMIC_RELAXED,
-									   __HIP_MEMORY_SCOPE_SYSTEM);
+							done_refresh(box, j, want);
 					}
 					else if (__builtin_amdgcn_s_memrealtime() - t0 > 4 * idle)
 						c = 2;
@@ -442,11 +453,11 @@ __global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const 
 		if (j >= W || cmd == 3) {
 			if (t == 0 && j == 0 && K > 1 && W == 1)
 				relay_store(dcmd + (seq & 1), (uint64_t)seq | (uint64_t)n << 32);
-			// a workgroup outside the request's W keeps its done word at the
-			// seq it stepped over (see the step-over above); the host reads
-			// done[j] only for j < W of the request it waits for
+			// a workgroup outside the request's W keeps its done word within
+			// kDoneLag of the seqs (done_refresh); the host reads done[j]
+			// only for j < W of the request it waits for
 			if (t == 0 && cmd == 1 && !(opts & 16))
-				__hip_atomic_store(&box->done[j], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+				done_refresh(box, j, seq);
 			__syncthreads(); // cmd / cmd_n are rewritten by the next poll
 			continue;
 		}

@@ -33,6 +33,17 @@ for step in "$@"; do
 	txloop) run txloop 400 tools/txloop 0.2 || exit 1 ;;
 	split) TXLOOP_SPLIT=1 run txloop_split 60 tools/txloop 0.5 || exit 1
 		TXLOOP_SPLIT=2 run txloop_split_reply 60 tools/txloop 0.5 || exit 1 ;;
+	splitlab) # the split timing with the Poster's phases (lab library)
+		for r in 1 16 64 256; do
+			TXLOOP_SPLIT=1 TXLOOP_SPLIT_R=$r run txloop_lab_split1_r$r 60 tools/txloop_lab 0.5 || exit 1
+		done
+		TXLOOP_SPLIT=2 TXLOOP_SPLIT_R=64 run txloop_lab_split2_r64 60 tools/txloop_lab 0.5 || exit 1 ;;
+	splitn) # the split timing per burst size (250 ns a frame), RX only and with replies
+		for r in 4 16 64 256; do
+			for m in 1 2; do
+				TXLOOP_SPLIT=$m TXLOOP_SPLIT_R=$r run txloop_split${m}_r$r 60 tools/txloop 0.5 || exit 1
+			done
+		done ;;
 	e2e) run e2e 300 python -u tools/e2e.py || exit 1 ;;
 	lpdab) # lab lpd variants against the product kernel, one process each (64 B)
 		for cfg in "64 6 2" "64 5 2" "32 8 5" "64 6 5" "16 8 2"; do

@@ -39,6 +39,7 @@
  *   tools/txloop [seconds per cell, default 0.2]
  *   TXLOOP_LEN=64  TXLOOP_BURSTS=1,2,4,8,16,32,64,256,2048  TXLOOP_NS=0,250
  */
+#define _GNU_SOURCE
 #include <dlfcn.h>
 #include <libgen.h>
 #include <stdint.h>
@@ -313,13 +314,23 @@ int main(int argc, char **argv)
 	/* where a small burst's fixed cost goes: the coalesced loop at one frame
 	 * a burst and 250 ns of stack work a frame, each call timed (mean ns) */
 	if (getenv("TXLOOP_SPLIT")) {
-		const int R = 1, split_reply = atoi(getenv("TXLOOP_SPLIT")) == 2;
+		/* TXLOOP_SPLIT_R: frames a burst (1), TXLOOP_SPLIT_NS: stack ns a frame (250) */
+		const int R = getenv("TXLOOP_SPLIT_R") ? atoi(getenv("TXLOOP_SPLIT_R")) : 1,
+			  split_reply = atoi(getenv("TXLOOP_SPLIT")) == 2;
+		const double sns = getenv("TXLOOP_SPLIT_NS") ? atof(getenv("TXLOOP_SPLIT_NS")) : 250;
+		if (R < 1 || R > MAXB / 2)
+			return 2;
 		double acc[10] = {0}, slow_t = 0;
 		long slow_n = 0, forced = 0, maxpend = 0;
 		long cnt[10] = {0}, k = 0, opened = 0;
 		static const char *nm[10] = {"tx_ready+complete", "tx_begin", "rx_post", "rx_pending+ready",
 					     "rx_begin_posted", "verify (+reply) calls", "rx_end", "tx_post", "spin", "iteration"};
+		/* the lab library's phase totals inside the Poster, when loaded */
+		void (*lab_times)(double *) = (void (*)(double *))dlsym(RTLD_DEFAULT, "cgck_lab_post_times");
+		double lt[16] = {0};
 		const double t0 = now();
+		if (lab_times)
+			lab_times(lt);
 		while (now() - t0 < budget * 4) {
 			double a = now(), b;
 			const double it0 = a;
@@ -345,9 +356,12 @@ int main(int argc, char **argv)
 					slow_t += b - a;
 				}
 				a = b;
-				verify(rxh[opened & 1] + L3, len, lib_in, lib_udp);
-				if (split_reply)
-					reply(txh[k & 1] + L3, rxh[opened & 1] + L3, lib_in, lib_udp);
+				for (int i = 0; i < R; i++) {
+					uint8_t *ip = rxh[opened & 1] + (size_t)i * SLOT + L3;
+					verify(ip, len, lib_in, lib_udp);
+					if (split_reply) /* the fill's slots: one transmit half a fill */
+						reply(txh[k & 1] + (size_t)i * SLOT + L3, ip, lib_in, lib_udp);
+				}
 				b = now(); acc[5] += b - a; cnt[5]++; a = b;
 				cgck_rx_end();
 				b = now(); acc[6] += b - a; cnt[6]++; a = b;
@@ -355,7 +369,7 @@ int main(int argc, char **argv)
 			}
 			cgck_tx_post();
 			b = now(); acc[7] += b - a; cnt[7]++; a = b;
-			spin(250e-9);
+			spin(R * sns * 1e-9);
 			b = now(); acc[8] += b - a; cnt[8]++;
 			acc[9] += b - it0;
 			cnt[9]++;
@@ -365,12 +379,32 @@ int main(int argc, char **argv)
 			cgck_rx_end();
 		while (cgck_tx_pending() > 0)
 			cgck_tx_complete();
-		printf("{\"mode\": \"split\", \"reply\": %d, \"burst\": 1, \"iterations\": %ld, \"bursts_opened\": %ld",
-		       split_reply, k, opened);
+		/* lab: one host load of a mailbox / done / alive word while the server polls */
+		int (*box_probe)(void *, int, double *) = (int (*)(void *, int, double *))dlsym(RTLD_DEFAULT, "cgck_lab_box_probe");
+		double bp[4] = {0};
+		if (box_probe)
+			box_probe(NULL, 2000, bp);
+		printf("{\"box_load_ns\": {\"mailbox\": %.1f, \"refused\": %.1f, \"done\": %.1f, \"alive\": %.1f}}\n", bp[0],
+		       bp[1], bp[2], bp[3]);
+		printf("{\"mode\": \"split\", \"reply\": %d, \"burst\": %d, \"stack_ns_per_frame\": %.0f, "
+		       "\"iterations\": %ld, \"bursts_opened\": %ld",
+		       split_reply, R, sns, k, opened);
 		for (int i = 0; i < 10; i++)
 			printf(", \"%s_ns\": %.1f", nm[i], cnt[i] ? acc[i] / cnt[i] * 1e9 : 0.0);
 		printf(", \"opens_over_1us\": %ld, \"their_mean_us\": %.2f, \"opens_not_ready\": %ld, \"max_pending\": %ld",
 		       slow_n, slow_n ? slow_t / slow_n * 1e6 : 0.0, forced, maxpend);
+		if (lab_times) { /* per iteration: ns in each phase (TSC ticks, scaled), and its calls */
+			static const char *ph[7] = {"lab_ready", "lab_collect", "lab_copy_out", "lab_send",
+						    "lab_wait_lock", "lab_wait_loop", "spare"};
+			const double tk0 = (double)__builtin_ia32_rdtsc(), c0 = now();
+			spin(0.02);
+			const double ns_per_tick = (now() - c0) * 1e9 / ((double)__builtin_ia32_rdtsc() - tk0);
+			lab_times(lt);
+			for (int i = 0; i < 6; i++)
+				printf(", \"%s_ns_per_it\": %.1f, \"%s_calls_per_it\": %.3f, \"%s_ns_per_call\": %.1f", ph[i],
+				       lt[2 * i] * ns_per_tick / k, ph[i], lt[2 * i + 1] / k, ph[i],
+				       lt[2 * i + 1] ? lt[2 * i] * ns_per_tick / lt[2 * i + 1] : 0.0);
+		}
 		printf("}\n");
 		return 0;
 	}
