@@ -278,10 +278,20 @@ __device__ __forceinline__ void burst_part(const BurstReq &h, uint32_t flags, co
 {
 	KParams p = {base, reinterpret_cast<const cgck_desc_t *>(desc), hi - lo, 0, 0, 0, flags,
 		     out ? out + lo : nullptr, verdict ? verdict + lo : nullptr, nullptr, 0, zero, meta + lo};
-	if (h.max_len <= 80)
-		cksum_body<4, 2, 4, true, false, LDSD>(p, 0, 1);
-	else
-		cksum_body<16, 6, 4, true, false, LDSD>(p, 0, 1);
+	// A part the block covers in one pass with one packet per group runs
+	// unrolled once (U = 1): a small request's time is the body's dependent
+	// VALU chain, which four unrolled packets per group quadruple.
+	if (h.max_len <= 80) {
+		if (hi - lo <= 64)
+			cksum_body<4, 2, 1, true, false, LDSD>(p, 0, 1);
+		else
+			cksum_body<4, 2, 4, true, false, LDSD>(p, 0, 1);
+	} else {
+		if (hi - lo <= 16)
+			cksum_body<16, 6, 1, true, false, LDSD>(p, 0, 1);
+		else
+			cksum_body<16, 6, 4, true, false, LDSD>(p, 0, 1);
+	}
 }
 
 // A request may carry two parts (a receive burst's frames, then a TX fill's
