@@ -318,6 +318,24 @@ __device__ __forceinline__ uint4 ldc(const uint4 *c0, int i, int nch, const void
 	return ld<NT>(nch > 0 ? c0 + min(i, nch - 1) : reinterpret_cast<const uint4 *>(zero));
 }
 
+// Two 16-byte system-coherent loads (global_load ... sc0 sc1), waited for
+// (inline asm: the compiler counts none of it, so the wait is inside): the
+// burst server's block read, coherent with the host's stores whatever the L2
+// holds, without a cache invalidate; whole-line requests like plain loads
+// (relaxed 8-byte atomic loads leave as one fabric read each).
+__device__ __forceinline__ void ld_sys16x2(const uint4 *p0, const uint4 *p1, uint4 &v0, uint4 &v1)
+{
+	u32x4_t a, b;
+	asm volatile("global_load_dwordx4 %0, %2, off sc0 sc1\n\t"
+		     "global_load_dwordx4 %1, %3, off sc0 sc1\n\t"
+		     "s_waitcnt vmcnt(0)"
+		     : "=&v"(a), "=&v"(b)
+		     : "v"(p0), "v"(p1)
+		     : "memory");
+	v0 = make_uint4(a[0], a[1], a[2], a[3]);
+	v1 = make_uint4(b[0], b[1], b[2], b[3]);
+}
+
 template <bool NT>
 struct GChunks {
 	const uint4 *p;

@@ -244,14 +244,15 @@ __global__ __launch_bounds__(256) void cksum_kernel(KParams p)
 //
 // Ordering of the request block: the host's block stores precede its `req`
 // store (x86 TSO, a release store); the block, the mailbox and the packet
-// bytes are system memory, which the GPU maps uncached (MTYPE UC: no L2 or L1
-// copy), so every read of them is a PCIe read served coherently by the host.
-// A worker's block reads are issued after its relay load returned, the relay
-// was stored after the leader's mailbox load returned the new seq, and that
-// load was served after the host's block stores were visible: each read is
-// causally after the block was written.  The system-scope acquire each
-// workgroup executes before its reads drops its CU's L1 and its XCD's L2
-// copies of the device scratch the whole-block path rewrites.
+// bytes are system memory, read with system-coherent loads (sc0 sc1:
+// ld_sys16x2, sys_relaxed) or with plain loads after a system-scope acquire,
+// so no line a cache holds from an earlier request is served.  A worker's block reads are issued after its relay load
+// returned, the relay was stored after the leader's mailbox load returned the
+// new seq, and that load was served after the host's block stores were
+// visible: each read is causally after the block was written.  The
+// whole-block path's device scratch copy is written and read by one
+// workgroup: a workgroup-scope release / acquire around the barrier and an
+// L1 invalidate, so no line of an earlier request's copy is served.
 // --------------------------------------------------------------------------
 
 __device__ __forceinline__ uint32_t sys_load(const uint32_t *p)
@@ -471,6 +472,12 @@ __global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const 
 			__syncthreads(); // cmd / cmd_n are rewritten by the next poll
 			continue;
 		}
+		// lab opts bit 512: every workgroup but the leader starts its slice
+		// 20 us late, so a host that took a stale done word for served would
+		// read outputs not yet written (the wrap test's control)
+		if ((opts & 512) && j > 0)
+			for (const uint64_t d0 = __builtin_amdgcn_s_memrealtime(); __builtin_amdgcn_s_memrealtime() - d0 < 2000;)
+				__builtin_amdgcn_s_sleep(8);
 		const uint8_t *req = req0 + (size_t)(seq & 1) * cap;
 		uint8_t *resp = resp0 + (size_t)(seq & 1) * rslot;
 		const uint4 *src = reinterpret_cast<const uint4 *>(req);
@@ -479,9 +486,19 @@ __global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const 
 		uint64_t lab_t0 = __builtin_amdgcn_s_memrealtime(), lab_t1 = 0, lab_t2 = 0;
 		uint64_t lab_c1 = 0;
 #endif
-		// One system-scope acquire: no line of the scratch copy of an
-		// earlier request is served from this CU's L1 or this XCD's L2.
-		__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+		// Host memory is cached in L2 (hipHostMallocCoherent staging too: a
+		// plain read of the block served an earlier request's header), so no
+		// read of it may be served from a line an earlier request left.  A
+		// system-scope acquire invalidates the caches, but costs 2 us (of a
+		// small request's 3 us block-read phase, tools/srvlat; an
+		// agent-scope one the same): a one-workgroup request reads its first
+		// block bytes with system-coherent loads (ld_sys16x2) and takes the
+		// acquire only before host memory it reads with plain loads (the
+		// rest of a large block, packet bytes in place); a slice of a wide
+		// request takes it first.  Lab opts bit 32: before every request.
+		const bool one_wg = W == 1 && !(opts & 1);
+		if (!one_wg || (opts & 32))
+			__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
 		bool ok;
 		// opts bits 1 / 2 (lab A/B, results then partial): no verdict stores
 		// / no stores at all
@@ -491,12 +508,13 @@ __global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const 
 		const BurstReq &h = *reinterpret_cast<const BurstReq *>(hdr_w);
 		// opts bit 0 (lab A/B): a one-workgroup request takes the slice path
 		// too (header and descriptors only, packets read where they lie)
-		if (W == 1 && !(opts & 1)) {
+		if (one_wg) {
 			// the first kBurstFirst bytes of the block in one round trip:
 			// plain 16-byte loads, so every wave's read leaves as whole-line
 			// requests
 			static_assert(kBurstFirst == 2 * 16 * 256, "two 16-byte loads per thread");
-			const uint4 v0 = src[t], v1 = src[256 + t];
+			uint4 v0, v1;
+			ld_sys16x2(src + t, src + 256 + t, v0, v1);
 			dst[t] = v0;
 			dst[256 + t] = v1;
 			if (t < 4)
@@ -505,7 +523,9 @@ __global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const 
 			ok = burst_hdr_ok(h, n, max_pkts, cap);
 			const uint32_t chunks = ok ? (h.bytes + 15) / 16 : 0;
 			// the rest of a larger block, 16 loads in flight per thread (64 KiB
-			// a round trip)
+			// a round trip), plain loads after the acquire
+			if (chunks > kBurstFirst / 16)
+				__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
 			for (uint32_t at = kBurstFirst / 16; at < chunks; at += 16 * 256) {
 				uint4 x[16];
 #pragma unroll
@@ -521,10 +541,12 @@ __global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const 
 				}
 			}
 			// scratch stores visible to the workgroup (its waves share one
-			// CU's L1: workgroup scope)
+			// CU's L1: workgroup scope), and no line of an earlier request's
+			// copy left in that L1
 			__builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
 			__syncthreads();
 			__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+			asm volatile("buffer_inv sc0" ::: "memory");
 			const uint32_t *sd = reinterpret_cast<const uint32_t *>(scratch + sizeof(BurstReq));
 			if (ok) {
 				const uint64_t limit = burst_limit(h);
@@ -537,7 +559,10 @@ __global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const 
 			lab_c1 = __builtin_amdgcn_s_memtime();
 #endif
 			if (ok) {
-				// staged packet bytes are read from the scratch copy
+				// staged packet bytes are read from the scratch copy; packet
+				// bytes in place with plain loads, after the acquire
+				if (h.base)
+					__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
 				const uint8_t *base = h.base ? reinterpret_cast<const uint8_t *>(h.base) : scratch + h.p_off;
 				burst_body<false>(h, sd, 0, n, o32, meta, ver, zero, base);
 				if (opts & 8) // lab: the body a second time (is a pass cold-start bound?)

@@ -22,10 +22,16 @@ for step in "$@"; do
 	tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread || exit 1 ;;
 	cycles) for i in 1 2 3; do run pytest_cycles$i 300 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread -k "not reregister or reregister" || true; done ;;
 	testsk) run pytest_gpu 900 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread || true ;;
-	lab) run pytest_lab 300 python -u -m pytest tests/test_gpu_burst_lab.py -m "gpu and lab" -x -v --timeout 120 --timeout-method thread || exit 1
+	lab) # workgroups but the leader start their slices 20 us late (opts 512), so a
+		# stale done word taken for served shows as outputs not yet written
+		CGCK_SERVER_OPTS=512 run pytest_lab 300 python -u -m pytest tests/test_gpu_burst_lab.py -m "gpu and lab" -x -v --timeout 120 --timeout-method thread || exit 1
 		# the control: the same test with the done-word refresh switched off must fail
-		CGCK_SERVER_OPTS=16 run pytest_lab_norefresh 300 python -u -m pytest tests/test_gpu_burst_lab.py -m "gpu and lab" -v --timeout 120 --timeout-method thread
+		CGCK_SERVER_OPTS=528 run pytest_lab_norefresh 300 python -u -m pytest tests/test_gpu_burst_lab.py -m "gpu and lab" -v --timeout 120 --timeout-method thread
 		echo "control (refresh off) rc=$?" ;;
+	srvlatab) # lab: the read phase without the system-scope acquire (32) or with an agent-scope one (64)
+		run srvlat_64_base 120 tools/srvlat 64 || exit 1
+		CGCK_SERVER_OPTS=64 run srvlat_64_agentacq 120 tools/srvlat 64
+		CGCK_SERVER_OPTS=128 run srvlat_64_l1inv 120 tools/srvlat 64 ;;
 	srvlat) run srvlat_64 120 tools/srvlat 64 || exit 1
 		run srvlat_64_raw 120 tools/srvlat 64 raw || exit 1 ;;
 	quick) run pytest_quick 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "burst or window or pipelined or rx_post or tx_" || exit 1 ;;
