@@ -323,6 +323,9 @@ __device__ __forceinline__ uint4 ldc(const uint4 *c0, int i, int nch, const void
 // burst server's block read, coherent with the host's stores whatever the L2
 // holds, without a cache invalidate; whole-line requests like plain loads
 // (relaxed 8-byte atomic loads leave as one fabric read each).
+template <int N>
+__device__ __forceinline__ void ld_sys16xN(const uint4 *const (&a)[N], uint4 (&v)[N]);
+
 __device__ __forceinline__ void ld_sys16x2(const uint4 *p0, const uint4 *p1, uint4 &v0, uint4 &v1)
 {
 	u32x4_t a, b;
@@ -334,6 +337,35 @@ __device__ __forceinline__ void ld_sys16x2(const uint4 *p0, const uint4 *p1, uin
 		     : "memory");
 	v0 = make_uint4(a[0], a[1], a[2], a[3]);
 	v1 = make_uint4(b[0], b[1], b[2], b[3]);
+}
+
+template <>
+__device__ __forceinline__ void ld_sys16xN<2>(const uint4 *const (&a)[2], uint4 (&v)[2])
+{
+	ld_sys16x2(a[0], a[1], v[0], v[1]);
+}
+
+// Six at once (the 16-lane group body's chunks), one wait for all.
+template <>
+__device__ __forceinline__ void ld_sys16xN<6>(const uint4 *const (&a)[6], uint4 (&v)[6])
+{
+	u32x4_t r0, r1, r2, r3, r4, r5;
+	asm volatile("global_load_dwordx4 %0, %6, off sc0 sc1\n\t"
+		     "global_load_dwordx4 %1, %7, off sc0 sc1\n\t"
+		     "global_load_dwordx4 %2, %8, off sc0 sc1\n\t"
+		     "global_load_dwordx4 %3, %9, off sc0 sc1\n\t"
+		     "global_load_dwordx4 %4, %10, off sc0 sc1\n\t"
+		     "global_load_dwordx4 %5, %11, off sc0 sc1\n\t"
+		     "s_waitcnt vmcnt(0)"
+		     : "=&v"(r0), "=&v"(r1), "=&v"(r2), "=&v"(r3), "=&v"(r4), "=&v"(r5)
+		     : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5])
+		     : "memory");
+	v[0] = make_uint4(r0[0], r0[1], r0[2], r0[3]);
+	v[1] = make_uint4(r1[0], r1[1], r1[2], r1[3]);
+	v[2] = make_uint4(r2[0], r2[1], r2[2], r2[3]);
+	v[3] = make_uint4(r3[0], r3[1], r3[2], r3[3]);
+	v[4] = make_uint4(r4[0], r4[1], r4[2], r4[3]);
+	v[5] = make_uint4(r5[0], r5[1], r5[2], r5[3]);
 }
 
 template <bool NT>

@@ -26,7 +26,11 @@ namespace cgck {
 constexpr int kGrpStage = 2048;
 
 // LDSD: p.desc points at descriptors staged in LDS (the burst server's slices).
-template <int G, int S, int U, bool DESC, bool NT, bool LDSD = false>
+// SYS (U = 1, packets of at most S * G chunks): the packet bytes are host
+// memory the burst server reads in place, with system-coherent loads
+// (ld_sys16xN) instead of after a cache-invalidating acquire; the header
+// bytes come from the chunks (lane shuffles) rather than byte loads.
+template <int G, int S, int U, bool DESC, bool NT, bool LDSD = false, bool SYS = false>
 __device__ __forceinline__ void cksum_body(const KParams &p, uint32_t bid, uint32_t nb)
 {
 	__shared__ uint32_t so[kGrpStage];
@@ -74,7 +78,7 @@ __device__ __forceinline__ void cksum_body(const KParams &p, uint32_t bid, uint3
 			b0[u] = 0;
 			proto[u] = 0;
 			tl[u] = 0;
-			if (need_hdr && pk[u].ok && span > 0) {
+			if (!SYS && need_hdr && pk[u].ok && span > 0) {
 				b0[u] = *gbl_at<const uint8_t>(a0);
 				if (span > 9)
 					proto[u] = *gbl_at<const uint8_t>(a0 + 9);
@@ -87,9 +91,37 @@ __device__ __forceinline__ void cksum_body(const KParams &p, uint32_t bid, uint3
 			const uint4 *c0 = reinterpret_cast<const uint4 *>(a0 & ~(uint64_t)15);
 			// clamped: chunks past the packet re-read its last chunk and
 			// eat() masks them out by position (zero-chunk lanes read zeros)
+			if constexpr (SYS) {
+				static_assert(U == 1, "the system-coherent body runs one packet per group");
+				const uint4 *a[S];
 #pragma unroll
-			for (int s = 0; s < S; ++s)
-				v[u][s] = ldc<NT>(c0, s * G + gl, nch[u], p.zero);
+				for (int s = 0; s < S; ++s)
+					a[s] = nch[u] > 0 ? c0 + min(s * G + gl, nch[u] - 1) : reinterpret_cast<const uint4 *>(p.zero);
+				ld_sys16xN<S>(a, v[u]);
+				// the header bytes at +0, +2, +3, +9 (aligned offsets q + k <
+				// 32): chunk 0 or 1 of the packet, lane 0 or 1 of the group
+				const int q = (int)(a0 & 15);
+				const int base_lane = lane & 63 & ~(G - 1); // the group's first lane in the wave
+				auto byte_at = [&](int k) {
+					const int o = q + k;
+					const uint4 w = v[u][0];
+					const int di = (o & 15) >> 2;
+					const uint32_t d = di == 0 ? w.x : di == 1 ? w.y : di == 2 ? w.z : w.w;
+					return (uint32_t)__shfl((int)((d >> (8 * (o & 3))) & 0xffu), base_lane + (o >> 4), 64);
+				};
+				const uint32_t h0 = byte_at(0), h2 = byte_at(2), h3 = byte_at(3), h9 = byte_at(9);
+				if (need_hdr && pk[u].ok && span > 0) {
+					b0[u] = h0;
+					if (span > 9)
+						proto[u] = h9;
+					if (rx && span >= 20)
+						tl[u] = h2 << 8 | h3;
+				}
+			} else {
+#pragma unroll
+				for (int s = 0; s < S; ++s)
+					v[u][s] = ldc<NT>(c0, s * G + gl, nch[u], p.zero);
+			}
 		}
 #pragma unroll
 		for (int u = 0; u < U; ++u) {
@@ -114,6 +146,7 @@ __device__ __forceinline__ void cksum_body(const KParams &p, uint32_t bid, uint3
 					eat<false>(pt, v[u][s], k, q, len, hl, fo, flags);
 			}
 			// Steps beyond the unrolled S (long packets): one at a time.
+			// (Never with SYS: its caller keeps packets within S * G chunks.)
 			const uint4 *c0 = reinterpret_cast<const uint4 *>(pk[u].a0 & ~(uint64_t)15);
 			for (int s = S; __any(s * G < nch[u]); ++s) {
 				const int k = s * G + gl;
@@ -272,13 +305,20 @@ __device__ __forceinline__ uint64_t sys_relaxed64(const uint64_t *p)
 
 // The group body over a request's packets [lo, hi) (block 0 of 1); desc is
 // packet lo's descriptor (in LDS when LDSD).
-template <bool LDSD>
+template <bool LDSD, bool SYS = false>
 __device__ __forceinline__ void burst_part(const BurstReq &h, uint32_t flags, const uint32_t *desc, uint32_t lo,
 					   uint32_t hi, uint32_t *out, uint32_t *meta, uint8_t *verdict,
 					   const void *zero, const uint8_t *base)
 {
 	KParams p = {base, reinterpret_cast<const cgck_desc_t *>(desc), hi - lo, 0, 0, 0, flags,
 		     out ? out + lo : nullptr, verdict ? verdict + lo : nullptr, nullptr, 0, zero, meta + lo};
+	if constexpr (SYS) { // burst_sys_ok: one packet per group covers the part
+		if (h.max_len <= 80)
+			cksum_body<4, 2, 1, true, false, false, true>(p, 0, 1);
+		else
+			cksum_body<16, 6, 1, true, false, false, true>(p, 0, 1);
+		return;
+	}
 	// A part the block covers in one pass with one packet per group runs
 	// unrolled once (U = 1): a small request's time is the body's dependent
 	// VALU chain, which four unrolled packets per group quadruple.
@@ -298,19 +338,29 @@ __device__ __forceinline__ void burst_part(const BurstReq &h, uint32_t flags, co
 // A request may carry two parts (a receive burst's frames, then a TX fill's
 // packets: BurstReq.n1): packets [lo, hi) on either side of n1 run with that
 // part's flags.
-template <bool LDSD>
+template <bool LDSD, bool SYS = false>
 __device__ __forceinline__ void burst_body(const BurstReq &h, const uint32_t *desc, uint32_t lo, uint32_t hi,
 					   uint32_t *out, uint32_t *meta, uint8_t *verdict, const void *zero,
 					   const uint8_t *base)
 {
 	const uint32_t n1 = h.n1 < h.n ? h.n1 : 0;
 	if (n1 > lo && n1 < hi) {
-		burst_part<LDSD>(h, h.flags, desc, lo, n1, out, meta, verdict, zero, base);
+		burst_part<LDSD, SYS>(h, h.flags, desc, lo, n1, out, meta, verdict, zero, base);
 		__syncthreads(); // (the body's LDS staging is reused)
-		burst_part<LDSD>(h, h.flags2, desc + 3 * (n1 - lo), n1, hi, out, meta, verdict, zero, base);
+		burst_part<LDSD, SYS>(h, h.flags2, desc + 3 * (n1 - lo), n1, hi, out, meta, verdict, zero, base);
 	} else {
-		burst_part<LDSD>(h, n1 && lo >= n1 ? h.flags2 : h.flags, desc, lo, hi, out, meta, verdict, zero, base);
+		burst_part<LDSD, SYS>(h, n1 && lo >= n1 ? h.flags2 : h.flags, desc, lo, hi, out, meta, verdict, zero,
+				      base);
 	}
+}
+
+// Can a one-workgroup request of n packets read its packet bytes in place
+// with the system-coherent body?  One packet per lane group must cover each
+// part in one pass (64 groups of 4 lanes up to 80 bytes, 16 of 16 lanes
+// above), with every packet within the body's S * G chunks (1536 bytes).
+__device__ __forceinline__ bool burst_sys_ok(const BurstReq &h, uint32_t n)
+{
+	return h.max_len <= 80 ? n <= 64 : (n <= 16 && h.max_len <= 1520);
 }
 
 // A request header the server can serve: the count it was told, inside the
@@ -560,11 +610,16 @@ __global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const 
 #endif
 			if (ok) {
 				// staged packet bytes are read from the scratch copy; packet
-				// bytes in place with plain loads, after the acquire
-				if (h.base)
-					__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+				// bytes in place by the system-coherent body, or with plain
+				// loads after the acquire (lab opts bit 256: always so)
 				const uint8_t *base = h.base ? reinterpret_cast<const uint8_t *>(h.base) : scratch + h.p_off;
-				burst_body<false>(h, sd, 0, n, o32, meta, ver, zero, base);
+				if (h.base && burst_sys_ok(h, n) && !(opts & 256)) {
+					burst_body<false, true>(h, sd, 0, n, o32, meta, ver, zero, base);
+				} else {
+					if (h.base)
+						__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+					burst_body<false>(h, sd, 0, n, o32, meta, ver, zero, base);
+				}
 				if (opts & 8) // lab: the body a second time (is a pass cold-start bound?)
 					burst_body<false>(h, sd, 0, n, o32, meta, ver, zero, base);
 			}

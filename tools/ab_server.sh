@@ -9,6 +9,7 @@ mkdir -p $O
 for i in 1 2; do
 	for v in head new; do
 		LD_LIBRARY_PATH=$PWD/tools/ab_$v timeout -k 10 120 tools/srvlat 64 > $O/srvlat_${v}_$i.log 2>&1 || exit 1
+		LD_LIBRARY_PATH=$PWD/tools/ab_$v timeout -k 10 120 tools/srvlat 64 fill > $O/srvlat_fill_${v}_$i.log 2>&1 || exit 1
 		LD_LIBRARY_PATH=$PWD/tools/ab_$v TXLOOP_BURSTS=1,16,64,256,2048 TXLOOP_NS=250 timeout -k 10 200 tools/txloop 0.1 > $O/txloop_${v}_$i.log 2>&1 || exit 1
 		echo "$v $i done"
 	done

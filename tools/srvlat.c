@@ -72,10 +72,14 @@ int main(int argc, char **argv)
 		fprintf(stderr, "srvlat: setup: %s\n", cgck_last_error());
 		return 1;
 	}
-	/* argv[2]: "raw" for CGCK_RAW requests (no header work), else the BSD verify flags */
-	const uint32_t vf = argc > 2 && !strcmp(argv[2], "raw")
-				    ? CGCK_RAW
-				    : CGCK_IP | CGCK_L4 | CGCK_VERIFY | CGCK_V_IP_ZERO_IS_FFFF | CGCK_V_UDP_ZERO_SKIP;
+	/* argv[2]: "raw" for CGCK_RAW requests (no header work), "fill" for an
+	 * in-place fill (the frames read where they lie in the registered ring,
+	 * the fields stored there), else the BSD verify flags (small requests
+	 * copy the frames into the request block) */
+	const int fill = argc > 2 && !strcmp(argv[2], "fill");
+	const uint32_t vf = argc > 2 && !strcmp(argv[2], "raw") ? CGCK_RAW
+			    : fill ? CGCK_IP | CGCK_L4 | CGCK_ZERO_FIELDS | CGCK_STORE
+				   : CGCK_IP | CGCK_L4 | CGCK_VERIFY | CGCK_V_IP_ZERO_IS_FFFF | CGCK_V_UDP_ZERO_SKIP;
 	const int bursts[] = {1, 32, 64, 65, 256, 2048};
 	for (unsigned bi = 0; bi < sizeof(bursts) / sizeof(bursts[0]); bi++) {
 		const int R = bursts[bi];
