@@ -427,6 +427,7 @@ static bool burst_all_alive(const cgck_ctx *c)
 // the last one completed (the pending ones are still in their slots).
 static int burst_restart(cgck_ctx *c)
 {
+	(void)hipSetDevice(c->device);
 	__atomic_store_n(&c->bbox->stop, 1u, __ATOMIC_RELEASE);
 	const hipError_t e = hipStreamSynchronize(c->bstream);
 	__atomic_store_n(&c->bbox->stop, 0u, __ATOMIC_RELEASE);
@@ -766,7 +767,6 @@ static int desc_host_impl(cgck_ctx *c, void *base, size_t bytes, const cgck_desc
 	// 256 x 64 B RX-window frames took 31 us at 256 packets per block (G4)
 	// against 19 us at 16 (tools/txburst).
 	const uint32_t hint = c->desc_len_hint;
-	HIP_TRY(hipSetDevice(c->device));
 	hipStream_t st = c->stream;
 	// registered through cgck_host_register (the per-thread cached lookup),
 	// else whatever HIP knows of the memory (a caller's hipHostMalloc)
@@ -822,6 +822,9 @@ static int desc_host_impl(cgck_ctx *c, void *base, size_t bytes, const cgck_desc
 		}
 		return burst_collect(c, &now);
 	}
+	// the launch paths below (the server's needs no current device: its
+	// calls name their stream, and a relaunch sets it)
+	HIP_TRY(hipSetDevice(c->device));
 	if (split) {
 		// a two-part request the server cannot take: each part computed at
 		// once on its own (the launch path takes one flag set)

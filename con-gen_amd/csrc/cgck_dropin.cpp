@@ -914,7 +914,8 @@ void Poster::pump(cgck_ctx *c, int kind, bool wait)
 		if (go)
 			collect(c, ri);
 	}
-	if (q[kRx].sent < q[kRx].count || q[kTx].sent < q[kTx].count) {
+	// only a kind with nothing in flight sends (send gathers for no other)
+	if ((inflight[kRx] < 0 && q[kRx].sent < q[kRx].count) || (inflight[kTx] < 0 && q[kTx].sent < q[kTx].count)) {
 		LAB_T0(t0);
 		send(c);
 		LAB_ADD(3, t0);

@@ -4,6 +4,7 @@
 #   tools/build_variant.sh NAME FILE 'SED-EXPR'   working tree + one sed edit
 #   tools/build_variant.sh NAME --rev REV         the sources of git revision REV
 #   tools/build_variant.sh NAME --tree            the working tree as it is (with $VARIANT_FLAGS)
+# VARIANT_PRODUCT=1: a product build (no -DCGCK_LAB) instead of a lab one.
 set -eu
 NAME=$1
 R=$(cd "$(dirname "$0")/.." && pwd)
@@ -22,8 +23,10 @@ else
 	if cmp -s "$R/con-gen_amd/csrc/$FILE" "$T/con-gen_amd/csrc/$FILE"; then echo "sed changed nothing" >&2; rm -rf "$T"; exit 1; fi
 fi
 cd "$T/con-gen_amd"
+LABFLAG=-DCGCK_LAB=1
+[ -n "${VARIANT_PRODUCT:-}" ] && LABFLAG=
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -Wall -Werror -mcode-object-version=5 \
-	-I"$T/include" -DCGCK_LAB=1 ${VARIANT_FLAGS:-} -shared -o "$R/con-gen_amd/$NAME.so" \
+	-I"$T/include" $LABFLAG ${VARIANT_FLAGS:-} -shared -o "$R/con-gen_amd/$NAME.so" \
 	csrc/*.hip csrc/*.cpp
 rm -rf "$T"
 echo "built con-gen_amd/$NAME.so"
