@@ -359,14 +359,29 @@ def bench_burst():
     burst, the RX window (cgck_rx_begin + the stack's per-packet verify calls
     + cgck_rx_end), and the deferred TX window on a registered ring.
     Host-resident, so PCIe/latency bound: never `value`.  Returns all rows."""
-    import subprocess
     exe = os.path.join(ROOT, "tools", "txburst")
     if not os.path.exists(exe):
         return None
-    r = subprocess.run([exe, "0.15"], capture_output=True, text=True, timeout=240)
+    r = run_pinned([exe, "0.15"], 240)
     if r.returncode != 0:
         return {"error": r.stderr.strip()[-300:]}
     return [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+
+
+def run_pinned(cmd, timeout):
+    """A host harness as a child process pinned to one core (the middle CPU
+    of this process's set, as cpu_burst pins the reference): the windows'
+    per-burst cost is mostly misses on GPU-written lines, and unpinned runs
+    of one build moved by up to 1.7x with the core they landed on
+    (profiles/r05/loop3/ab_host/unpinned/)."""
+    import subprocess
+    cpus = sorted(os.sched_getaffinity(0))
+    old = set(cpus)
+    try:
+        os.sched_setaffinity(0, {cpus[len(cpus) // 2]})  # the child inherits it
+        return subprocess.run(cmd, capture_output=True, text=True, timeout=timeout)
+    finally:
+        os.sched_setaffinity(0, old)
 
 
 def bench_loop():
@@ -376,11 +391,10 @@ def bench_loop():
     form (the reference's own functions, pipelined, coalesced, synchronous)
     the worker's us per iteration, its wait and the post-to-verdict latency.
     Host-resident: never `value`.  Returns all rows."""
-    import subprocess
     exe = os.path.join(ROOT, "tools", "txloop")
     if not os.path.exists(exe):
         return None
-    r = subprocess.run([exe, "0.1"], capture_output=True, text=True, timeout=300)
+    r = run_pinned([exe, "0.1"], 300)
     if r.returncode != 0:
         return {"error": r.stderr.strip()[-300:]}
     return [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
