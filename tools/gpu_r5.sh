@@ -36,7 +36,9 @@ for step in "$@"; do
 		run srvlat_64_raw 120 tools/srvlat 64 raw || exit 1 ;;
 	quick) run pytest_quick 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "burst or window or pipelined or rx_post or tx_" || exit 1 ;;
 	txburst) run txburst 400 tools/txburst 0.2 || exit 1 ;;
-	txloop) run txloop 400 tools/txloop 0.2 || exit 1 ;;
+	txloop) # pinned to the middle CPU of the allowed set, as bench.py pins it
+		C=$(python3 -c "import os; c=sorted(os.sched_getaffinity(0)); print(c[len(c)//2])")
+		run txloop 400 taskset -c $C tools/txloop 0.2 || exit 1 ;;
 	split) TXLOOP_SPLIT=1 run txloop_split 60 tools/txloop 0.5 || exit 1
 		TXLOOP_SPLIT=2 run txloop_split_reply 60 tools/txloop 0.5 || exit 1 ;;
 	splitlab) # the split timing with the Poster's phases (lab library)
