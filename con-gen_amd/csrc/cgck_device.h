@@ -190,6 +190,41 @@ __device__ __forceinline__ void store16(uint8_t *p, uint32_t v)
 	}
 }
 
+// Stores, or (SYS) system-coherent ones (sc0 sc1: written through to the
+// memory they name, complete when visible there) — the burst server's
+// outputs in host memory.
+template <bool SYS>
+__device__ __forceinline__ void st32p(CGCK_GLOBAL uint32_t *p, uint32_t v)
+{
+	if (SYS)
+		__hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+	else
+		*p = v;
+}
+
+template <bool SYS>
+__device__ __forceinline__ void st8p(CGCK_GLOBAL uint8_t *p, uint8_t v)
+{
+	if (SYS)
+		__hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+	else
+		*p = v;
+}
+
+template <bool SYS>
+__device__ __forceinline__ void store16p(uint8_t *p, uint32_t v)
+{
+	if (!SYS) {
+		store16(p, v);
+	} else if ((reinterpret_cast<uintptr_t>(p) & 1) == 0) {
+		__hip_atomic_store((CGCK_GLOBAL uint16_t *)p, (uint16_t)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+	} else {
+		__hip_atomic_store((CGCK_GLOBAL uint8_t *)p, (uint8_t)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+		__hip_atomic_store((CGCK_GLOBAL uint8_t *)p + 1, (uint8_t)(v >> 8), __ATOMIC_RELAXED,
+				   __HIP_MEMORY_SCOPE_SYSTEM);
+	}
+}
+
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 
 // Packet memory, descriptors and outputs are addressed through explicit

@@ -30,7 +30,10 @@ constexpr int kGrpStage = 2048;
 // memory the burst server reads in place, with system-coherent loads
 // (ld_sys16xN) instead of after a cache-invalidating acquire; the header
 // bytes come from the chunks (lane shuffles) rather than byte loads.
-template <int G, int S, int U, bool DESC, bool NT, bool LDSD = false, bool SYS = false>
+// SYSST: every store is a system-coherent one (sc0 sc1, written through to
+// host memory): the burst server's outputs and in-place fields, which it then
+// publishes after the stores' own completion instead of an L2 write-back.
+template <int G, int S, int U, bool DESC, bool NT, bool LDSD = false, bool SYS = false, bool SYSST = false>
 __device__ __forceinline__ void cksum_body(const KParams &p, uint32_t bid, uint32_t nb)
 {
 	__shared__ uint32_t so[kGrpStage];
@@ -215,19 +218,19 @@ __device__ __forceinline__ void cksum_body(const KParams &p, uint32_t bid, uint3
 				if (flags & CGCK_STORE) {
 					uint8_t *ipp = reinterpret_cast<uint8_t *>(pk[u].a0);
 					if (flags & CGCK_IP)
-						store16(ipp + 10, lo);
+						store16p<SYSST>(ipp + 10, lo);
 					if ((flags & CGCK_L4) && fo >= 0)
-						store16(ipp + hl + fo, hi);
+						store16p<SYSST>(ipp + hl + fo, hi);
 				}
 			}
 			if (stage)
 				so[k - wb] = lo | (hi << 16);
 			else if (p.out)
-				gbl(p.out)[k] = lo | (hi << 16);
+				st32p<SYSST>(gbl(p.out) + k, lo | (hi << 16));
 			if (p.verdict)
-				gbl(p.verdict)[k] = (uint8_t)verdict;
+				st8p<SYSST>(gbl(p.verdict) + k, (uint8_t)verdict);
 			if (rx && p.meta)
-				gbl(p.meta)[k] = rxm;
+				st32p<SYSST>(gbl(p.meta) + k, rxm);
 			if (p.bad) {
 				if (verdict & CGCK_BAD_IP)
 					atomicAdd(p.bad + 0, 1u);
@@ -312,11 +315,12 @@ __device__ __forceinline__ void burst_part(const BurstReq &h, uint32_t flags, co
 {
 	KParams p = {base, reinterpret_cast<const cgck_desc_t *>(desc), hi - lo, 0, 0, 0, flags,
 		     out ? out + lo : nullptr, verdict ? verdict + lo : nullptr, nullptr, 0, zero, meta + lo};
+	// (every server body stores system-coherent: SYSST, burst_publish)
 	if constexpr (SYS) { // burst_sys_ok: one packet per group covers the part
 		if (h.max_len <= 80)
-			cksum_body<4, 2, 1, true, false, false, true>(p, 0, 1);
+			cksum_body<4, 2, 1, true, false, false, true, true>(p, 0, 1);
 		else
-			cksum_body<16, 6, 1, true, false, false, true>(p, 0, 1);
+			cksum_body<16, 6, 1, true, false, false, true, true>(p, 0, 1);
 		return;
 	}
 	// A part the block covers in one pass with one packet per group runs
@@ -324,14 +328,14 @@ __device__ __forceinline__ void burst_part(const BurstReq &h, uint32_t flags, co
 	// VALU chain, which four unrolled packets per group quadruple.
 	if (h.max_len <= 80) {
 		if (hi - lo <= 64)
-			cksum_body<4, 2, 1, true, false, LDSD>(p, 0, 1);
+			cksum_body<4, 2, 1, true, false, LDSD, false, true>(p, 0, 1);
 		else
-			cksum_body<4, 2, 4, true, false, LDSD>(p, 0, 1);
+			cksum_body<4, 2, 4, true, false, LDSD, false, true>(p, 0, 1);
 	} else {
 		if (hi - lo <= 16)
-			cksum_body<16, 6, 1, true, false, LDSD>(p, 0, 1);
+			cksum_body<16, 6, 1, true, false, LDSD, false, true>(p, 0, 1);
 		else
-			cksum_body<16, 6, 4, true, false, LDSD>(p, 0, 1);
+			cksum_body<16, 6, 4, true, false, LDSD, false, true>(p, 0, 1);
 	}
 }
 
@@ -678,10 +682,17 @@ __global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const 
 		lab_t2 = __builtin_amdgcn_s_memrealtime();
 		const uint64_t lab_c2 = __builtin_amdgcn_s_memtime();
 #endif
-		// every thread's outputs (and in-place stores) written back to host
-		// memory before thread 0 publishes done[j]: a system-scope release per
-		// thread (one fence per request, noise next to the ~5 us round trip)
-		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+		// every thread's outputs (and in-place stores) in host memory before
+		// thread 0 publishes done[j].  The body's stores to host memory are
+		// system-coherent (SYSST: written through), so their own completion
+		// is enough: a wait per thread, the barrier, then done[j].  A
+		// system-scope release (an L2 write-back) before both cost ~2.3 us
+		// a request (tools/srvlat, profiles/r05/burst/release/).  Lab opts
+		// bit 2048: the release as before.
+		if (opts & 2048)
+			__builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+		else
+			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 		__syncthreads();
 #if CGCK_LAB
 		if (t == 0 && j == 0) {
@@ -694,7 +705,10 @@ __global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const 
 		}
 #endif
 		if (t == 0) {
-			__hip_atomic_store(&box->done[j], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+			if (opts & 2048)
+				__hip_atomic_store(&box->done[j], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+			else
+				__hip_atomic_store(&box->done[j], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 			if (j == 0 && K > 1 && W == 1)
 				relay_store(dcmd + (seq & 1), (uint64_t)seq | (uint64_t)n << 32);
 		}

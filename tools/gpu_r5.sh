@@ -32,6 +32,13 @@ for step in "$@"; do
 		run srvlat_64_base 120 tools/srvlat 64 || exit 1
 		CGCK_SERVER_OPTS=64 run srvlat_64_agentacq 120 tools/srvlat 64
 		CGCK_SERVER_OPTS=128 run srvlat_64_l1inv 120 tools/srvlat 64 ;;
+	srvlatrel) # the publish after the stores' own completion against the system release (opts 2048)
+		for i in 1 2; do
+			run srvlat_64_new$i 120 tools/srvlat 64 || exit 1
+			run srvlat_64_fill_new$i 120 tools/srvlat 64 fill || exit 1
+			CGCK_SERVER_OPTS=2048 run srvlat_64_rel$i 120 tools/srvlat 64 || exit 1
+			CGCK_SERVER_OPTS=2048 run srvlat_64_fill_rel$i 120 tools/srvlat 64 fill || exit 1
+		done ;;
 	srvlat) run srvlat_64 120 tools/srvlat 64 || exit 1
 		run srvlat_64_raw 120 tools/srvlat 64 raw || exit 1 ;;
 	quick) run pytest_quick 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "burst or window or pipelined or rx_post or tx_" || exit 1 ;;
