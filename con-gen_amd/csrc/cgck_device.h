@@ -467,6 +467,33 @@ __device__ __forceinline__ Pkt get_pkt(const KParams &p, uint64_t k)
 // The same over descriptors staged in the workgroup's LDS (the burst server's
 // slice path): p.desc is a generic pointer into LDS, read as ds_read.
 typedef __attribute__((address_space(3))) const uint32_t lds_u32;
+typedef __attribute__((address_space(3))) const u32x4_t lds_v4;
+typedef __attribute__((address_space(3))) const uint8_t lds_u8;
+
+// Packet bytes from global memory, or (LDSP) from LDS through a generic
+// pointer into it (the burst server's small request block, copied into LDS)
+template <bool NT, bool LDSP>
+__device__ __forceinline__ uint4 ldq(const uint4 *p)
+{
+	if constexpr (LDSP) {
+		const u32x4_t v = *(lds_v4 *)p;
+		return make_uint4(v[0], v[1], v[2], v[3]);
+	} else {
+		return ld<NT>(p);
+	}
+}
+
+template <bool NT, bool LDSP>
+__device__ __forceinline__ uint4 ldcq(const uint4 *c0, int i, int nch, const void *zero)
+{
+	return ldq<NT, LDSP>(nch > 0 ? c0 + min(i, nch - 1) : reinterpret_cast<const uint4 *>(zero));
+}
+
+template <bool LDSP>
+__device__ __forceinline__ uint32_t ld8q(uint64_t a)
+{
+	return LDSP ? (uint32_t) * (lds_u8 *)(const uint8_t *)a : (uint32_t)*gbl_at<const uint8_t>(a);
+}
 __device__ __forceinline__ Pkt get_pkt_lds(const KParams &p, uint64_t k)
 {
 	Pkt r;

@@ -33,7 +33,9 @@ constexpr int kGrpStage = 2048;
 // SYSST: every store is a system-coherent one (sc0 sc1, written through to
 // host memory): the burst server's outputs and in-place fields, which it then
 // publishes after the stores' own completion instead of an L2 write-back.
-template <int G, int S, int U, bool DESC, bool NT, bool LDSD = false, bool SYS = false, bool SYSST = false>
+// LDSP: packet bytes in LDS (p.base and p.zero generic pointers into it).
+template <int G, int S, int U, bool DESC, bool NT, bool LDSD = false, bool SYS = false, bool SYSST = false,
+	  bool LDSP = false>
 __device__ __forceinline__ void cksum_body(const KParams &p, uint32_t bid, uint32_t nb)
 {
 	__shared__ uint32_t so[kGrpStage];
@@ -82,14 +84,14 @@ __device__ __forceinline__ void cksum_body(const KParams &p, uint32_t bid, uint3
 			proto[u] = 0;
 			tl[u] = 0;
 			if (!SYS && need_hdr && pk[u].ok && span > 0) {
-				b0[u] = *gbl_at<const uint8_t>(a0);
+				b0[u] = ld8q<LDSP>(a0);
 				if (span > 9)
-					proto[u] = *gbl_at<const uint8_t>(a0 + 9);
+					proto[u] = ld8q<LDSP>(a0 + 9);
 				// kFlagRx: the frame's own length field, read with the
 				// chunks (one round trip), so its coverage is decided after
 				// the loads and the surplus chunks are masked by position
 				if (rx && span >= 20)
-					tl[u] = (uint32_t)*gbl_at<const uint8_t>(a0 + 2) << 8 | *gbl_at<const uint8_t>(a0 + 3);
+					tl[u] = ld8q<LDSP>(a0 + 2) << 8 | ld8q<LDSP>(a0 + 3);
 			}
 			const uint4 *c0 = reinterpret_cast<const uint4 *>(a0 & ~(uint64_t)15);
 			// clamped: chunks past the packet re-read its last chunk and
@@ -123,7 +125,7 @@ __device__ __forceinline__ void cksum_body(const KParams &p, uint32_t bid, uint3
 			} else {
 #pragma unroll
 				for (int s = 0; s < S; ++s)
-					v[u][s] = ldc<NT>(c0, s * G + gl, nch[u], p.zero);
+					v[u][s] = ldcq<NT, LDSP>(c0, s * G + gl, nch[u], p.zero);
 			}
 		}
 #pragma unroll
@@ -153,7 +155,7 @@ __device__ __forceinline__ void cksum_body(const KParams &p, uint32_t bid, uint3
 			const uint4 *c0 = reinterpret_cast<const uint4 *>(pk[u].a0 & ~(uint64_t)15);
 			for (int s = S; __any(s * G < nch[u]); ++s) {
 				const int k = s * G + gl;
-				uint4 w = k < nch[u] ? ld<NT>(c0 + k) : make_uint4(0, 0, 0, 0);
+				uint4 w = k < nch[u] ? ldq<NT, LDSP>(c0 + k) : make_uint4(0, 0, 0, 0);
 				if (need_hdr && s * G * 16 < 96)
 					eat<true>(pt, w, k, q, len, hl, fo, flags);
 				else
@@ -307,8 +309,8 @@ __device__ __forceinline__ uint64_t sys_relaxed64(const uint64_t *p)
 }
 
 // The group body over a request's packets [lo, hi) (block 0 of 1); desc is
-// packet lo's descriptor (in LDS when LDSD).
-template <bool LDSD, bool SYS = false>
+// packet lo's descriptor (in LDS when LDSD); LDSP: the packet bytes too.
+template <bool LDSD, bool SYS = false, bool LDSP = false>
 __device__ __forceinline__ void burst_part(const BurstReq &h, uint32_t flags, const uint32_t *desc, uint32_t lo,
 					   uint32_t hi, uint32_t *out, uint32_t *meta, uint8_t *verdict,
 					   const void *zero, const uint8_t *base)
@@ -318,9 +320,16 @@ __device__ __forceinline__ void burst_part(const BurstReq &h, uint32_t flags, co
 	// (every server body stores system-coherent: SYSST, burst_publish)
 	if constexpr (SYS) { // burst_sys_ok: one packet per group covers the part
 		if (h.max_len <= 80)
-			cksum_body<4, 2, 1, true, false, false, true, true>(p, 0, 1);
+			cksum_body<4, 2, 1, true, false, LDSD, true, true>(p, 0, 1);
 		else
-			cksum_body<16, 6, 1, true, false, false, true, true>(p, 0, 1);
+			cksum_body<16, 6, 1, true, false, LDSD, true, true>(p, 0, 1);
+		return;
+	}
+	if constexpr (LDSP) { // a block of <= 8 KiB: at most ~64 small packets
+		if (h.max_len <= 80)
+			cksum_body<4, 2, 1, true, false, LDSD, false, true, true>(p, 0, 1);
+		else
+			cksum_body<16, 6, 1, true, false, LDSD, false, true, true>(p, 0, 1);
 		return;
 	}
 	// A part the block covers in one pass with one packet per group runs
@@ -342,19 +351,19 @@ __device__ __forceinline__ void burst_part(const BurstReq &h, uint32_t flags, co
 // A request may carry two parts (a receive burst's frames, then a TX fill's
 // packets: BurstReq.n1): packets [lo, hi) on either side of n1 run with that
 // part's flags.
-template <bool LDSD, bool SYS = false>
+template <bool LDSD, bool SYS = false, bool LDSP = false>
 __device__ __forceinline__ void burst_body(const BurstReq &h, const uint32_t *desc, uint32_t lo, uint32_t hi,
 					   uint32_t *out, uint32_t *meta, uint8_t *verdict, const void *zero,
 					   const uint8_t *base)
 {
 	const uint32_t n1 = h.n1 < h.n ? h.n1 : 0;
 	if (n1 > lo && n1 < hi) {
-		burst_part<LDSD, SYS>(h, h.flags, desc, lo, n1, out, meta, verdict, zero, base);
+		burst_part<LDSD, SYS, LDSP>(h, h.flags, desc, lo, n1, out, meta, verdict, zero, base);
 		__syncthreads(); // (the body's LDS staging is reused)
-		burst_part<LDSD, SYS>(h, h.flags2, desc + 3 * (n1 - lo), n1, hi, out, meta, verdict, zero, base);
+		burst_part<LDSD, SYS, LDSP>(h, h.flags2, desc + 3 * (n1 - lo), n1, hi, out, meta, verdict, zero, base);
 	} else {
-		burst_part<LDSD, SYS>(h, n1 && lo >= n1 ? h.flags2 : h.flags, desc, lo, hi, out, meta, verdict, zero,
-				      base);
+		burst_part<LDSD, SYS, LDSP>(h, n1 && lo >= n1 ? h.flags2 : h.flags, desc, lo, hi, out, meta, verdict,
+					    zero, base);
 	}
 }
 
@@ -432,6 +441,10 @@ __global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const 
 	__shared__ uint32_t cmd, cmd_n, cmd_seq;
 	__shared__ uint4 hdr_w[4];
 	__shared__ uint32_t sdesc[3 * kSliceLds];
+	__shared__ uint4 sblock[kBurstFirst / 16]; // a small request's block (the one-workgroup path)
+	__shared__ uint4 szero;                    // the zero chunk of the LDS-resident body
+	if (threadIdx.x == 0)
+		szero = make_uint4(0, 0, 0, 0);
 	const int t = threadIdx.x;
 	const uint32_t j = blockIdx.x, K = gridDim.x;
 	const uint32_t rslot = burst_resp_slot(max_pkts);
@@ -569,40 +582,56 @@ __global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const 
 			static_assert(kBurstFirst == 2 * 16 * 256, "two 16-byte loads per thread");
 			uint4 v0, v1;
 			ld_sys16x2(src + t, src + 256 + t, v0, v1);
-			dst[t] = v0;
-			dst[256 + t] = v1;
 			if (t < 4)
 				hdr_w[t] = v0;
+			// A block of up to kBurstFirst bytes (a small request: every
+			// drop-in call, a burst of up to ~64 small frames) stays in LDS:
+			// descriptors and staged bytes are read from there (ds_read, no
+			// L2 round trips); a larger one is copied into device scratch.
+			sblock[t] = v0;
+			sblock[256 + t] = v1;
 			__syncthreads();
 			ok = burst_hdr_ok(h, n, max_pkts, cap);
-			const uint32_t chunks = ok ? (h.bytes + 15) / 16 : 0;
-			// the rest of a larger block, 16 loads in flight per thread (64 KiB
-			// a round trip), plain loads after the acquire
-			if (chunks > kBurstFirst / 16)
+			// (lab opts bit 4096: the scratch copy for every block, the A/B)
+			const bool in_lds = !ok || (h.bytes <= kBurstFirst && !(opts & 4096));
+			const uint32_t *sd;
+			if (in_lds) {
+				sd = reinterpret_cast<const uint32_t *>(reinterpret_cast<const uint8_t *>(sblock) + sizeof(BurstReq));
+				if (ok) {
+					const uint64_t limit = burst_limit(h);
+					for (uint32_t i = t; i < n; i += 256)
+						ok = ok && desc_inside(((lds_u32 *)sd)[3 * i], ((lds_u32 *)sd)[3 * i + 1],
+								       ((lds_u32 *)sd)[3 * i + 2], limit);
+				}
+			} else {
+				dst[t] = v0;
+				dst[256 + t] = v1;
+				const uint32_t chunks = (h.bytes + 15) / 16;
+				// the rest of the block, 16 loads in flight per thread (64
+				// KiB a round trip), plain loads after the acquire
 				__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-			for (uint32_t at = kBurstFirst / 16; at < chunks; at += 16 * 256) {
-				uint4 x[16];
+				for (uint32_t at = kBurstFirst / 16; at < chunks; at += 16 * 256) {
+					uint4 x[16];
 #pragma unroll
-				for (int k = 0; k < 16; ++k) {
-					const uint32_t i = at + k * 256 + t;
-					x[k] = i < chunks ? src[i] : make_uint4(0, 0, 0, 0);
-				}
+					for (int k = 0; k < 16; ++k) {
+						const uint32_t i = at + k * 256 + t;
+						x[k] = i < chunks ? src[i] : make_uint4(0, 0, 0, 0);
+					}
 #pragma unroll
-				for (int k = 0; k < 16; ++k) {
-					const uint32_t i = at + k * 256 + t;
-					if (i < chunks)
-						dst[i] = x[k];
+					for (int k = 0; k < 16; ++k) {
+						const uint32_t i = at + k * 256 + t;
+						if (i < chunks)
+							dst[i] = x[k];
+					}
 				}
-			}
-			// scratch stores visible to the workgroup (its waves share one
-			// CU's L1: workgroup scope), and no line of an earlier request's
-			// copy left in that L1
-			__builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-			__syncthreads();
-			__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-			asm volatile("buffer_inv sc0" ::: "memory");
-			const uint32_t *sd = reinterpret_cast<const uint32_t *>(scratch + sizeof(BurstReq));
-			if (ok) {
+				// scratch stores visible to the workgroup (its waves share
+				// one CU's L1: workgroup scope), and no line of an earlier
+				// request's copy left in that L1
+				__builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+				__syncthreads();
+				__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+				asm volatile("buffer_inv sc0" ::: "memory");
+				sd = reinterpret_cast<const uint32_t *>(scratch + sizeof(BurstReq));
 				const uint64_t limit = burst_limit(h);
 				for (uint32_t i = t; i < n; i += 256)
 					ok = ok && desc_inside(gbl(sd)[3 * i], gbl(sd)[3 * i + 1], gbl(sd)[3 * i + 2], limit);
@@ -613,19 +642,28 @@ __global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const 
 			lab_c1 = __builtin_amdgcn_s_memtime();
 #endif
 			if (ok) {
-				// staged packet bytes are read from the scratch copy; packet
-				// bytes in place by the system-coherent body, or with plain
-				// loads after the acquire (lab opts bit 256: always so)
-				const uint8_t *base = h.base ? reinterpret_cast<const uint8_t *>(h.base) : scratch + h.p_off;
-				if (h.base && burst_sys_ok(h, n) && !(opts & 256)) {
-					burst_body<false, true>(h, sd, 0, n, o32, meta, ver, zero, base);
+				// staged packet bytes are read from the LDS or scratch copy;
+				// packet bytes in place by the system-coherent body, or with
+				// plain loads after the acquire (lab opts bit 256: always so)
+				const bool sys = h.base && burst_sys_ok(h, n) && !(opts & 256);
+				if (h.base && !sys)
+					__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+				if (in_lds) {
+					const uint8_t *base = h.base ? reinterpret_cast<const uint8_t *>(h.base)
+								     : reinterpret_cast<const uint8_t *>(sblock) + h.p_off;
+					if (sys)
+						burst_body<true, true>(h, sd, 0, n, o32, meta, ver, zero, base);
+					else if (h.base)
+						burst_body<true>(h, sd, 0, n, o32, meta, ver, zero, base);
+					else
+						burst_body<true, false, true>(h, sd, 0, n, o32, meta, ver, &szero, base);
 				} else {
-					if (h.base)
-						__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-					burst_body<false>(h, sd, 0, n, o32, meta, ver, zero, base);
+					const uint8_t *base = h.base ? reinterpret_cast<const uint8_t *>(h.base) : scratch + h.p_off;
+					if (sys)
+						burst_body<false, true>(h, sd, 0, n, o32, meta, ver, zero, base);
+					else
+						burst_body<false>(h, sd, 0, n, o32, meta, ver, zero, base);
 				}
-				if (opts & 8) // lab: the body a second time (is a pass cold-start bound?)
-					burst_body<false>(h, sd, 0, n, o32, meta, ver, zero, base);
 			}
 		} else {
 			// Slice [lo, hi) in passes of up to kSliceLds descriptors: the

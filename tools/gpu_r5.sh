@@ -39,6 +39,13 @@ for step in "$@"; do
 			CGCK_SERVER_OPTS=2048 run srvlat_64_rel$i 120 tools/srvlat 64 || exit 1
 			CGCK_SERVER_OPTS=2048 run srvlat_64_fill_rel$i 120 tools/srvlat 64 fill || exit 1
 		done ;;
+	srvlatlds) # a small request's block in LDS against the scratch copy (opts 4096)
+		for i in 1 2; do
+			run srvlat_64_lds$i 120 tools/srvlat 64 || exit 1
+			run srvlat_64_fill_lds$i 120 tools/srvlat 64 fill || exit 1
+			CGCK_SERVER_OPTS=4096 run srvlat_64_scr$i 120 tools/srvlat 64 || exit 1
+			CGCK_SERVER_OPTS=4096 run srvlat_64_fill_scr$i 120 tools/srvlat 64 fill || exit 1
+		done ;;
 	srvlat) run srvlat_64 120 tools/srvlat 64 || exit 1
 		run srvlat_64_raw 120 tools/srvlat 64 raw || exit 1 ;;
 	quick) run pytest_quick 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "burst or window or pipelined or rx_post or tx_" || exit 1 ;;
