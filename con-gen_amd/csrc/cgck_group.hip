@@ -310,14 +310,18 @@ __device__ __forceinline__ uint64_t sys_relaxed64(const uint64_t *p)
 
 // The group body over a request's packets [lo, hi) (block 0 of 1); desc is
 // packet lo's descriptor (in LDS when LDSD); LDSP: the packet bytes too.
-template <bool LDSD, bool SYS = false, bool LDSP = false>
+template <bool LDSD, bool SYS = false, bool LDSP = false, bool WT = true>
 __device__ __forceinline__ void burst_part(const BurstReq &h, uint32_t flags, const uint32_t *desc, uint32_t lo,
 					   uint32_t hi, uint32_t *out, uint32_t *meta, uint8_t *verdict,
 					   const void *zero, const uint8_t *base)
 {
 	KParams p = {base, reinterpret_cast<const cgck_desc_t *>(desc), hi - lo, 0, 0, 0, flags,
 		     out ? out + lo : nullptr, verdict ? verdict + lo : nullptr, nullptr, 0, zero, meta + lo};
-	// (every server body stores system-coherent: SYSST, burst_publish)
+	// WT: the body's stores to host memory are system-coherent (SYSST),
+	// published after their own completion (a one-workgroup request); a
+	// wide request's slices store plainly and publish after an L2 write-back
+	// (thousands of written-through 4-byte stores leave as as many fabric
+	// writes: 2048 x 1500 B in place 79 -> 86 us, tools/e2e.py)
 	if constexpr (SYS) { // burst_sys_ok: one packet per group covers the part
 		if (h.max_len <= 80)
 			cksum_body<4, 2, 1, true, false, LDSD, true, true>(p, 0, 1);
@@ -337,32 +341,32 @@ __device__ __forceinline__ void burst_part(const BurstReq &h, uint32_t flags, co
 	// VALU chain, which four unrolled packets per group quadruple.
 	if (h.max_len <= 80) {
 		if (hi - lo <= 64)
-			cksum_body<4, 2, 1, true, false, LDSD, false, true>(p, 0, 1);
+			cksum_body<4, 2, 1, true, false, LDSD, false, WT>(p, 0, 1);
 		else
-			cksum_body<4, 2, 4, true, false, LDSD, false, true>(p, 0, 1);
+			cksum_body<4, 2, 4, true, false, LDSD, false, WT>(p, 0, 1);
 	} else {
 		if (hi - lo <= 16)
-			cksum_body<16, 6, 1, true, false, LDSD, false, true>(p, 0, 1);
+			cksum_body<16, 6, 1, true, false, LDSD, false, WT>(p, 0, 1);
 		else
-			cksum_body<16, 6, 4, true, false, LDSD, false, true>(p, 0, 1);
+			cksum_body<16, 6, 4, true, false, LDSD, false, WT>(p, 0, 1);
 	}
 }
 
 // A request may carry two parts (a receive burst's frames, then a TX fill's
 // packets: BurstReq.n1): packets [lo, hi) on either side of n1 run with that
 // part's flags.
-template <bool LDSD, bool SYS = false, bool LDSP = false>
+template <bool LDSD, bool SYS = false, bool LDSP = false, bool WT = true>
 __device__ __forceinline__ void burst_body(const BurstReq &h, const uint32_t *desc, uint32_t lo, uint32_t hi,
 					   uint32_t *out, uint32_t *meta, uint8_t *verdict, const void *zero,
 					   const uint8_t *base)
 {
 	const uint32_t n1 = h.n1 < h.n ? h.n1 : 0;
 	if (n1 > lo && n1 < hi) {
-		burst_part<LDSD, SYS, LDSP>(h, h.flags, desc, lo, n1, out, meta, verdict, zero, base);
+		burst_part<LDSD, SYS, LDSP, WT>(h, h.flags, desc, lo, n1, out, meta, verdict, zero, base);
 		__syncthreads(); // (the body's LDS staging is reused)
-		burst_part<LDSD, SYS, LDSP>(h, h.flags2, desc + 3 * (n1 - lo), n1, hi, out, meta, verdict, zero, base);
+		burst_part<LDSD, SYS, LDSP, WT>(h, h.flags2, desc + 3 * (n1 - lo), n1, hi, out, meta, verdict, zero, base);
 	} else {
-		burst_part<LDSD, SYS, LDSP>(h, n1 && lo >= n1 ? h.flags2 : h.flags, desc, lo, hi, out, meta, verdict,
+		burst_part<LDSD, SYS, LDSP, WT>(h, n1 && lo >= n1 ? h.flags2 : h.flags, desc, lo, hi, out, meta, verdict,
 					    zero, base);
 	}
 }
@@ -707,7 +711,7 @@ __global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const 
 				if (!ok)
 					break;
 				const uint8_t *base = h.base ? reinterpret_cast<const uint8_t *>(h.base) : req + h.p_off;
-				burst_body<true>(h, sdesc, c0, c1, o32, meta, ver, zero, base);
+				burst_body<true, false, false, false>(h, sdesc, c0, c1, o32, meta, ver, zero, base);
 				__syncthreads(); // the next pass rewrites sdesc
 			}
 		}
@@ -721,16 +725,18 @@ __global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const 
 		const uint64_t lab_c2 = __builtin_amdgcn_s_memtime();
 #endif
 		// every thread's outputs (and in-place stores) in host memory before
-		// thread 0 publishes done[j].  The body's stores to host memory are
-		// system-coherent (SYSST: written through), so their own completion
-		// is enough: a wait per thread, the barrier, then done[j].  A
-		// system-scope release (an L2 write-back) before both cost ~2.3 us
-		// a request (tools/srvlat, profiles/r05/burst/release/).  Lab opts
-		// bit 2048: the release as before.
-		if (opts & 2048)
-			__builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-		else
+		// thread 0 publishes done[j].  A one-workgroup request's bodies store
+		// to host memory system-coherent (WT: written through), so their own
+		// completion is enough: a wait per thread, the barrier, then done[j]
+		// (a system-scope release, an L2 write-back, before both cost up to
+		// ~1 us a request: tools/srvlat, profiles/r05/burst/release/); a
+		// wide request's slices store plainly and publish after the release.
+		// Lab opts bit 2048: the release for every request.
+		const bool wt = one_wg && !(opts & 2048);
+		if (wt)
 			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+		else
+			__builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
 		__syncthreads();
 #if CGCK_LAB
 		if (t == 0 && j == 0) {
@@ -743,10 +749,10 @@ __global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const 
 		}
 #endif
 		if (t == 0) {
-			if (opts & 2048)
-				__hip_atomic_store(&box->done[j], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-			else
+			if (wt)
 				__hip_atomic_store(&box->done[j], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+			else
+				__hip_atomic_store(&box->done[j], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 			if (j == 0 && K > 1 && W == 1)
 				relay_store(dcmd + (seq & 1), (uint64_t)seq | (uint64_t)n << 32);
 		}
