@@ -5,7 +5,10 @@ seq space ahead, as a word untouched for 2^31 requests would compare).  The
 first requests after it — narrow ones, which those workgroups have no slice
 of — must bring every done word up to date, so the wide requests that
 follow are not reported served before their slices are written; results
-stay exact across the wrap."""
+stay exact across the wrap.  tools/gpu_r5.sh runs it with CGCK_SERVER_OPTS=512
+(every workgroup but the leader starts its slice 20 us late), so that its
+control — the same run with the refresh switched off (opts 528) — fails
+deterministically instead of by timing."""
 import ctypes
 import os
 
