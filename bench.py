@@ -438,6 +438,14 @@ def loop_summary(rows):
             cross[f] = first
         out["crossover"][key] = cross
     out["lone_latency_us"] = {r["burst"]: r["us_latency"] for r in rows if r.get("mode") == "lone"}
+    # a cell that processed no burst measured nothing (its figures are null,
+    # tools/txloop.c): listed, never a crossover win, and the leg not exact
+    empty = [f"{r['mix']}@{r['stack_ns_per_frame']:g}ns+{r['stack_us_fixed']:g}us/{r['form']}/{r['burst']}"
+             f" (iters {r.get('iters')}, longest {r.get('max_iter_us')} us)"
+             for r in loop if not r.get("bursts", 1)]
+    out["empty_cells"] = empty
+    if empty:
+        out["exact"] = False
     return out
 
 

@@ -70,6 +70,8 @@ EXPORTS = (
     "cgck_ctx_set_kernel", "cgck_synth_imix_ring", "cgck_burst_request", "cgck_host_device_ptr",
     "cgck_rx_post", "cgck_rx_begin_posted", "cgck_tx_post", "cgck_tx_complete",
     "cgck_rx_pending", "cgck_rx_ready", "cgck_tx_pending", "cgck_tx_ready",
+    "cgck_window_stats_n", "cgck_thread_bind", "cgck_thread_device",
+    "cgck_test_burst_seq", "cgck_test_burst_stale",
 )
 # Descriptor layout hint (cgck_set_desc_layout)
 LAYOUT_ANY = 0
@@ -160,6 +162,9 @@ def bind(path):
     if hasattr(L, "cgck_rx_post"):
         L.cgck_rx_post.argtypes = [_vp, ctypes.c_size_t, _vp, _u64]
     L.cgck_window_stats.argtypes = [ctypes.POINTER(_u64)]
+    if hasattr(L, "cgck_window_stats_n"):   # ABI additions of round 6
+        L.cgck_window_stats_n.argtypes = [ctypes.POINTER(_u64), ctypes.c_int]
+        L.cgck_thread_bind.argtypes = [ctypes.c_int]
     L.cgck_ctx_last_kernel.restype = ctypes.c_char_p
     L.cgck_ctx_last_kernel.argtypes = [_vp]
     return L
@@ -311,6 +316,23 @@ def window_stats():
     a = (_u64 * 4)()
     _check(load().cgck_window_stats(a), "cgck_window_stats")
     return list(a)
+
+
+def window_stats_n():
+    """window_stats() plus [4]: TX-window calls queued on a header of the
+    last closed RX window's frames (cgck_window_stats_n)."""
+    a = (_u64 * 8)()
+    k = _check(load().cgck_window_stats_n(a, 8), "cgck_window_stats_n")
+    return list(a)[:k]
+
+
+def thread_bind(device):
+    """cgck_thread_bind: this thread's drop-in context goes on `device`."""
+    return _check(load().cgck_thread_bind(device), "cgck_thread_bind")
+
+
+def thread_device():
+    return load().cgck_thread_device()
 
 
 _err_cb = None

@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <errno.h>
+#include <sched.h>
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -331,24 +332,94 @@ static uint32_t server_opts()
 // device memory a later server may get again) never matches another's tag.
 static std::atomic<uint32_t> g_burst_epoch{0};
 
-// No server kernel runs while a host mapping changes: every request, launch
-// and close holds g_map_mu shared; cgck_host_register / _unregister hold it
-// exclusively and drain every open server first (the next request relaunches
-// it).  g_srv lists the contexts with an open server.
+// No server kernel runs while a host mapping changes.  cgck_host_register /
+// _unregister (and burst open / close) take g_map_wr, raise g_map_changing,
+// wait until no context with a server is inside a request (its bbusy word),
+// and drain every open server (the next request relaunches it).  A request
+// (post, wait, relaunch) runs inside a MapGuard on its own context: it sets
+// the context's bbusy and then checks g_map_changing (both sequentially
+// consistent, so either the writer sees the context busy or the request sees
+// the change and steps back until it is over).  The request path thus writes
+// only its own context's line and reads a line no request writes: no
+// process-wide lock or shared read-modify-write per request (32 workers each
+// posting bursts do not bounce a lock line).  g_srv lists the
+// contexts with an open server (changed under g_map_wr).
 namespace {
-std::shared_mutex g_map_mu;
+std::mutex g_map_wr;
+std::atomic<uint32_t> g_map_changing{0};
 std::mutex g_srv_mu;
 std::vector<cgck_ctx *> g_srv;
+
+class MapGuard {
+      public:
+	explicit MapGuard(cgck_ctx *c) : c_(c)
+	{
+		for (;;) {
+			__atomic_store_n(&c_->bbusy, 1u, __ATOMIC_SEQ_CST);
+			if (!g_map_changing.load(std::memory_order_seq_cst))
+				return;
+			__atomic_store_n(&c_->bbusy, 0u, __ATOMIC_RELEASE);
+			for (uint32_t k = 0; g_map_changing.load(std::memory_order_acquire); k++) {
+				if (k < 4096)
+					__builtin_ia32_pause();
+				else
+					sched_yield();
+			}
+		}
+	}
+	~MapGuard() { __atomic_store_n(&c_->bbusy, 0u, __ATOMIC_RELEASE); }
+	MapGuard(const MapGuard &) = delete;
+	MapGuard &operator=(const MapGuard &) = delete;
+
+      private:
+	cgck_ctx *c_;
+};
+
+// The writer side: g_map_wr held; no request of any server context is in
+// flight on the host side when it returns (ended by ~MapChange).
+class MapChange {
+      public:
+	MapChange() : lk_(g_map_wr)
+	{
+		g_map_changing.store(1, std::memory_order_seq_cst);
+		std::lock_guard<std::mutex> lk(g_srv_mu);
+		for (cgck_ctx *c : g_srv)
+			for (uint32_t k = 0; __atomic_load_n(&c->bbusy, __ATOMIC_SEQ_CST); k++) {
+				if (k < 4096)
+					__builtin_ia32_pause();
+				else
+					sched_yield();
+			}
+	}
+	~MapChange() { g_map_changing.store(0, std::memory_order_release); }
+	MapChange(const MapChange &) = delete;
+	MapChange &operator=(const MapChange &) = delete;
+
+      private:
+	std::lock_guard<std::mutex> lk_;
+};
 } // namespace
 
 static bool burst_all_alive(const cgck_ctx *c);
 static int burst_restart(cgck_ctx *c);
 
+// Requests complete in order, so the last one known complete is the latest
+// seq collected, whatever order the posted requests are collected in (the
+// pipelined windows collect a TX fill, then the older RX burst that shares
+// nothing with it).  bdone only moves forward: a relaunch starts after it, and
+// one that started after an older seq would have its leader poll a slot the
+// host has since posted a later request into.
+static void burst_done_at(cgck_ctx *c, uint32_t seq)
+{
+	if ((int32_t)(seq - c->bdone) > 0)
+		c->bdone = seq;
+}
+
 // Serve every request posted to c and not collected yet (the seqs after
 // bdone up to bseq: a pipelined window's burst or fill), relaunching the
 // server if it idled out, without collecting them: their outputs stay in
 // their slots for the poster's own collect, which then finds them done.
-// The caller holds g_map_mu exclusively, so neither seq moves meanwhile.
+// The caller holds a MapChange, so neither seq moves meanwhile.
 // A request not served in 2 s is abandoned (the next launch starts after
 // it; its poster's collect times out): it must not be served after the
 // mapping it reads has changed.
@@ -360,7 +431,8 @@ static void burst_finish_posted(cgck_ctx *c)
 		const uint32_t n = (uint32_t)(__atomic_load_n(&b->req[s & 1], __ATOMIC_ACQUIRE) >> 32);
 		const uint32_t W = burst_wgs(n, c->bwgs, c->bper);
 		const double t0 = now_s();
-		for (uint32_t j = 0, spin = 0; j < W;) {
+		uint32_t j = 0;
+		for (uint32_t spin = 0; j < W;) {
 			if ((int32_t)(__atomic_load_n(&b->done[j], __ATOMIC_ACQUIRE) - s) >= 0) {
 				j++;
 				continue;
@@ -369,17 +441,21 @@ static void burst_finish_posted(cgck_ctx *c)
 			if ((++spin & 1023) != 0)
 				continue;
 			if (!burst_all_alive(c) && burst_restart(c) != 0)
-				break;
+				return;
 			if (now_s() - t0 > 2.0) {
 				c->bdone = c->bseq;
 				return;
 			}
 		}
+		// served: the relaunch after the mapping change starts after it (its
+		// outputs stay in the slot for the poster's collect, which finds its
+		// done words past it), so it is never served again over the new mapping
+		burst_done_at(c, s);
 	}
 }
 
 // Stop every open server and wait until its workgroups have left (caller
-// holds g_map_mu exclusively, so no request is posted meanwhile).  Requests
+// holds a MapChange, so no request is posted meanwhile).  Requests
 // already posted are served first (burst_finish_posted): a relaunch after
 // the mapping change must not read or store through a range that is gone.
 static void burst_quiesce_all()
@@ -499,18 +575,6 @@ static const uint8_t *burst_resp(const cgck_ctx *c, uint32_t seq)
 	return c->bresp + (size_t)(seq & 1) * burst_resp_slot(c->bmax);
 }
 
-// Requests complete in order, so the last one known complete is the latest
-// seq collected, whatever order the posted requests are collected in (the
-// pipelined windows collect a TX fill, then the older RX burst that shares
-// nothing with it).  bdone only moves forward: a relaunch starts after it, and
-// one that started after an older seq would have its leader poll a slot the
-// host has since posted a later request into.
-static void burst_done_at(cgck_ctx *c, uint32_t seq)
-{
-	if ((int32_t)(seq - c->bdone) > 0)
-		c->bdone = seq;
-}
-
 // Wait until request seq (n packets) is served.  Requests complete in order,
 // so a workgroup's done word at or past seq means its slice is in.
 static int burst_wait(cgck_ctx *c, uint32_t seq, uint32_t n, uint64_t range)
@@ -518,7 +582,7 @@ static int burst_wait(cgck_ctx *c, uint32_t seq, uint32_t n, uint64_t range)
 #if CGCK_LAB
 	const uint64_t tl0 = __builtin_ia32_rdtsc();
 #endif
-	std::shared_lock<std::shared_mutex> map_lk(g_map_mu);
+	MapGuard map_g(c);
 #if CGCK_LAB
 	LAB_TICK(4, tl0);
 	const uint64_t tl1 = __builtin_ia32_rdtsc();
@@ -635,7 +699,7 @@ int cgck::burst_ready(cgck_ctx *c, const BurstPending *p)
 			// its last poll is relaunched here, as burst_wait would, so a
 			// caller that only ever asks does not wait forever
 			if (!burst_all_alive(c)) {
-				std::shared_lock<std::shared_mutex> map_lk(g_map_mu);
+				MapGuard map_g(c);
 				(void)burst_restart(c);
 			}
 			return 0;
@@ -661,7 +725,7 @@ static int burst_slot_free(cgck_ctx *c, uint8_t **block)
 static int burst_post(cgck_ctx *c, const uint8_t *base_dev, uint64_t range, uint64_t n, uint32_t flags,
 		      uint32_t max_len, const BurstLayout &L, uint32_t *seq_out, const DescSplit *split = nullptr)
 {
-	std::shared_lock<std::shared_mutex> map_lk(g_map_mu);
+	MapGuard map_g(c);
 	BurstBox *b = c->bbox;
 	const uint32_t seq = burst_next(c->bseq);
 	BurstReq *r = (BurstReq *)burst_block(c, seq);
@@ -1048,7 +1112,7 @@ extern "C" int cgck_host_register(void *ptr, size_t bytes)
 			       "and re-faults under a registration; register a mapping of its own (mmap, hugetlbfs, the "
 			       "transport's pool)",
 			       ptr, bytes);
-	std::unique_lock<std::shared_mutex> map_lk(g_map_mu);
+	MapChange map_c;
 	burst_quiesce_all();
 	HIP_TRY(hipHostRegister(ptr, bytes, hipHostRegisterDefault));
 	void *dev = nullptr;
@@ -1076,7 +1140,7 @@ extern "C" int cgck_host_device_ptr(const void *ptr, size_t bytes, void **dev)
 
 extern "C" int cgck_host_unregister(void *ptr)
 {
-	std::unique_lock<std::shared_mutex> map_lk(g_map_mu);
+	MapChange map_c;
 	burst_quiesce_all();
 	{
 		std::unique_lock<std::shared_mutex> lk(g_reg_mu);
@@ -1230,7 +1294,8 @@ extern "C" int cgck_burst_open(cgck_ctx_t *c, uint32_t max_pkts, size_t max_byte
 	c->bdone = 0;
 	c->bbad = 0;
 	c->bslot[0] = c->bslot[1] = nullptr;
-	std::shared_lock<std::shared_mutex> map_lk(g_map_mu);
+	c->bbusy = 0;
+	std::lock_guard<std::mutex> map_wr(g_map_wr); // no mapping changes while it joins g_srv and launches
 	{
 		std::lock_guard<std::mutex> lk(g_srv_mu);
 		g_srv.push_back(c);
@@ -1238,25 +1303,27 @@ extern "C" int cgck_burst_open(cgck_ctx_t *c, uint32_t max_pkts, size_t max_byte
 	return burst_launch(c, 0);
 }
 
-#if CGCK_LAB
-// Lab (tests/test_gpu_burst_lab.py).  cgck_lab_burst_poke: restart ctx's
-// server as if `seq` were the last request served (a few seqs before the
-// 32-bit wrap).  cgck_lab_burst_stale: with the server running and nothing
-// posted, set the done words of workgroups >= from half the seq space ahead,
-// as a word untouched for 2^31 requests would compare; the next request must
-// refresh them (a workgroup outside a request's slices stores the seq it
-// steps over), or a wider request after it would be reported served before
-// those workgroups wrote anything.
-extern "C" int cgck_lab_burst_poke(cgck_ctx_t *c, uint32_t seq)
+// Test hooks in the product library (include/cgck.h, tests/test_gpu_burst_seq.py:
+// the driver's -m gpu gate runs the 32-bit seq-wrap test against libcgck.so).
+// cgck_test_burst_seq: restart ctx's server as if `seq` were the last request
+// served (a few seqs before the wrap).  cgck_test_burst_stale: with the
+// server running and nothing posted, set the done words of workgroups >= from
+// half the seq space ahead, as a word untouched for 2^31 requests would
+// compare; the next request must refresh them (a workgroup outside a
+// request's slices stores the seq it steps over), or a wider request after it
+// would be reported served before those workgroups wrote anything.
+extern "C" int cgck_test_burst_seq(cgck_ctx_t *c, uint32_t seq)
 {
 	if (!c || !c->bbox || c->bslot[0] || c->bslot[1])
-		return -EINVAL;
-	std::shared_lock<std::shared_mutex> map_lk(g_map_mu);
+		return set_err(-EINVAL, "cgck_test_burst_seq: no open server, or a request posted");
+	if (seq == 0)
+		return set_err(-EINVAL, "cgck_test_burst_seq: seq 0 is never posted");
+	MapGuard map_g(c);
 	__atomic_store_n(&c->bbox->stop, 1u, __ATOMIC_RELEASE);
 	const hipError_t e = hipStreamSynchronize(c->bstream);
 	__atomic_store_n(&c->bbox->stop, 0u, __ATOMIC_RELEASE);
 	if (e != hipSuccess)
-		return -EIO;
+		return set_err(-EIO, "cgck_test_burst_seq: drain: %s", hipGetErrorString(e));
 	for (uint32_t j = 0; j < kBurstMaxWG; j++)
 		__atomic_store_n(&c->bbox->done[j], seq, __ATOMIC_RELEASE);
 	c->bbox->req[0] = c->bbox->req[1] = 0;
@@ -1265,15 +1332,16 @@ extern "C" int cgck_lab_burst_poke(cgck_ctx_t *c, uint32_t seq)
 	return burst_launch(c, seq);
 }
 
-extern "C" int cgck_lab_burst_stale(cgck_ctx_t *c, uint32_t from)
+extern "C" int cgck_test_burst_stale(cgck_ctx_t *c, uint32_t from)
 {
 	if (!c || !c->bbox || c->bslot[0] || c->bslot[1])
-		return -EINVAL;
+		return set_err(-EINVAL, "cgck_test_burst_stale: no open server, or a request posted");
 	for (uint32_t j = from; j < kBurstMaxWG; j++)
 		__atomic_store_n(&c->bbox->done[j], c->bseq + 0x7ffffff0u, __ATOMIC_RELEASE);
 	return 0;
 }
 
+#if CGCK_LAB
 // Lab: what one host load of a BurstBox word costs while the server polls
 // (ns, mean over reps, each load after ~2 us of spin): out[0] the mailbox
 // line (stop, which the leader polls with req), out[1] refused[] (the same
@@ -1332,7 +1400,7 @@ extern "C" int cgck_burst_close(cgck_ctx_t *c)
 	for (BurstPending *p : {c->bslot[0], c->bslot[1]})
 		if (p)
 			(void)burst_collect(c, p);
-	std::shared_lock<std::shared_mutex> map_lk(g_map_mu);
+	std::lock_guard<std::mutex> map_wr(g_map_wr); // leaves g_srv with no mapping change under way
 	{
 		std::lock_guard<std::mutex> lk(g_srv_mu);
 		for (size_t i = 0; i < g_srv.size(); i++)

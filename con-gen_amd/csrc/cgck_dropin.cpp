@@ -138,6 +138,7 @@ struct PostReq {
 	std::vector<uint32_t> o, m; // values, meta words (RX)
 	BurstPending pend{};
 	unsigned items = 0; // posted items it carries, not yet consumed
+	bool used = false;  // slot taken (from its send until done with no item left)
 	bool done = false;  // o / m hold its values (or rc its failure)
 	int rc = 0;
 	char msg[192] = {0};
@@ -208,8 +209,12 @@ static inline double lab_ns() { return (double)__builtin_ia32_rdtsc(); } // TSC 
 
 struct Poster {
 	PostQueue q[2];
-	PostReq rq[2 * kPostQ]; // each carries >= 1 item: never more live than items
-	unsigned rhead = 0, rcount = 0;
+	// Each live request carries >= 1 unconsumed item, so at most 2 * kPostQ
+	// are live at once; a request frees when done with no item left, in any
+	// order (one that still holds an old unconsumed fill must not pin the slots
+	// of later requests), and send takes the next free slot after the last.
+	PostReq rq[2 * kPostQ];
+	unsigned rnext = 0, rlive = 0;
 	int inflight[2] = {-1, -1}; // the request carrying each kind's sent items (one, when fused)
 
 	bool done(const PostItem &x) const { return x.own || (x.req >= 0 && rq[x.req].done); }
@@ -217,6 +222,8 @@ struct Poster {
 	const char *msg_of(const PostItem &x) const { return x.own ? "" : rq[x.req].msg; }
 	const uint32_t *values(const PostItem &x) const { return x.own ? x.vals.data() : rq[x.req].o.data() + x.off; }
 	const uint32_t *metas(const PostItem &x) const { return x.own ? nullptr : rq[x.req].m.data() + x.off; }
+	int take_slot();
+	void release_if_free(int ri);
 	void send(cgck_ctx *c);
 	void collect(cgck_ctx *c, int ri);
 	void pump(cgck_ctx *c, int kind, bool wait);
@@ -236,8 +243,12 @@ struct TxFill {
 	uint8_t *lo = nullptr;
 };
 
+// cgck_window_stats_n's counters (the first four are cgck_window_stats')
+constexpr int kStats = 5;
+
 struct ThreadState {
 	cgck_ctx *ctx = nullptr;
+	int bind_dev = -1; // cgck_thread_bind's device (-1: $CGCK_DEVICE, default 0)
 	// TX window
 	bool tx_open = false;
 	bool tx_icmp = false; // an ICMP message was queued (icmp_send, ip_icmp.c:68-80)
@@ -284,10 +295,20 @@ struct ThreadState {
 	std::vector<std::pair<uintptr_t, uintptr_t>> rx_iv;
 	bool rx_span_built = false;
 	uintptr_t rx_lo = 0, rx_hi = 0;
+	// the last closed RX window's frames (descriptors swapped out of the
+	// burst at cgck_rx_end, no copy): a TX-window call queued on one of their
+	// headers is counted in stats[4] (the stack verifying a received frame
+	// outside an RX window, include/cgck.h); its header addresses are sorted
+	// on the first queued call inside the burst's span
+	std::vector<cgck_desc_t> last_d;
+	const uint8_t *last_base = nullptr;
+	bool last_span = false, last_sorted = false;
+	uintptr_t last_lo = 0, last_hi = 0;
+	std::vector<uintptr_t> last_hdr;
 	RxBurst rxs;      // cgck_rx_begin's burst
 	Poster post;      // posted bursts (cgck_rx_post) and fills (cgck_tx_post)
 	uint64_t rx_served0 = 0; // stats[0] at rx_begin
-	uint64_t stats[4] = {0, 0, 0, 0};
+	uint64_t stats[kStats] = {0, 0, 0, 0, 0};
 	// the registered range of the last TX-window hit, valid while g_reg_gen
 	// holds reg_gen (the window's per-call check without a call out)
 	RegRange reg_last{nullptr, nullptr, nullptr};
@@ -301,13 +322,16 @@ struct ThreadState {
 // cgck_thread_release, which keeps only the counters.
 __attribute__((tls_model("initial-exec"))) thread_local ThreadState *t_st = nullptr;
 // the window counters of a released state (cgck_thread_release frees the state)
-__attribute__((tls_model("initial-exec"))) thread_local uint64_t t_stats_kept[4] = {0, 0, 0, 0};
+__attribute__((tls_model("initial-exec"))) thread_local uint64_t t_stats_kept[kStats] = {0, 0, 0, 0, 0};
+// and its cgck_thread_bind device
+__attribute__((tls_model("initial-exec"))) thread_local int t_bind_kept = -1;
 
 ThreadState &tstate()
 {
 	if (__builtin_expect(!t_st, 0)) {
 		t_st = new ThreadState;
 		memcpy(t_st->stats, t_stats_kept, sizeof(t_stats_kept));
+		t_st->bind_dev = t_bind_kept;
 	}
 	return *t_st;
 }
@@ -457,6 +481,44 @@ __attribute__((noinline)) bool rx_owns(ThreadState &t, const uint8_t *p)
 	const uintptr_t a = (uintptr_t)p;
 	auto it = std::upper_bound(t.rx_iv.begin(), t.rx_iv.end(), std::make_pair(a, UINTPTR_MAX));
 	return it != t.rx_iv.begin() && (it - 1)->second > a;
+}
+
+// A TX-window call queued on the header of a frame of the last closed RX
+// burst (stats[4]): a received frame verified outside an RX window looks like
+// a transmit call and is queued, so the stack got 0 for it (include/cgck.h).
+// A transport that reuses a received frame for a reply in the same iteration
+// counts here too; the counter names the frames to look at, it drops nothing.
+__attribute__((noinline)) void tx_note_last_rx_slow(ThreadState &t, const uint8_t *ip)
+{
+	const size_t n = t.last_d.size();
+	if (!t.last_span) {
+		uintptr_t lo = UINTPTR_MAX, hi = 0;
+		for (size_t i = 0; i < n; i++) {
+			const uintptr_t a = (uintptr_t)(t.last_base + t.last_d[i].frame_off + t.last_d[i].l3_off);
+			lo = a < lo ? a : lo;
+			hi = a + 1 > hi ? a + 1 : hi;
+		}
+		t.last_lo = lo;
+		t.last_hi = hi;
+		t.last_span = true;
+	}
+	const uintptr_t p = (uintptr_t)ip;
+	if (p < t.last_lo || p >= t.last_hi)
+		return;
+	if (!t.last_sorted) {
+		t.last_hdr.resize(n);
+		for (size_t i = 0; i < n; i++)
+			t.last_hdr[i] = (uintptr_t)(t.last_base + t.last_d[i].frame_off + t.last_d[i].l3_off);
+		std::sort(t.last_hdr.begin(), t.last_hdr.end());
+		t.last_sorted = true;
+	}
+	t.stats[4] += std::binary_search(t.last_hdr.begin(), t.last_hdr.end(), p);
+}
+
+inline void tx_note_last_rx(ThreadState &t, const uint8_t *ip)
+{
+	if (__builtin_expect(!t.last_d.empty(), 0))
+		tx_note_last_rx_slow(t, ip);
 }
 
 // Is [p, p + bytes) registered (the TX window queues only ring memory)?  The
@@ -613,7 +675,7 @@ cgck_ctx *cgck::thread_ctx()
 	ThreadState &t = tstate();
 	if (!t.ctx) {
 		const char *e = getenv("CGCK_DEVICE");
-		const int dev = e ? atoi(e) : 0;
+		const int dev = t.bind_dev >= 0 ? t.bind_dev : e ? atoi(e) : 0;
 		cgck_ctx *c = nullptr;
 		if (cgck_ctx_create(dev, &c) != 0)
 			return nullptr;
@@ -642,6 +704,34 @@ extern "C" void cgck_set_error_handler(cgck_error_fn fn, void *arg)
 
 extern "C" cgck_ctx_t *cgck_thread_ctx(void) { return thread_ctx(); }
 
+// The device of this thread's drop-in context, chosen before its first use
+// (con-gen's thread_init: the worker's RSS queue id modulo the devices).
+extern "C" int cgck_thread_bind(int device)
+{
+	const int nd = cgck_device_count();
+	if (nd < 0)
+		return nd;
+	if (device < 0 || device >= nd)
+		return set_err(-EINVAL, "cgck_thread_bind: device %d of %d", device, nd);
+	ThreadState &t = tstate();
+	if (t.ctx && t.ctx->device != device)
+		return set_err(-EBUSY, "cgck_thread_bind: this thread's context is already on device %d "
+				       "(cgck_thread_release first)", t.ctx->device);
+	t.bind_dev = device;
+	return 0;
+}
+
+extern "C" int cgck_thread_device(void)
+{
+	const ThreadState *t = t_st;
+	if (t && t->ctx)
+		return t->ctx->device;
+	if (t && t->bind_dev >= 0)
+		return t->bind_dev;
+	const char *e = getenv("CGCK_DEVICE");
+	return e ? atoi(e) : 0;
+}
+
 extern "C" int cgck_thread_release(void)
 {
 	ThreadState *t = t_st;
@@ -653,6 +743,7 @@ extern "C" int cgck_thread_release(void)
 	// TLS): the state with its window queues, maps and burst-sized buffers is
 	// freed, so a pool that retires threads keeps nothing per thread.
 	memcpy(t_stats_kept, t->stats, sizeof(t_stats_kept));
+	t_bind_kept = t->bind_dev;
 	delete t;
 	t_st = nullptr;
 	return 0;
@@ -662,8 +753,17 @@ extern "C" int cgck_window_stats(uint64_t stats[4])
 {
 	if (!stats)
 		return set_err(-EINVAL, "cgck_window_stats: NULL");
-	memcpy(stats, t_st ? t_st->stats : t_stats_kept, sizeof(t_stats_kept));
+	memcpy(stats, t_st ? t_st->stats : t_stats_kept, 4 * sizeof(uint64_t));
 	return 0;
+}
+
+extern "C" int cgck_window_stats_n(uint64_t *stats, int n)
+{
+	if (!stats || n < 0)
+		return set_err(-EINVAL, "cgck_window_stats_n: NULL or negative count");
+	const int k = n < kStats ? n : kStats;
+	memcpy(stats, t_st ? t_st->stats : t_stats_kept, (size_t)k * sizeof(uint64_t));
+	return kStats;
 }
 
 // --------------------------------------------------------------------------
@@ -704,6 +804,7 @@ extern "C" uint16_t in_cksum(void *data, int len)
 		if (len >= 20 && (b[0] >> 4) == 4 && len == (b[0] & 15) * 4) {
 			// ip_cksum(ip) in ip_output (ip_output.c:62)
 			if (tx_registered(t, b, (size_t)len)) {
+				tx_note_last_rx(t, b);
 				tx_queue(t, (uint8_t *)data, (uint32_t)len, (uint16_t)len, -1);
 				t.stats[2]++;
 				return 0;
@@ -718,6 +819,7 @@ extern "C" uint16_t in_cksum(void *data, int len)
 			const uint8_t *ip = b - 20;
 			if (tx_registered(t, ip, 20 + (size_t)len)) {
 				if (ip[0] == 0x45 && ip[9] == 1) {
+					tx_note_last_rx(t, ip);
 					tx_queue(t, const_cast<uint8_t *>(ip), 20 + (uint32_t)len, 20, 2);
 					t.tx_icmp = true;
 					t.stats[2]++;
@@ -764,6 +866,7 @@ extern "C" uint16_t udp_cksum(struct ip *ipp, int len)
 		const int fo = ip[9] == 6 ? 16 : 6;
 		if ((uint32_t)len >= (uint32_t)fo + 2) {
 			if (tx_registered(t, ip, ip_len)) {
+				tx_note_last_rx(t, ip);
 				tx_queue(t, (uint8_t *)ip, ip_len, (uint16_t)hl, (int16_t)fo);
 				t.stats[2]++;
 				return 0;
@@ -821,6 +924,31 @@ static Group gather(PostQueue &q, uint64_t cap_n, size_t cap_b)
 	return g;
 }
 
+// A free request slot.  Live requests never exceed live items (<= 2 * kPostQ),
+// so one is always free when an item waits to be sent.
+int Poster::take_slot()
+{
+	for (unsigned k = 0; k < 2 * kPostQ; k++) {
+		const unsigned ri = (rnext + k) % (2 * kPostQ);
+		if (!rq[ri].used) {
+			rq[ri].used = true;
+			rnext = (ri + 1) % (2 * kPostQ);
+			rlive++;
+			return (int)ri;
+		}
+	}
+	return -1;
+}
+
+void Poster::release_if_free(int ri)
+{
+	PostReq &r = rq[ri];
+	if (r.used && r.done && r.items == 0) {
+		r.used = false;
+		rlive--;
+	}
+}
+
 // Send what each kind with nothing in flight has waiting: both kinds as one
 // two-part request when they share the range (the receive frames first, so
 // their meta words come back too), else one request each.
@@ -840,8 +968,9 @@ void Poster::send(cgck_ctx *c)
 		if (!g[k].f || (fuse && k == kTx))
 			continue;
 		const int parts = fuse ? 2 : 1;
-		const int ri = (int)((rhead + rcount) % (2 * kPostQ));
-		rcount++;
+		const int ri = take_slot();
+		if (ri < 0) // cannot happen (see take_slot); leave the items unsent
+			die("cgck posted windows: no free request slot");
 		PostReq &r = rq[ri];
 		r.d.clear();
 		r.items = 0;
@@ -940,16 +1069,15 @@ void Poster::pop(int kind)
 {
 	PostQueue &qq = q[kind];
 	PostItem &x = qq.oldest();
-	if (x.req >= 0)
-		rq[x.req].items--;
+	const int ri = x.req;
+	if (ri >= 0)
+		rq[ri].items--;
 	qq.head = (qq.head + 1) % kPostQ;
 	qq.count--;
 	if (qq.sent)
 		qq.sent--;
-	while (rcount && rq[rhead].done && rq[rhead].items == 0) {
-		rhead = (rhead + 1) % (2 * kPostQ);
-		rcount--;
-	}
+	if (ri >= 0)
+		release_if_free(ri);
 }
 
 // Open the window over a computed burst; returns the frames it answers for.
@@ -1107,8 +1235,15 @@ extern "C" int cgck_rx_end(void)
 	if (!t.rx_open)
 		return set_err(-EINVAL, "cgck_rx_end: no open RX window on this thread");
 	t.rx_open = false;
-	t.rx_n = 0;
 	t.rx_map = false;
+	// keep the closed burst's frames for stats[4] (a swap, no copy)
+	if (t.rx_posted)
+		std::swap(t.last_d, t.post.q[kRx].oldest().d);
+	else
+		std::swap(t.last_d, t.rxs.d);
+	t.last_base = t.rx_base;
+	t.last_span = t.last_sorted = false;
+	t.rx_n = 0;
 	if (t.rx_posted) {
 		t.rx_posted = false;
 		t.post.pop(kRx);
@@ -1356,18 +1491,19 @@ extern "C" int cgck_tx_post(void)
 	if (!t.tx_open)
 		return set_err(-EINVAL, "cgck_tx_post: no open window on this thread");
 	PostQueue &q = t.post.q[kTx];
+	int old_rc = 0;
+	char old_msg[200] = {0};
 	if (q.count == kPostQ) {
 		// The queue is full: the oldest fill completes first (its fields
 		// are written now, before the kick that was to wait for them —
 		// final values either way), so no queued field is dropped.
-		const int rc = cgck_tx_complete();
-		if (rc < 0) {
-			t.tx_open = false;
-			t.txq.clear();
-			char msg[256];
-			snprintf(msg, sizeof(msg), "%s", err_text());
-			return set_err(rc, "cgck_tx_post: completing the oldest fill: %s", msg);
-		}
+		// A failed completion still frees the oldest slot: this window is
+		// posted regardless (its calls were answered 0, so dropping it would
+		// send zero checksums), and the oldest fill's error is returned
+		// after the post (include/cgck.h).
+		old_rc = cgck_tx_complete();
+		if (old_rc < 0)
+			snprintf(old_msg, sizeof(old_msg), "%s", err_text());
 	}
 	cgck_ctx *c = thread_ctx();
 	if (!c)
@@ -1384,6 +1520,9 @@ extern "C" int cgck_tx_post(void)
 		return rc;
 	}
 	t.post.pump(c, kTx, false);
+	if (old_rc < 0)
+		return set_err(old_rc, "cgck_tx_post: this window was posted, but completing the oldest fill failed "
+				       "(its fields are not written): %s", old_msg);
 	return f.n;
 }
 

@@ -75,6 +75,7 @@ struct cgck_ctx {
 	uint32_t bseq;              // the last request posted
 	uint32_t bdone;             // the last request known complete (a relaunch serves the ones after it)
 	cgck::BurstPending *bslot[2]; // a posted request not yet collected, per slot
+	uint32_t bbusy;             // the owner thread is inside a request (MapGuard, cgck_api.cpp)
 	hipStream_t bstream; // the server's own stream (it stays resident)
 };
 

@@ -173,6 +173,18 @@ int cgck_host_device_ptr(const void *ptr, size_t bytes, void **dev);
 cgck_ctx_t *cgck_thread_ctx(void);
 int cgck_thread_release(void);
 
+/* Per-thread device binding (one host thread per device).  A
+ * worker calls cgck_thread_bind(queue_id % cgck_device_count()) in its
+ * thread_init (con-gen.c:1062-1100 starts one worker per RSS queue, up to
+ * N_THREADS_MAX = 32, subr.h:58) before its first checksum call; its
+ * drop-in context, windows and burst server then live on that device.  The
+ * binding outlives cgck_thread_release.  -EINVAL: no such device; -EBUSY:
+ * the thread's context already exists on another device (release it first).
+ * cgck_thread_device returns the device the thread's context is (or will be)
+ * on. */
+int cgck_thread_bind(int device);
+int cgck_thread_device(void);
+
 /* The drop-in symbols have no error channel (their prototypes are the
  * reference's).  When one cannot produce a result (no device, a launch or
  * synchronisation failure) it calls the handler set here with what failed
@@ -237,7 +249,7 @@ int cgck_rx_begin_posted(void);
  * waits for its values if the GPU is not done), runs the stack over it,
  * closes it and releases its slots.  A burst therefore
  * never waits longer than one loop iteration after its post.
- * cgck_rx_pending returns the bursts posted and not yet opened (0..2);
+ * cgck_rx_pending returns the bursts posted and not yet opened (0..64);
  * cgck_rx_ready, without waiting, 1 when the oldest one's values are in
  * (opening it will not wait), 0 while the GPU still computes it, -ENOENT
  * when nothing is posted.  A transport may also drain a ready burst early,
@@ -265,7 +277,10 @@ int cgck_rx_ready(void);
  * A call about a frame of the open RX window is never queued (it is the
  * stack verifying what it received).  A received frame must therefore be
  * processed inside an RX window whenever the TX window is open: its verify
- * calls outside one would look like a transmit call and be queued. */
+ * calls outside one would look like a transmit call and be queued.
+ * cgck_window_stats_n's counter [4] counts queued calls on a header of the
+ * last closed RX window's frames, so an integration that misses that rule
+ * shows up there. */
 int cgck_tx_begin(void);
 int cgck_tx_flush(void);
 
@@ -279,7 +294,10 @@ int cgck_tx_flush(void);
  * it before it hands those slots to the NIC — at the next loop's kick
  * (con-gen.c:493), so the GPU computes burst k while the stack builds burst
  * k + 1.  Up to 64 fills may be posted and not yet completed: one more
- * cgck_tx_post completes the oldest first (its fields are written then). */
+ * cgck_tx_post completes the oldest first (its fields are written then); if
+ * that completion fails, the new window is still posted and the oldest
+ * fill's error is returned (its fields stay unwritten: the transport drops
+ * or recomputes those packets). */
 int cgck_tx_post(void);
 int cgck_tx_complete(void);
 
@@ -298,6 +316,11 @@ int cgck_tx_ready(void);
  * computed synchronously (no match), [2] calls queued by a TX window, [3]
  * calls inside a TX window computed synchronously (memory not registered). */
 int cgck_window_stats(uint64_t stats[4]);
+/* The same counters and more: writes min(n, 5) of them and returns how many
+ * the library keeps (5).  [4]: TX-window calls queued on the IPv4 header of a
+ * frame of the last closed RX window (a received frame verified outside an RX
+ * window, see cgck_tx_begin; or a received frame reused for a reply). */
+int cgck_window_stats_n(uint64_t *stats, int n);
 
 /* Burst server (latency).  Keeps up to 32 workgroups
  * (one per 64 packets of max_pkts) resident on `ctx` (NULL: this thread's
@@ -427,6 +450,15 @@ int cgck_event_elapsed_ms(cgck_event_t *start, cgck_event_t *stop, float *ms);
  * memory, 16-byte aligned) with minimal arithmetic — the practical HBM-read
  * ceiling the checksum kernels are compared with.  `sink` is a device u32. */
 int cgck_probe_read(cgck_ctx_t *ctx, const void *src, uint64_t bytes, uint32_t *sink, void *stream);
+
+/* Test hooks (tests/test_gpu_burst_seq.py; not for production callers).
+ * cgck_test_burst_seq restarts ctx's open, idle burst server as if `seq` were
+ * the last request served (the 32-bit seq wrap test); cgck_test_burst_stale
+ * sets the done words of workgroups >= from half the seq space ahead (a word
+ * untouched for 2^31 requests), which the next request must refresh.
+ * -EINVAL: no server open, or a posted request not yet collected. */
+int cgck_test_burst_seq(cgck_ctx_t *ctx, uint32_t seq);
+int cgck_test_burst_stale(cgck_ctx_t *ctx, uint32_t from);
 
 #ifdef __cplusplus
 }

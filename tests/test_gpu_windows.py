@@ -752,6 +752,87 @@ def test_posted_burst_survives_unregister(port):
         cgck.burst_close()
 
 
+def test_posted_burst_not_reserved_after_mapping_change(port):
+    """A burst posted over a ring; another range registered (the mapping
+    change serves the posted request and stops the server); the ring's
+    bytes then change; a synchronous drop-in call on the same thread posts
+    the next seq and relaunches the server.  The relaunch must start after
+    the request the mapping change served: served again, it would read the
+    changed bytes into the burst's values."""
+    R = referee(port)
+    L = cgck.load()
+    cgck.burst_open(max_pkts=1024, max_bytes=4 << 20)
+    other = None
+    try:
+        rng = np.random.default_rng(5310)
+        buf, desc = rxcorpus.ring(rxcorpus.corpus(rng, R, 120, clean=True))
+        raw, ring, size = rxcorpus.registered_copy(buf)
+        assert L.cgck_host_register(ring.ctypes.data, size) == 0
+        got = ring[:len(buf)]
+        assert cgck.rx_post(got, desc) == 120
+        other = rxcorpus.registered_copy(np.zeros(8192, np.uint8))
+        assert L.cgck_host_register(other[1].ctypes.data, other[2]) == 0
+        saved = got.copy()
+        got[:] = rng.integers(0, 256, len(got), dtype=np.uint8)    # the ring reused meanwhile
+        hdr = np.array([0x45, 0, 0, 20, 0, 0, 0x40, 0, 64, 6, 0, 0, 10, 0, 0, 1, 10, 0, 0, 2], np.uint8)
+        assert cgck.ip_cksum(hdr) == port.in_cksum(hdr, 20)           # sync call: next seq, relaunch
+        got[:] = saved
+        served, d, calls = replay_posted(port, R, buf, desc, got, FLAGS[7])
+        assert served == d[0] and served + d[1] == calls
+        L.cgck_host_unregister(ring.ctypes.data)
+    finally:
+        cgck.burst_close()
+        if other is not None:
+            L.cgck_host_unregister(other[1].ctypes.data)
+
+
+@pytest.mark.parametrize("server", [False, True])
+def test_pending_fill_across_many_rx_cycles(port, server):
+    """One TX fill posted and left pending while 140 receive bursts are
+    posted, opened and closed: the requests behind the fill's are freed out
+    of order, so none reuses the fill's request slot (128 slots
+    freed only from the oldest overflowed into the fill's at the 128th), and
+    the completion writes the fill's own values."""
+    R = referee(port)
+    L = cgck.load()
+    raw, ring, size = rxcorpus.registered_copy(np.zeros(16 * 2048, np.uint8))
+    slots = ring[:16 * 2048].reshape(16, 2048)
+    assert L.cgck_host_register(ring.ctypes.data, size) == 0
+    if server:
+        cgck.burst_open(max_pkts=1024, max_bytes=4 << 20)
+    rng = np.random.default_rng(5320 + server)
+    try:
+        want = []
+        cgck.tx_begin()
+        for i in range(4):
+            ln = int(rng.integers(40, 1501))
+            pkt = tcp_pkt(rng, ln)
+            slots[i, 14:14 + ln] = pkt
+            want.append((i, ln, expected(port, pkt, 16)))
+            tx_calls(slots[i], ln, 16)
+        assert cgck.tx_post() == 8
+        buf, desc = rxcorpus.ring(rxcorpus.corpus(rng, R, 6, clean=True))
+        raw2, ring2, size2 = rxcorpus.registered_copy(buf)
+        assert L.cgck_host_register(ring2.ctypes.data, size2) == 0
+        got = ring2[:len(buf)]
+        try:
+            for it in range(140):
+                got[:] = buf
+                assert cgck.rx_post(got, desc) == 6
+                served, d, calls = replay_posted(port, R, buf, desc, got, FLAGS[(it * 5) % len(FLAGS)])
+                assert served == d[0], it
+            assert cgck.tx_pending() == 1
+        finally:
+            L.cgck_host_unregister(ring2.ctypes.data)
+        assert cgck.tx_complete() == 8
+        for i, ln, r in want:
+            assert np.array_equal(slots[i, 14:14 + ln], r), i
+    finally:
+        if server:
+            cgck.burst_close()
+        L.cgck_host_unregister(ring.ctypes.data)
+
+
 @pytest.mark.parametrize("server", [False, True])
 def test_tx_post_beyond_queue_completes_oldest(port, server):
     """64 fills posted and a 65th window closed: cgck_tx_post completes the
@@ -1192,3 +1273,78 @@ def test_coalesced_threads_with_mapping_changes(port):
         x.join()
     assert not errs, errs
     assert cycles > 0
+
+
+def test_verify_outside_rx_window_counted(port):
+    """include/cgck.h: with the TX window open, a received frame verified
+    outside an RX window looks like a transmit call and is queued (the stack
+    gets 0).  cgck_window_stats_n's [4] counts such calls on the headers of
+    the last closed RX window's frames, and nothing else."""
+    R = referee(port)
+    L = cgck.load()
+    rng = np.random.default_rng(5330)
+    buf, desc = rxcorpus.ring(rxcorpus.corpus(rng, R, 24, clean=True))
+    raw, ring, size = rxcorpus.registered_copy(np.concatenate([buf, np.zeros(4 * 2048, np.uint8)]))
+    assert L.cgck_host_register(ring.ctypes.data, size) == 0
+    got = ring[:len(buf)]
+    tx = ring[len(buf):len(buf) + 4 * 2048].reshape(4, 2048)
+    try:
+        cgck.tx_begin()
+        s0 = cgck.window_stats_n()
+        assert len(s0) == 5
+        cgck.rx_begin(got, desc)
+        try:
+            port.replay_rx(*cgck.fn_pointers(), got, desc.view(np.uint8), len(desc), 0, 2, 2)
+        finally:
+            cgck.rx_end()
+        s1 = cgck.window_stats_n()
+        assert s1[4] == s0[4]                          # inside the window: answered, not counted
+        for k in range(3):                             # the missed path: verified after rx_end
+            off = int(desc[k]["frame_off"]) + 14
+            got[off + 10:off + 12] = 0
+            assert cgck.ip_cksum(got, off) == 0        # queued (the hazard itself)
+        for i in range(2):                             # a genuine transmit slot: not counted
+            pkt = tcp_pkt(rng, 200)
+            tx[i, 14:214] = pkt
+            tx_calls(tx[i], 200, 16)
+        s2 = cgck.window_stats_n()
+        assert s2[4] - s1[4] == 3 and s2[2] - s1[2] == 3 + 4, (s1, s2)
+        cgck.tx_flush()
+    finally:
+        L.cgck_host_unregister(ring.ctypes.data)
+
+
+def test_thread_bind(port):
+    """cgck_thread_bind picks the device of a worker's drop-in context before
+    its first use (con-gen.c:1062-1100: workers bound by queue
+    id modulo the devices); a binding to another device after the context
+    exists is refused, and survives cgck_thread_release."""
+    nd = cgck.device_count()
+    errs = []
+
+    def worker(q):
+        try:
+            dev = q % nd
+            assert cgck.thread_bind(dev) == 0
+            assert cgck.thread_device() == dev
+            rng = np.random.default_rng(5340 + q)
+            for _ in range(20):
+                pkt = tcp_pkt(rng, int(rng.integers(40, 1501)))
+                pkt[10:12] = 0
+                assert cgck.ip_cksum(pkt) == port.in_cksum(pkt, 0, 20)
+            if nd > 1:
+                with pytest.raises(cgck.CgckError, match="already on device"):
+                    cgck.thread_bind((dev + 1) % nd)
+            with pytest.raises(cgck.CgckError, match="cgck_thread_bind: device"):
+                cgck.thread_bind(nd)
+            cgck.thread_release()
+            assert cgck.thread_device() == dev
+        except Exception as e:          # noqa: BLE001 - reported below
+            errs.append((q, repr(e)))
+
+    ths = [threading.Thread(target=worker, args=(q,)) for q in range(6)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    assert not errs, errs

@@ -41,6 +41,8 @@
  */
 #define _GNU_SOURCE
 #include <dlfcn.h>
+#include <pthread.h>
+#include <sched.h>
 #include <libgen.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -151,6 +153,9 @@ struct cell {
 	int it, itl, bad_rx, bad_tx_checked, bad_tx;
 	double total; /* worker seconds over the recorded iterations */
 	long bursts;  /* bursts they processed */
+	double max_iter; /* the longest iteration (all of it, spin included), warm-up too */
+	int max_at;      /* at which iteration */
+	int iters_all;   /* iterations run, warm-up included */
 };
 
 static in_fn ref_in;
@@ -218,6 +223,461 @@ static int fill_done(struct fills *f, int mix, const uint8_t *tx0, struct cell *
 	return 0;
 }
 
+/* One worker's ring: a pool as a netmap pool holds both rings (two receive
+ * halves, bursts k and k - 1; two transmit halves, fills k and k - 1), the
+ * descriptors of each receive half, and the post timestamps. */
+struct wk {
+	uint8_t *pool, *rxh[2], *txh[2];
+	size_t pool_bytes;
+	cgck_desc_t *descs[2];
+	double *tpost;
+	int len;
+};
+
+static int cell_alloc(struct cell *c)
+{
+	c->worker = malloc(sizeof(double) * MAXIT);
+	c->wait = malloc(sizeof(double) * MAXIT);
+	c->lat = malloc(sizeof(double) * MAXIT);
+	return c->worker && c->wait && c->lat ? 0 : -1;
+}
+
+/* A worker's pool: MAXB frames of `len` bytes in each receive half, every
+ * 64th corrupted, checksummed by the sender with the reference functions. */
+static int wk_setup(struct wk *W, int len)
+{
+	const size_t half = (size_t)MAXB * SLOT;
+	W->len = len;
+	W->pool_bytes = 4 * half;
+	W->pool = mmap(NULL, W->pool_bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+	W->tpost = malloc(sizeof(double) * (MAXIT + 64));
+	W->descs[0] = malloc(sizeof(cgck_desc_t) * MAXB);
+	W->descs[1] = malloc(sizeof(cgck_desc_t) * MAXB);
+	if (W->pool == MAP_FAILED || !W->tpost || !W->descs[0] || !W->descs[1])
+		return -1;
+	W->rxh[0] = W->pool;
+	W->rxh[1] = W->pool + half;
+	W->txh[0] = W->pool + 2 * half;
+	W->txh[1] = W->pool + 3 * half;
+	uint64_t s = 0x9E3779B97F4A7C15ull;
+	for (int i = 0; i < MAXB; i++) {
+		uint8_t *ip = W->rxh[0] + (size_t)i * SLOT + L3;
+		make_packet(ip, len, &s);
+		uint16_t v = ref_udp((struct ip *)ip, len - 20); /* the sender's fill (reference functions) */
+		memcpy(ip + 36, &v, 2);
+		v = ref_in(ip, 20);
+		memcpy(ip + 10, &v, 2);
+		if (i % 64 == 0) /* every 64th frame corrupted */
+			ip[len - 1] ^= 0x5A;
+		/* every post names the whole pool, as a transport's does (one base,
+		 * the frames by offset), so bursts posted back to back can share a
+		 * request */
+		W->descs[0][i].frame_off = (uint64_t)i * SLOT;
+		W->descs[0][i].l3_off = L3;
+		W->descs[0][i].ip_len = (uint16_t)len;
+		W->descs[1][i] = W->descs[0][i];
+		W->descs[1][i].frame_off += half;
+	}
+	memcpy(W->rxh[1], W->rxh[0], half);
+	return 0;
+}
+
+/* One (form, mix, burst, stack budget) cell of con-gen's loop on this thread
+ * for `budget` seconds; 0, or -1 on a library error (cgck_last_error). */
+static int run_cell(struct wk *W, int form, int mix, int R, double ns, double fixed_us, double budget,
+		    struct cell *cp)
+{
+	struct cell c = *cp;
+	uint8_t *const pool = W->pool, *const *rxh = W->rxh, *const *txh = W->txh;
+	const size_t pool_bytes = W->pool_bytes;
+	cgck_desc_t *const *descs = W->descs;
+	double *tpost = W->tpost;
+	const int len = W->len;
+	const double other = (R * ns + fixed_us * 1000) * 1e-9;
+	const int expect = (R + 63) / 64;
+	in_fn lib_in = (in_fn)in_cksum;
+	udp_fn lib_udp = (udp_fn)udp_cksum;
+		c.it = c.itl = c.bad_rx = c.bad_tx = c.bad_tx_checked = 0;
+		c.total = 0;
+		c.bursts = 0;
+		c.max_iter = 0;
+		c.max_at = -1;
+		int k = 0;
+		long copened = 0; /* coalesced form: bursts opened */
+		struct fills cf;
+		memset(&cf, 0, sizeof(cf));
+		const double t0 = now();
+		while (c.it < MAXIT && now() - t0 < budget) {
+			const int rec = k >= 20;
+			g_check = 0;
+			double a = now(), w = 0, lat = 0;
+			int nburst = form == 1 ? k > 0 : 1; /* bursts this iteration processed */
+			int bad = 0;
+			uint8_t *tx = txh[k & 1];
+			if (form == 0) {
+				uint8_t *rx = rxh[k & 1];
+				for (int i = 0; i < R; i++) {
+					uint8_t *ip = rx + (size_t)i * SLOT + L3;
+					bad += verify(ip, len, ref_in, ref_udp);
+					if (mix)
+						reply(tx + (size_t)i * SLOT + L3, ip, ref_in, ref_udp);
+				}
+				lat = now() - a;
+			} else if (form == 1) {
+				double w0 = now();
+				const int done = cgck_tx_complete(); /* fill k - 1 */
+				w += now() - w0;
+				if (done < 0)
+					return -1;
+				if (mix && k > 0 && done == 2 * R) {
+					c.bad_tx += check_replies(txh[(k + 1) & 1], R);
+					c.bad_tx_checked++;
+				}
+				cgck_tx_begin();
+				tpost[k] = now();
+				if (cgck_rx_post(pool, pool_bytes, descs[k & 1], R) != R)
+					return -1;
+				if (k > 0) {
+					uint8_t *rx = rxh[(k + 1) & 1];
+					w0 = now();
+					if (cgck_rx_begin_posted() != R)
+						return -1;
+					w += now() - w0;
+					for (int i = 0; i < R; i++) {
+						uint8_t *ip = rx + (size_t)i * SLOT + L3;
+						bad += verify(ip, len, lib_in, lib_udp);
+						if (mix)
+							reply(tx + (size_t)i * SLOT + L3, ip, lib_in, lib_udp);
+					}
+					if (cgck_rx_end() != 2 * R)
+						return -1;
+					lat = now() - tpost[k - 1];
+				} else {
+					bad = expect;
+				}
+			} else if (form == 3) {
+				/* the kick releases the fills that are back
+				 * (no wait unless 48 are outstanding); burst k
+				 * is posted; every burst whose values are in
+				 * is processed, oldest first (no wait unless
+				 * 48 are outstanding).  Replies go to a rolling
+				 * cursor over both transmit halves; a fill's
+				 * slots are reused only after it completed. */
+				double w0 = now();
+				while (cf.n > 0 && (cgck_tx_ready() == 1 || cf.n >= 48)) {
+					if (fill_done(&cf, mix, txh[0], &c) < 0)
+						return -1;
+				}
+				w += now() - w0;
+				cgck_tx_begin();
+				tpost[k % 64] = now();
+				if (cgck_rx_post(pool, pool_bytes, descs[k & 1], R) != R)
+					return -1;
+				int got = 0;
+				long cur = 0; /* this iteration's reply slots */
+				const long at = cf.cursor % (2 * MAXB);
+				const long gap = mix && at + R > 2 * MAXB ? 2 * MAXB - at : 0;
+				const long room = 2 * MAXB - (at + gap) % (2 * MAXB);
+				for (;;) {
+					const int pend = cgck_rx_pending();
+					const int rdy = pend ? cgck_rx_ready() : 0;
+					if (!pend || (rdy != 1 && pend < 48) || (mix && cur + R > room))
+						break;
+					w0 = now();
+					while (cf.n > 0 && cf.busy + gap + cur + R > 2 * MAXB)
+						if (fill_done(&cf, mix, txh[0], &c) < 0)
+							return -1;
+					if (cgck_rx_begin_posted() != R)
+						return -1;
+					w += now() - w0;
+					uint8_t *rx = rxh[copened & 1];
+					for (int i = 0; i < R; i++) {
+						uint8_t *ip = rx + (size_t)i * SLOT + L3;
+						bad += verify(ip, len, lib_in, lib_udp);
+						if (mix)
+							reply(txh[0] + (size_t)((cf.cursor + gap + cur + i) % (2 * MAXB)) *
+									       SLOT +
+								      L3,
+							      ip, lib_in, lib_udp);
+					}
+					if (mix)
+						cur += R;
+					if (cgck_rx_end() != 2 * R)
+						return -1;
+					lat += now() - tpost[copened % 64];
+					copened++;
+					got++;
+				}
+				bad = got ? (bad == got * expect ? expect : -1) : expect;
+				lat = got ? lat / got : 0;
+				nburst = got;
+				fill_push(&cf, cur ? gap : 0, cur);
+			} else {
+				uint8_t *rx = rxh[k & 1];
+				cgck_tx_begin();
+				double w0 = now();
+				if (cgck_rx_begin(pool, pool_bytes, descs[k & 1], R) != R)
+					return -1;
+				w += now() - w0;
+				for (int i = 0; i < R; i++) {
+					uint8_t *ip = rx + (size_t)i * SLOT + L3;
+					bad += verify(ip, len, lib_in, lib_udp);
+					if (mix)
+						reply(tx + (size_t)i * SLOT + L3, ip, lib_in, lib_udp);
+				}
+				if (cgck_rx_end() != 2 * R)
+					return -1;
+				lat = now() - a;
+			}
+			const double a_spin = now();
+			spin(other);
+			const double spun = now() - a_spin;
+			if (form == 1 || form == 3) {
+				if (cgck_tx_post() < 0)
+					return -1;
+			} else if (form == 2) {
+				const double w0 = now();
+				if (cgck_tx_flush() != (mix ? 2 * R : 0))
+					return -1;
+				w += now() - w0;
+				if (mix) {
+					c.bad_tx += check_replies(tx, R);
+					c.bad_tx_checked++;
+				}
+			}
+			c.bad_rx += bad != expect;
+			if (now() - a > c.max_iter) {
+				c.max_iter = now() - a;
+				c.max_at = k;
+			}
+			if (rec) {
+				c.total += now() - a - spun - g_check;
+				c.bursts += nburst;
+				c.worker[c.it] = now() - a - spun - g_check;
+				c.wait[c.it] = w;
+				c.it++;
+				if (lat > 0) /* (the coalesced form: iterations that opened bursts) */
+					c.lat[c.itl++] = lat;
+			}
+			k++;
+		}
+		if (form == 1 || form == 3) { /* drain: the bursts and fills left */
+			while (cgck_rx_pending() > 0 && cgck_rx_begin_posted() >= 0)
+				cgck_rx_end();
+			while (cgck_tx_pending() > 0)
+				cgck_tx_complete();
+			memset(&cf, 0, sizeof(cf));
+		}
+	c.iters_all = k;
+	*cp = c;
+	return 0;
+}
+
+/* ------------------------------------------------------------------------
+ * N workers (TXLOOP_WORKERS=1,8,16,32): con-gen's normal mode, one worker
+ * thread per RSS queue (con-gen.c:1062-1100, up to N_THREADS_MAX 32,
+ * subr.h:58), each pinned to its own CPU, with its own pool, its own drop-in
+ * context bound to device queue % devices (cgck_thread_bind) and its own
+ * burst server, all running the same cell at once.  Per N and form one JSON
+ * line: the per-thread us per burst (median / p90 / max over the threads),
+ * the threads' p90 iteration, latency, and whether every thread stayed exact.
+ * The reference form runs the same threads without the GPU: its slowdown
+ * with N is the host's own (cores, caches, the CPU quota), the control for
+ * the GPU forms'.
+ *   TXLOOP_MW_BURST (64)  TXLOOP_MW_NS (250)  TXLOOP_MW_MIX (1: with replies)
+ * ---------------------------------------------------------------------- */
+#define MW_MAXT 64
+#define MW_FORMS 3
+
+struct mw {
+	int id, cpu, nforms;
+	int forms[MW_FORMS];
+	int R, mix;
+	double ns, budget;
+	struct wk W;
+	struct cell c;
+	int rc, dev;
+	char err[200];
+	/* per form: us per burst, p50 / p90 iteration, p50 latency, bursts, exact */
+	double per[MW_FORMS], w50[MW_FORMS], w90[MW_FORMS], l50[MW_FORMS];
+	long bursts[MW_FORMS];
+	int exact[MW_FORMS];
+};
+
+static pthread_barrier_t g_bar;
+
+static void mw_fail(struct mw *m, const char *what)
+{
+	if (!m->rc) {
+		m->rc = -1;
+		snprintf(m->err, sizeof(m->err), "%s: %s", what, cgck_last_error());
+	}
+}
+
+static void *mw_thread(void *arg)
+{
+	struct mw *m = arg;
+	cpu_set_t cs;
+	CPU_ZERO(&cs);
+	CPU_SET(m->cpu, &cs);
+	pthread_setaffinity_np(pthread_self(), sizeof(cs), &cs);
+	const int nd = cgck_device_count();
+	if (nd < 1 || cgck_thread_bind(m->id % nd) != 0)
+		mw_fail(m, "cgck_thread_bind");
+	m->dev = cgck_thread_device();
+	if (!m->rc && cgck_host_register(m->W.pool, m->W.pool_bytes) != 0)
+		mw_fail(m, "cgck_host_register");
+	pthread_barrier_wait(&g_bar); /* every ring registered (each registration stops every server) */
+	if (!m->rc && cgck_burst_open(NULL, MAXB, (size_t)MAXB * 1536, 0) != 0)
+		mw_fail(m, "cgck_burst_open");
+	pthread_barrier_wait(&g_bar);
+	for (int f = 0; f < m->nforms; f++) {
+		const int form = m->forms[f];
+		if (!m->rc && form != 0) /* warm the server and the queues, not recorded */
+			if (run_cell(&m->W, form, m->mix, m->R, m->ns, 0, 0.02, &m->c) < 0)
+				mw_fail(m, "warm-up");
+		pthread_barrier_wait(&g_bar); /* every thread runs the same cell at once */
+		if (!m->rc && run_cell(&m->W, form, m->mix, m->R, m->ns, 0, m->budget, &m->c) < 0)
+			mw_fail(m, "cell");
+		struct cell *c = &m->c;
+		m->bursts[f] = c->bursts;
+		m->per[f] = c->bursts ? c->total / c->bursts * 1e6 : -1;
+		m->w50[f] = c->it ? pct(c->worker, c->it, 50) * 1e6 : -1;
+		m->w90[f] = c->it ? pct(c->worker, c->it, 90) * 1e6 : -1;
+		m->l50[f] = c->itl ? pct(c->lat, c->itl, 50) * 1e6 : -1;
+		m->exact[f] = !m->rc && c->bursts > 0 && c->bad_rx == 0 && c->bad_tx == 0;
+		pthread_barrier_wait(&g_bar);
+	}
+	cgck_burst_close(NULL);
+	pthread_barrier_wait(&g_bar); /* every server closed before the mappings change */
+	cgck_host_unregister(m->W.pool);
+	cgck_thread_release();
+	return NULL;
+}
+
+static int cmpd_desc_free(const void *a, const void *b) { return cmpd(a, b); }
+
+/* median / p90 / max / min of the threads' values (v is sorted) */
+static void mw_stats(double *v, int n, double out[4])
+{
+	qsort(v, n, sizeof(double), cmpd_desc_free);
+	out[0] = v[n / 2];
+	out[1] = v[(long)n * 90 / 100 < n ? (long)n * 90 / 100 : n - 1];
+	out[2] = v[n - 1];
+	out[3] = v[0];
+}
+
+static int multi_main(double budget, int len)
+{
+	int counts[8], nc = 0;
+	for (char *e = getenv("TXLOOP_WORKERS"); *e && nc < 8;) {
+		const int v = (int)strtol(e, &e, 10);
+		if (v >= 1 && v <= MW_MAXT)
+			counts[nc++] = v;
+		while (*e == ',')
+			e++;
+	}
+	const int R = getenv("TXLOOP_MW_BURST") ? atoi(getenv("TXLOOP_MW_BURST")) : 64;
+	const double ns = getenv("TXLOOP_MW_NS") ? atof(getenv("TXLOOP_MW_NS")) : 250;
+	const int mix = getenv("TXLOOP_MW_MIX") ? atoi(getenv("TXLOOP_MW_MIX")) : 1;
+	if (R < 1 || R > MAXB / 2)
+		return 2;
+	static const char *fname[4] = {"reference", "pipelined", "sync", "coalesced"};
+	const int forms[MW_FORMS] = {0, 3, 1};
+	cpu_set_t all;
+	int cpus[1024], ncpu = 0;
+	if (sched_getaffinity(0, sizeof(all), &all) == 0)
+		for (int i = 0; i < CPU_SETSIZE && ncpu < 1024; i++)
+			if (CPU_ISSET(i, &all))
+				cpus[ncpu++] = i;
+	if (ncpu == 0)
+		return 1;
+	char quota[64] = "unknown";
+	FILE *fq = fopen("/sys/fs/cgroup/cpu.max", "r");
+	if (fq) {
+		if (fgets(quota, sizeof(quota), fq))
+			quota[strcspn(quota, "\n")] = 0;
+		fclose(fq);
+	}
+	static struct mw M[MW_MAXT];
+	int maxn = 0;
+	for (int i = 0; i < nc; i++)
+		maxn = counts[i] > maxn ? counts[i] : maxn;
+	for (int t = 0; t < maxn; t++) /* pools made once; each run registers them anew */
+		if (wk_setup(&M[t].W, len) != 0 || cell_alloc(&M[t].c) != 0) {
+			fprintf(stderr, "txloop: out of memory\n");
+			return 1;
+		}
+	for (int ci = 0; ci < nc; ci++) {
+		const int N = counts[ci];
+		pthread_t th[MW_MAXT];
+		pthread_barrier_init(&g_bar, NULL, N);
+		for (int t = 0; t < N; t++) {
+			struct mw *m = &M[t];
+			m->id = t;
+			m->cpu = cpus[(ncpu / 2 + t) % ncpu]; /* from the middle of the set, as bench.py pins one */
+			m->nforms = MW_FORMS;
+			memcpy(m->forms, forms, sizeof(forms));
+			m->R = R;
+			m->mix = mix;
+			m->ns = ns;
+			m->budget = budget;
+			m->rc = 0;
+			m->err[0] = 0;
+			pthread_create(&th[t], NULL, mw_thread, m);
+		}
+		for (int t = 0; t < N; t++)
+			pthread_join(th[t], NULL);
+		pthread_barrier_destroy(&g_bar);
+		for (int f = 0; f < MW_FORMS; f++) {
+			double per[MW_MAXT], w90[MW_MAXT], l50[MW_MAXT], sp[4], s90[4], sl[4];
+			int exact = 1, np = 0, nl = 0;
+			long bursts = 0;
+			for (int t = 0; t < N; t++) {
+				exact = exact && M[t].exact[f];
+				bursts += M[t].bursts[f];
+				if (M[t].per[f] >= 0) {
+					per[np] = M[t].per[f];
+					w90[np++] = M[t].w90[f];
+				}
+				if (M[t].l50[f] >= 0)
+					l50[nl++] = M[t].l50[f];
+			}
+			printf("{\"mode\": \"workers\", \"workers\": %d, \"form\": \"%s\", \"mix\": \"%s\", \"pkt_len\": %d, "
+			       "\"burst\": %d, \"stack_ns_per_frame\": %.0f, \"cpus\": %d, \"cpu_max\": \"%s\", \"bursts\": %ld",
+			       N, fname[forms[f]], mix ? "rx+reply" : "rx", len, R, ns, ncpu, quota, bursts);
+			if (np) {
+				mw_stats(per, np, sp);
+				mw_stats(w90, np, s90);
+				printf(", \"us_per_burst\": {\"median\": %.3f, \"p90\": %.3f, \"max\": %.3f, \"min\": %.3f}"
+				       ", \"us_iter_p90\": {\"median\": %.3f, \"max\": %.3f}",
+				       sp[0], sp[1], sp[2], sp[3], s90[0], s90[2]);
+			} else {
+				printf(", \"us_per_burst\": null");
+			}
+			if (nl) {
+				mw_stats(l50, nl, sl);
+				printf(", \"us_latency\": {\"median\": %.3f, \"max\": %.3f}", sl[0], sl[2]);
+			}
+			printf(", \"per_thread_us\": [");
+			for (int t = 0; t < N; t++)
+				printf("%s%.3f", t ? ", " : "", M[t].per[f]);
+			printf("], \"devices\": [");
+			for (int t = 0; t < N; t++)
+				printf("%s%d", t ? ", " : "", M[t].dev);
+			printf("], \"exact\": %s", exact ? "true" : "false");
+			for (int t = 0; t < N; t++)
+				if (M[t].rc) {
+					printf(", \"error\": \"thread %d: %s\"", t, M[t].err);
+					break;
+				}
+			printf("}\n");
+			fflush(stdout);
+		}
+	}
+	return 0;
+}
+
 int main(int argc, char **argv)
 {
 	const double budget = argc > 1 ? atof(argv[1]) : 0.2;
@@ -263,48 +723,17 @@ int main(int argc, char **argv)
 		fprintf(stderr, "txloop: oracle/_ref/libref_cksum.so not found (make -C oracle ref)\n");
 		return 1;
 	}
-	/* one pool, as a netmap pool holds both rings: two receive halves
-	 * (bursts k and k - 1), two transmit halves (fills k and k - 1) */
-	const size_t half = (size_t)MAXB * SLOT, pool_bytes = 4 * half;
-	uint8_t *pool = mmap(NULL, pool_bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
-	cgck_desc_t *desc = malloc(sizeof(cgck_desc_t) * MAXB);
-	uint32_t *out = malloc(4 * MAXB);
+	if (getenv("TXLOOP_WORKERS"))
+		return multi_main(budget, len);
+	struct wk W0;
 	struct cell c;
-	c.worker = malloc(sizeof(double) * MAXIT);
-	c.wait = malloc(sizeof(double) * MAXIT);
-	c.lat = malloc(sizeof(double) * MAXIT);
-	double *tpost = malloc(sizeof(double) * (MAXIT + 64));
-	if (pool == MAP_FAILED || !desc || !out || !c.worker || !c.wait || !c.lat || !tpost) {
+	if (wk_setup(&W0, len) != 0 || cell_alloc(&c) != 0) {
 		fprintf(stderr, "txloop: out of memory\n");
 		return 1;
 	}
-	uint8_t *rxh[2] = {pool, pool + half}, *txh[2] = {pool + 2 * half, pool + 3 * half};
-	uint64_t s = 0x9E3779B97F4A7C15ull;
-	for (int i = 0; i < MAXB; i++) {
-		make_packet(rxh[0] + (size_t)i * SLOT + L3, len, &s);
-		desc[i].frame_off = (uint64_t)i * SLOT;
-		desc[i].l3_off = L3;
-		desc[i].ip_len = (uint16_t)len;
-	}
-	for (int i = 0; i < MAXB; i++) { /* the sender's fill (reference functions) */
-		uint8_t *ip = rxh[0] + (size_t)i * SLOT + L3;
-		uint16_t v = ref_udp((struct ip *)ip, len - 20);
-		memcpy(ip + 36, &v, 2);
-		v = ref_in(ip, 20);
-		memcpy(ip + 10, &v, 2);
-	}
-	for (int i = 0; i < MAXB; i += 64) /* every 64th frame corrupted */
-		rxh[0][(size_t)i * SLOT + L3 + len - 1] ^= 0x5A;
-	memcpy(rxh[1], rxh[0], half);
-	/* every post names the whole pool, as a transport's does (one base, the
-	 * frames by offset), so bursts posted back to back can share a request */
-	cgck_desc_t *descs[2] = {desc, malloc(sizeof(cgck_desc_t) * MAXB)};
-	if (!descs[1])
-		return 1;
-	for (int i = 0; i < MAXB; i++) {
-		descs[1][i] = desc[i];
-		descs[1][i].frame_off += half;
-	}
+	uint8_t *pool = W0.pool, **rxh = W0.rxh, **txh = W0.txh;
+	const size_t pool_bytes = W0.pool_bytes;
+	cgck_desc_t **descs = W0.descs;
 	if (cgck_host_register(pool, pool_bytes) || cgck_burst_open(NULL, MAXB, (size_t)MAXB * 1536, 0)) {
 		fprintf(stderr, "txloop: setup failed: %s\n", cgck_last_error());
 		return 1;
@@ -414,185 +843,31 @@ int main(int argc, char **argv)
 			const double ns = bud < nns ? nsl[bud] : 0, fixed_us = bud < nns ? 0 : 50;
 			for (int bi = 0; bi < nb; bi++) {
 				const int R = bursts[bi];
-				const double other = (R * ns + fixed_us * 1000) * 1e-9;
-				const int expect = (R + 63) / 64;
 				for (int form = 0; form < 4; form++) {
-					c.it = c.itl = c.bad_rx = c.bad_tx = c.bad_tx_checked = 0;
-					c.total = 0;
-					c.bursts = 0;
-					int k = 0;
-					long copened = 0; /* coalesced form: bursts opened */
-					struct fills cf;
-					memset(&cf, 0, sizeof(cf));
-					const double t0 = now();
-					while (c.it < MAXIT && now() - t0 < budget) {
-						const int rec = k >= 20;
-						g_check = 0;
-						double a = now(), w = 0, lat = 0;
-						int nburst = form == 1 ? k > 0 : 1; /* bursts this iteration processed */
-						int bad = 0;
-						uint8_t *tx = txh[k & 1];
-						if (form == 0) {
-							uint8_t *rx = rxh[k & 1];
-							for (int i = 0; i < R; i++) {
-								uint8_t *ip = rx + (size_t)i * SLOT + L3;
-								bad += verify(ip, len, ref_in, ref_udp);
-								if (mix)
-									reply(tx + (size_t)i * SLOT + L3, ip, ref_in, ref_udp);
-							}
-							lat = now() - a;
-						} else if (form == 1) {
-							double w0 = now();
-							const int done = cgck_tx_complete(); /* fill k - 1 */
-							w += now() - w0;
-							if (done < 0)
-								goto fail;
-							if (mix && k > 0 && done == 2 * R) {
-								c.bad_tx += check_replies(txh[(k + 1) & 1], R);
-								c.bad_tx_checked++;
-							}
-							cgck_tx_begin();
-							tpost[k] = now();
-							if (cgck_rx_post(pool, pool_bytes, descs[k & 1], R) != R)
-								goto fail;
-							if (k > 0) {
-								uint8_t *rx = rxh[(k + 1) & 1];
-								w0 = now();
-								if (cgck_rx_begin_posted() != R)
-									goto fail;
-								w += now() - w0;
-								for (int i = 0; i < R; i++) {
-									uint8_t *ip = rx + (size_t)i * SLOT + L3;
-									bad += verify(ip, len, lib_in, lib_udp);
-									if (mix)
-										reply(tx + (size_t)i * SLOT + L3, ip, lib_in, lib_udp);
-								}
-								if (cgck_rx_end() != 2 * R)
-									goto fail;
-								lat = now() - tpost[k - 1];
-							} else {
-								bad = expect;
-							}
-						} else if (form == 3) {
-							/* the kick releases the fills that are back
-							 * (no wait unless 48 are outstanding); burst k
-							 * is posted; every burst whose values are in
-							 * is processed, oldest first (no wait unless
-							 * 48 are outstanding).  Replies go to a rolling
-							 * cursor over both transmit halves; a fill's
-							 * slots are reused only after it completed. */
-							double w0 = now();
-							while (cf.n > 0 && (cgck_tx_ready() == 1 || cf.n >= 48)) {
-								if (fill_done(&cf, mix, txh[0], &c) < 0)
-									goto fail;
-							}
-							w += now() - w0;
-							cgck_tx_begin();
-							tpost[k % 64] = now();
-							if (cgck_rx_post(pool, pool_bytes, descs[k & 1], R) != R)
-								goto fail;
-							int got = 0;
-							long cur = 0; /* this iteration's reply slots */
-							const long at = cf.cursor % (2 * MAXB);
-							const long gap = mix && at + R > 2 * MAXB ? 2 * MAXB - at : 0;
-							const long room = 2 * MAXB - (at + gap) % (2 * MAXB);
-							for (;;) {
-								const int pend = cgck_rx_pending();
-								const int rdy = pend ? cgck_rx_ready() : 0;
-								if (!pend || (rdy != 1 && pend < 48) || (mix && cur + R > room))
-									break;
-								w0 = now();
-								while (cf.n > 0 && cf.busy + gap + cur + R > 2 * MAXB)
-									if (fill_done(&cf, mix, txh[0], &c) < 0)
-										goto fail;
-								if (cgck_rx_begin_posted() != R)
-									goto fail;
-								w += now() - w0;
-								uint8_t *rx = rxh[copened & 1];
-								for (int i = 0; i < R; i++) {
-									uint8_t *ip = rx + (size_t)i * SLOT + L3;
-									bad += verify(ip, len, lib_in, lib_udp);
-									if (mix)
-										reply(txh[0] + (size_t)((cf.cursor + gap + cur + i) % (2 * MAXB)) *
-												       SLOT +
-											      L3,
-										      ip, lib_in, lib_udp);
-								}
-								if (mix)
-									cur += R;
-								if (cgck_rx_end() != 2 * R)
-									goto fail;
-								lat += now() - tpost[copened % 64];
-								copened++;
-								got++;
-							}
-							bad = got ? (bad == got * expect ? expect : -1) : expect;
-							lat = got ? lat / got : 0;
-							nburst = got;
-							fill_push(&cf, cur ? gap : 0, cur);
-						} else {
-							uint8_t *rx = rxh[k & 1];
-							cgck_tx_begin();
-							double w0 = now();
-							if (cgck_rx_begin(pool, pool_bytes, descs[k & 1], R) != R)
-								goto fail;
-							w += now() - w0;
-							for (int i = 0; i < R; i++) {
-								uint8_t *ip = rx + (size_t)i * SLOT + L3;
-								bad += verify(ip, len, lib_in, lib_udp);
-								if (mix)
-									reply(tx + (size_t)i * SLOT + L3, ip, lib_in, lib_udp);
-							}
-							if (cgck_rx_end() != 2 * R)
-								goto fail;
-							lat = now() - a;
-						}
-						const double a_spin = now();
-						spin(other);
-						const double spun = now() - a_spin;
-						if (form == 1 || form == 3) {
-							if (cgck_tx_post() < 0)
-								goto fail;
-						} else if (form == 2) {
-							const double w0 = now();
-							if (cgck_tx_flush() != (mix ? 2 * R : 0))
-								goto fail;
-							w += now() - w0;
-							if (mix) {
-								c.bad_tx += check_replies(tx, R);
-								c.bad_tx_checked++;
-							}
-						}
-						c.bad_rx += bad != expect;
-						if (rec) {
-							c.total += now() - a - spun - g_check;
-							c.bursts += nburst;
-							c.worker[c.it] = now() - a - spun - g_check;
-							c.wait[c.it] = w;
-							c.it++;
-							if (lat > 0) /* (the coalesced form: iterations that opened bursts) */
-								c.lat[c.itl++] = lat;
-						}
-						k++;
-					}
-					if (form == 1 || form == 3) { /* drain: the bursts and fills left */
-						while (cgck_rx_pending() > 0 && cgck_rx_begin_posted() >= 0)
-							cgck_rx_end();
-						while (cgck_tx_pending() > 0)
-							cgck_tx_complete();
-						memset(&cf, 0, sizeof(cf));
-					}
+					if (run_cell(&W0, form, mix, R, ns, fixed_us, budget, &c) < 0)
+						goto fail;
 					const int n = c.it;
 					const double wm = pct(c.worker, n, 50) * 1e6, w90 = pct(c.worker, n, 90) * 1e6;
 					const double wt = pct(c.wait, n, 50) * 1e6;
 					const double lm = pct(c.lat, c.itl, 50) * 1e6, l90 = pct(c.lat, c.itl, 90) * 1e6;
+					/* A cell that recorded no burst measured nothing: its
+					 * figures are null and it is not exact (bench.py then
+					 * never counts it as beating the reference). */
+					char per[32], wk[96], lt[64];
+					const int none = c.bursts == 0;
+					snprintf(per, sizeof(per), none ? "null" : "%.3f", none ? 0.0 : c.total / c.bursts * 1e6);
+					snprintf(wk, sizeof(wk), n ? "%.3f, \"us_worker_p90\": %.3f, \"us_wait\": %.3f"
+								   : "null, \"us_worker_p90\": null, \"us_wait\": null",
+						 wm, w90, wt);
+					snprintf(lt, sizeof(lt), c.itl ? "%.3f, \"us_latency_p90\": %.3f" : "null, \"us_latency_p90\": null",
+						 lm, l90);
 					printf("{\"mode\": \"loop\", \"form\": \"%s\", \"mix\": \"%s\", \"pkt_len\": %d, "
 					       "\"burst\": %d, \"stack_ns_per_frame\": %.0f, \"stack_us_fixed\": %.0f, "
-					       "\"iters\": %d, \"us_per_burst\": %.3f, \"us_worker\": %.3f, \"us_worker_p90\": %.3f, \"us_wait\": %.3f, "
-					       "\"us_latency\": %.3f, \"us_latency_p90\": %.3f, \"exact\": %s}\n",
-					       forms[form], mix ? "rx+reply" : "rx", len, R, ns, fixed_us, n,
-					       c.bursts ? c.total / c.bursts * 1e6 : 0.0, wm, w90, wt, lm,
-					       l90, c.bad_rx == 0 && c.bad_tx == 0 ? "true" : "false");
+					       "\"iters\": %d, \"iters_all\": %d, \"bursts\": %ld, \"max_iter_us\": %.1f, \"max_iter_at\": %d, "
+					       "\"us_per_burst\": %s, \"us_worker\": %s, \"us_latency\": %s, \"exact\": %s}\n",
+					       forms[form], mix ? "rx+reply" : "rx", len, R, ns, fixed_us, n, c.iters_all, c.bursts,
+					       c.max_iter * 1e6, c.max_at, per, wk, lt,
+					       !none && c.bad_rx == 0 && c.bad_tx == 0 ? "true" : "false");
 					fflush(stdout);
 				}
 			}
