@@ -224,6 +224,8 @@ struct Poster {
 	const uint32_t *metas(const PostItem &x) const { return x.own ? nullptr : rq[x.req].m.data() + x.off; }
 	int take_slot();
 	void release_if_free(int ri);
+	bool backlog(const cgck_ctx *c, int kind);
+	void bound(cgck_ctx *c, int kind);
 	void send(cgck_ctx *c);
 	void collect(cgck_ctx *c, int ri);
 	void pump(cgck_ctx *c, int kind, bool wait);
@@ -949,6 +951,41 @@ void Poster::release_if_free(int ri)
 	}
 }
 
+// The latency bound of the coalesced queues.  While a
+// kind's request is in flight, what is posted meanwhile waits and goes out
+// together when it is back; a loop that posts faster than the GPU serves (a
+// burst of 2048 frames every few us) would otherwise queue up to kPostQ
+// requests' worth behind it — 48 bursts, 1.1 ms from post to verdict at 2048
+// frames (profiles/r05/final/table_64.txt).  Only one request per kind is
+// ever in flight, so a deeper queue buys no GPU throughput: once the unsent
+// items hold more than one server request can carry (max_pkts frames or
+// max_bytes), the post waits for the request in flight and sends the next
+// one, so a posted item is at most ~two service times from its values.
+// Small bursts coalesce as before (64 bursts of up to 32 frames fit one
+// request).
+bool Poster::backlog(const cgck_ctx *c, int kind)
+{
+	if (!c->bbox || inflight[kind] < 0)
+		return false;
+	const PostQueue &qq = q[kind];
+	uint64_t n = 0;
+	size_t b = 0;
+	for (unsigned k = qq.sent; k < qq.count; k++) {
+		const PostItem &x = qq.it[(qq.head + k) % kPostQ];
+		if (x.own)
+			continue;
+		n += x.n;
+		b += x.pkt_bytes;
+	}
+	return n > c->bmax || b > c->bmax_bytes;
+}
+
+void Poster::bound(cgck_ctx *c, int kind)
+{
+	for (int k = 0; k < 4 && backlog(c, kind); k++)
+		pump(c, kind, true);
+}
+
 // Send what each kind with nothing in flight has waiting: both kinds as one
 // two-part request when they share the range (the receive frames first, so
 // their meta words come back too), else one request each.
@@ -1181,6 +1218,7 @@ extern "C" int cgck_rx_post(void *base, size_t bytes, const cgck_desc_t *desc, u
 	x.own = n == 0;
 	x.vals.clear();
 	t.post.pump(c, kRx, false);
+	t.post.bound(c, kRx);
 	return (int)n;
 }
 
@@ -1520,6 +1558,7 @@ extern "C" int cgck_tx_post(void)
 		return rc;
 	}
 	t.post.pump(c, kTx, false);
+	t.post.bound(c, kTx);
 	if (old_rc < 0)
 		return set_err(old_rc, "cgck_tx_post: this window was posted, but completing the oldest fill failed "
 				       "(its fields are not written): %s", old_msg);

@@ -104,6 +104,10 @@ for step in "$@"; do
 		run workers_q4 600 tools/txloop 0.3 || exit 1 ;;
 	workersq) # the same with more hardware queues per process (each resident server needs its own)
 		GPU_MAX_HW_QUEUES=32 run workers_q32 600 tools/txloop 0.3 || exit 1 ;;
+	workersk) # the knee: 16..32 workers, the stack work spun, then slept (the CPU-quota control)
+		TXLOOP_WORKERS=16,20,24,28,32 run workers_knee 600 tools/txloop 0.3 || exit 1
+		TXLOOP_SLEEP=1 TXLOOP_WORKERS=1,16,24,32 run workers_sleep 600 tools/txloop 0.3 || exit 1 ;;
+	vramdb) run vramdb 120 tools/vramdb 0.3 || exit 1 ;;
 	shards) run shards 600 python -u -m pytest tests/test_gpu_shards.py -m gpu -x -v -s --timeout 500 --timeout-method thread || exit 1 ;;
 	prof) bash tools/gpu_prof_layouts.sh $(basename $O)/prof || exit 1 ;;
 	*) echo "unknown step $step"; exit 2 ;;

@@ -84,8 +84,18 @@ static double pct(double *t, int n, int p)
 	return t[(long)n * p / 100 < n ? (long)n * p / 100 : n - 1];
 }
 
+/* TXLOOP_SLEEP=1: the stack's other work is slept instead of spun (the
+ * workers mode's control for the host's CPU quota: 32 spinning workers on a
+ * box that grants 16 CPUs are throttled whatever the GPU does) */
+static int g_sleep;
+
 static void spin(double sec)
 {
+	if (g_sleep && sec > 0) {
+		const struct timespec ts = {0, (long)(sec * 1e9)};
+		nanosleep(&ts, NULL);
+		return;
+	}
 	for (const double s0 = now(); now() - s0 < sec;)
 		;
 }
@@ -181,6 +191,34 @@ static int check_replies(const uint8_t *txh, int R)
 		c[10] = c[11] = 0;
 		bad += ref_in(c, 20) != s_ip;
 	}
+	g_check += now() - t0;
+	return bad;
+}
+
+/* The full-transmit-ring regime: with no free slot, the stack builds the
+ * segment in its stack-local struct packet (bsd44/tcp_output.c:60,
+ * netmap.c:76-78, dpdk.c:232-236) and parks it with add_pending_packet
+ * (subr.c:264-286).  That memory is not registered, so the TX window computes
+ * both checksums synchronously (cgck_window_stats [3]).  Every 16th reply is
+ * checked against the reference's values (time kept out of the worker's). */
+static int reply_body(const uint8_t *rx, in_fn fin, udp_fn fudp, int i)
+{
+	uint8_t pkt_body[128];
+	reply(pkt_body, rx, fin, fudp);
+	if (i % 16)
+		return 0;
+	const double t0 = now();
+	uint8_t c[64];
+	memcpy(c, pkt_body, 40);
+	uint16_t s_ip, s_tcp, v;
+	memcpy(&s_ip, c + 10, 2);
+	memcpy(&s_tcp, c + 36, 2);
+	c[36] = c[37] = 0;
+	v = ref_udp((struct ip *)c, 20);
+	int bad = v != s_tcp;
+	memcpy(c + 36, &v, 2);
+	c[10] = c[11] = 0;
+	bad += ref_in(c, 20) != s_ip;
 	g_check += now() - t0;
 	return bad;
 }
@@ -297,177 +335,189 @@ static int run_cell(struct wk *W, int form, int mix, int R, double ns, double fi
 	const int expect = (R + 63) / 64;
 	in_fn lib_in = (in_fn)in_cksum;
 	udp_fn lib_udp = (udp_fn)udp_cksum;
-		c.it = c.itl = c.bad_rx = c.bad_tx = c.bad_tx_checked = 0;
-		c.total = 0;
-		c.bursts = 0;
-		c.max_iter = 0;
-		c.max_at = -1;
-		int k = 0;
-		long copened = 0; /* coalesced form: bursts opened */
-		struct fills cf;
-		memset(&cf, 0, sizeof(cf));
-		const double t0 = now();
-		while (c.it < MAXIT && now() - t0 < budget) {
-			const int rec = k >= 20;
-			g_check = 0;
-			double a = now(), w = 0, lat = 0;
-			int nburst = form == 1 ? k > 0 : 1; /* bursts this iteration processed */
-			int bad = 0;
-			uint8_t *tx = txh[k & 1];
-			if (form == 0) {
-				uint8_t *rx = rxh[k & 1];
-				for (int i = 0; i < R; i++) {
-					uint8_t *ip = rx + (size_t)i * SLOT + L3;
-					bad += verify(ip, len, ref_in, ref_udp);
-					if (mix)
-						reply(tx + (size_t)i * SLOT + L3, ip, ref_in, ref_udp);
-				}
-				lat = now() - a;
-			} else if (form == 1) {
-				double w0 = now();
-				const int done = cgck_tx_complete(); /* fill k - 1 */
-				w += now() - w0;
-				if (done < 0)
-					return -1;
-				if (mix && k > 0 && done == 2 * R) {
-					c.bad_tx += check_replies(txh[(k + 1) & 1], R);
-					c.bad_tx_checked++;
-				}
-				cgck_tx_begin();
-				tpost[k] = now();
-				if (cgck_rx_post(pool, pool_bytes, descs[k & 1], R) != R)
-					return -1;
-				if (k > 0) {
-					uint8_t *rx = rxh[(k + 1) & 1];
-					w0 = now();
-					if (cgck_rx_begin_posted() != R)
-						return -1;
-					w += now() - w0;
-					for (int i = 0; i < R; i++) {
-						uint8_t *ip = rx + (size_t)i * SLOT + L3;
-						bad += verify(ip, len, lib_in, lib_udp);
-						if (mix)
-							reply(tx + (size_t)i * SLOT + L3, ip, lib_in, lib_udp);
-					}
-					if (cgck_rx_end() != 2 * R)
-						return -1;
-					lat = now() - tpost[k - 1];
-				} else {
-					bad = expect;
-				}
-			} else if (form == 3) {
-				/* the kick releases the fills that are back
-				 * (no wait unless 48 are outstanding); burst k
-				 * is posted; every burst whose values are in
-				 * is processed, oldest first (no wait unless
-				 * 48 are outstanding).  Replies go to a rolling
-				 * cursor over both transmit halves; a fill's
-				 * slots are reused only after it completed. */
-				double w0 = now();
-				while (cf.n > 0 && (cgck_tx_ready() == 1 || cf.n >= 48)) {
-					if (fill_done(&cf, mix, txh[0], &c) < 0)
-						return -1;
-				}
-				w += now() - w0;
-				cgck_tx_begin();
-				tpost[k % 64] = now();
-				if (cgck_rx_post(pool, pool_bytes, descs[k & 1], R) != R)
-					return -1;
-				int got = 0;
-				long cur = 0; /* this iteration's reply slots */
-				const long at = cf.cursor % (2 * MAXB);
-				const long gap = mix && at + R > 2 * MAXB ? 2 * MAXB - at : 0;
-				const long room = 2 * MAXB - (at + gap) % (2 * MAXB);
-				for (;;) {
-					const int pend = cgck_rx_pending();
-					const int rdy = pend ? cgck_rx_ready() : 0;
-					if (!pend || (rdy != 1 && pend < 48) || (mix && cur + R > room))
-						break;
-					w0 = now();
-					while (cf.n > 0 && cf.busy + gap + cur + R > 2 * MAXB)
-						if (fill_done(&cf, mix, txh[0], &c) < 0)
-							return -1;
-					if (cgck_rx_begin_posted() != R)
-						return -1;
-					w += now() - w0;
-					uint8_t *rx = rxh[copened & 1];
-					for (int i = 0; i < R; i++) {
-						uint8_t *ip = rx + (size_t)i * SLOT + L3;
-						bad += verify(ip, len, lib_in, lib_udp);
-						if (mix)
-							reply(txh[0] + (size_t)((cf.cursor + gap + cur + i) % (2 * MAXB)) *
-									       SLOT +
-								      L3,
-							      ip, lib_in, lib_udp);
-					}
-					if (mix)
-						cur += R;
-					if (cgck_rx_end() != 2 * R)
-						return -1;
-					lat += now() - tpost[copened % 64];
-					copened++;
-					got++;
-				}
-				bad = got ? (bad == got * expect ? expect : -1) : expect;
-				lat = got ? lat / got : 0;
-				nburst = got;
-				fill_push(&cf, cur ? gap : 0, cur);
-			} else {
-				uint8_t *rx = rxh[k & 1];
-				cgck_tx_begin();
-				double w0 = now();
-				if (cgck_rx_begin(pool, pool_bytes, descs[k & 1], R) != R)
+	/* mix 2: the replies go to the stack-local struct packet (a full
+	 * transmit ring), mix 1 to transmit slots; below, `mix` is the latter */
+	const int body = mix == 2;
+	mix = body ? 0 : mix;
+	c.it = c.itl = c.bad_rx = c.bad_tx = c.bad_tx_checked = 0;
+	c.total = 0;
+	c.bursts = 0;
+	c.max_iter = 0;
+	c.max_at = -1;
+	int k = 0;
+	long copened = 0; /* coalesced form: bursts opened */
+	struct fills cf;
+	memset(&cf, 0, sizeof(cf));
+	const double t0 = now();
+	while (c.it < MAXIT && now() - t0 < budget) {
+		const int rec = k >= 20;
+		g_check = 0;
+		double a = now(), w = 0, lat = 0;
+		int nburst = form == 1 ? k > 0 : 1; /* bursts this iteration processed */
+		int bad = 0;
+		uint8_t *tx = txh[k & 1];
+		if (form == 0) {
+			uint8_t *rx = rxh[k & 1];
+			for (int i = 0; i < R; i++) {
+				uint8_t *ip = rx + (size_t)i * SLOT + L3;
+				bad += verify(ip, len, ref_in, ref_udp);
+				if (body)
+					c.bad_tx += reply_body(ip, ref_in, ref_udp, i);
+				if (mix)
+					reply(tx + (size_t)i * SLOT + L3, ip, ref_in, ref_udp);
+			}
+			lat = now() - a;
+		} else if (form == 1) {
+			double w0 = now();
+			const int done = cgck_tx_complete(); /* fill k - 1 */
+			w += now() - w0;
+			if (done < 0)
+				return -1;
+			if (mix && k > 0 && done == 2 * R) {
+				c.bad_tx += check_replies(txh[(k + 1) & 1], R);
+				c.bad_tx_checked++;
+			}
+			cgck_tx_begin();
+			tpost[k] = now();
+			if (cgck_rx_post(pool, pool_bytes, descs[k & 1], R) != R)
+				return -1;
+			if (k > 0) {
+				uint8_t *rx = rxh[(k + 1) & 1];
+				w0 = now();
+				if (cgck_rx_begin_posted() != R)
 					return -1;
 				w += now() - w0;
 				for (int i = 0; i < R; i++) {
 					uint8_t *ip = rx + (size_t)i * SLOT + L3;
 					bad += verify(ip, len, lib_in, lib_udp);
+					if (body)
+						c.bad_tx += reply_body(ip, lib_in, lib_udp, i);
 					if (mix)
 						reply(tx + (size_t)i * SLOT + L3, ip, lib_in, lib_udp);
 				}
 				if (cgck_rx_end() != 2 * R)
 					return -1;
-				lat = now() - a;
+				lat = now() - tpost[k - 1];
+			} else {
+				bad = expect;
 			}
-			const double a_spin = now();
-			spin(other);
-			const double spun = now() - a_spin;
-			if (form == 1 || form == 3) {
-				if (cgck_tx_post() < 0)
+		} else if (form == 3) {
+			/* the kick releases the fills that are back
+			 * (no wait unless 48 are outstanding); burst k
+			 * is posted; every burst whose values are in
+			 * is processed, oldest first (no wait unless
+			 * 48 are outstanding).  Replies go to a rolling
+			 * cursor over both transmit halves; a fill's
+			 * slots are reused only after it completed. */
+			double w0 = now();
+			while (cf.n > 0 && (cgck_tx_ready() == 1 || cf.n >= 48)) {
+				if (fill_done(&cf, mix, txh[0], &c) < 0)
 					return -1;
-			} else if (form == 2) {
-				const double w0 = now();
-				if (cgck_tx_flush() != (mix ? 2 * R : 0))
+			}
+			w += now() - w0;
+			cgck_tx_begin();
+			tpost[k % 64] = now();
+			if (cgck_rx_post(pool, pool_bytes, descs[k & 1], R) != R)
+				return -1;
+			int got = 0;
+			long cur = 0; /* this iteration's reply slots */
+			const long at = cf.cursor % (2 * MAXB);
+			const long gap = mix && at + R > 2 * MAXB ? 2 * MAXB - at : 0;
+			const long room = 2 * MAXB - (at + gap) % (2 * MAXB);
+			for (;;) {
+				const int pend = cgck_rx_pending();
+				const int rdy = pend ? cgck_rx_ready() : 0;
+				if (!pend || (rdy != 1 && pend < 48) || (mix && cur + R > room))
+					break;
+				w0 = now();
+				while (cf.n > 0 && cf.busy + gap + cur + R > 2 * MAXB)
+					if (fill_done(&cf, mix, txh[0], &c) < 0)
+						return -1;
+				if (cgck_rx_begin_posted() != R)
 					return -1;
 				w += now() - w0;
-				if (mix) {
-					c.bad_tx += check_replies(tx, R);
-					c.bad_tx_checked++;
+				uint8_t *rx = rxh[copened & 1];
+				for (int i = 0; i < R; i++) {
+					uint8_t *ip = rx + (size_t)i * SLOT + L3;
+					bad += verify(ip, len, lib_in, lib_udp);
+					if (body)
+						c.bad_tx += reply_body(ip, lib_in, lib_udp, i);
+					if (mix)
+						reply(txh[0] + (size_t)((cf.cursor + gap + cur + i) % (2 * MAXB)) *
+								       SLOT +
+							      L3,
+						      ip, lib_in, lib_udp);
 				}
+				if (mix)
+					cur += R;
+				if (cgck_rx_end() != 2 * R)
+					return -1;
+				lat += now() - tpost[copened % 64];
+				copened++;
+				got++;
 			}
-			c.bad_rx += bad != expect;
-			if (now() - a > c.max_iter) {
-				c.max_iter = now() - a;
-				c.max_at = k;
+			bad = got ? (bad == got * expect ? expect : -1) : expect;
+			lat = got ? lat / got : 0;
+			nburst = got;
+			fill_push(&cf, cur ? gap : 0, cur);
+		} else {
+			uint8_t *rx = rxh[k & 1];
+			cgck_tx_begin();
+			double w0 = now();
+			if (cgck_rx_begin(pool, pool_bytes, descs[k & 1], R) != R)
+				return -1;
+			w += now() - w0;
+			for (int i = 0; i < R; i++) {
+				uint8_t *ip = rx + (size_t)i * SLOT + L3;
+				bad += verify(ip, len, lib_in, lib_udp);
+				if (body)
+					c.bad_tx += reply_body(ip, lib_in, lib_udp, i);
+				if (mix)
+					reply(tx + (size_t)i * SLOT + L3, ip, lib_in, lib_udp);
 			}
-			if (rec) {
-				c.total += now() - a - spun - g_check;
-				c.bursts += nburst;
-				c.worker[c.it] = now() - a - spun - g_check;
-				c.wait[c.it] = w;
-				c.it++;
-				if (lat > 0) /* (the coalesced form: iterations that opened bursts) */
-					c.lat[c.itl++] = lat;
-			}
-			k++;
+			if (cgck_rx_end() != 2 * R)
+				return -1;
+			lat = now() - a;
 		}
-		if (form == 1 || form == 3) { /* drain: the bursts and fills left */
-			while (cgck_rx_pending() > 0 && cgck_rx_begin_posted() >= 0)
-				cgck_rx_end();
-			while (cgck_tx_pending() > 0)
-				cgck_tx_complete();
-			memset(&cf, 0, sizeof(cf));
+		const double a_spin = now();
+		spin(other);
+		const double spun = now() - a_spin;
+		if (form == 1 || form == 3) {
+			if (cgck_tx_post() < 0)
+				return -1;
+		} else if (form == 2) {
+			const double w0 = now();
+			if (cgck_tx_flush() != (mix ? 2 * R : 0))
+				return -1;
+			w += now() - w0;
+			if (mix) {
+				c.bad_tx += check_replies(tx, R);
+				c.bad_tx_checked++;
+			}
 		}
+		c.bad_rx += bad != expect;
+		if (now() - a > c.max_iter) {
+			c.max_iter = now() - a;
+			c.max_at = k;
+		}
+		if (rec) {
+			c.total += now() - a - spun - g_check;
+			c.bursts += nburst;
+			c.worker[c.it] = now() - a - spun - g_check;
+			c.wait[c.it] = w;
+			c.it++;
+			if (lat > 0) /* (the coalesced form: iterations that opened bursts) */
+				c.lat[c.itl++] = lat;
+		}
+		k++;
+	}
+	if (form == 1 || form == 3) { /* drain: the bursts and fills left */
+		while (cgck_rx_pending() > 0 && cgck_rx_begin_posted() >= 0)
+			cgck_rx_end();
+		while (cgck_tx_pending() > 0)
+			cgck_tx_complete();
+		memset(&cf, 0, sizeof(cf));
+	}
 	c.iters_all = k;
 	*cp = c;
 	return 0;
@@ -580,6 +630,7 @@ static int multi_main(double budget, int len)
 	const int R = getenv("TXLOOP_MW_BURST") ? atoi(getenv("TXLOOP_MW_BURST")) : 64;
 	const double ns = getenv("TXLOOP_MW_NS") ? atof(getenv("TXLOOP_MW_NS")) : 250;
 	const int mix = getenv("TXLOOP_MW_MIX") ? atoi(getenv("TXLOOP_MW_MIX")) : 1;
+	g_sleep = getenv("TXLOOP_SLEEP") && atoi(getenv("TXLOOP_SLEEP"));
 	if (R < 1 || R > MAXB / 2)
 		return 2;
 	static const char *fname[4] = {"reference", "pipelined", "sync", "coalesced"};
@@ -644,8 +695,10 @@ static int multi_main(double budget, int len)
 					l50[nl++] = M[t].l50[f];
 			}
 			printf("{\"mode\": \"workers\", \"workers\": %d, \"form\": \"%s\", \"mix\": \"%s\", \"pkt_len\": %d, "
-			       "\"burst\": %d, \"stack_ns_per_frame\": %.0f, \"cpus\": %d, \"cpu_max\": \"%s\", \"bursts\": %ld",
-			       N, fname[forms[f]], mix ? "rx+reply" : "rx", len, R, ns, ncpu, quota, bursts);
+			       "\"burst\": %d, \"stack_ns_per_frame\": %.0f, \"stack_work\": \"%s\", \"cpus\": %d, \"cpu_max\": \"%s\", "
+			       "\"bursts\": %ld",
+			       N, fname[forms[f]], mix ? "rx+reply" : "rx", len, R, ns, g_sleep ? "slept" : "spun", ncpu, quota,
+			       bursts);
 			if (np) {
 				mw_stats(per, np, sp);
 				mw_stats(w90, np, s90);
@@ -838,7 +891,22 @@ int main(int argc, char **argv)
 		return 0;
 	}
 	static const char *forms[4] = {"reference", "pipelined", "sync", "coalesced"};
-	for (int mix = 0; mix < 2; mix++) {
+	/* TXLOOP_MIXES: 0 rx, 1 rx + replies in transmit slots, 2 rx + replies
+	 * in the stack-local packet (a full transmit ring); default 0,1 */
+	int mixes[3] = {0, 1, 2}, nmix = 2;
+	if (getenv("TXLOOP_MIXES")) {
+		nmix = 0;
+		for (char *e = getenv("TXLOOP_MIXES"); *e && nmix < 3;) {
+			const int v = (int)strtol(e, &e, 10);
+			if (v >= 0 && v <= 2)
+				mixes[nmix++] = v;
+			while (*e == ',')
+				e++;
+		}
+	}
+	static const char *mixname[3] = {"rx", "rx+reply", "rx+reply(full ring)"};
+	for (int mi = 0; mi < nmix; mi++) {
+		const int mix = mixes[mi];
 		for (int bud = 0; bud <= nns; bud++) {
 			const double ns = bud < nns ? nsl[bud] : 0, fixed_us = bud < nns ? 0 : 50;
 			for (int bi = 0; bi < nb; bi++) {
@@ -865,7 +933,7 @@ int main(int argc, char **argv)
 					       "\"burst\": %d, \"stack_ns_per_frame\": %.0f, \"stack_us_fixed\": %.0f, "
 					       "\"iters\": %d, \"iters_all\": %d, \"bursts\": %ld, \"max_iter_us\": %.1f, \"max_iter_at\": %d, "
 					       "\"us_per_burst\": %s, \"us_worker\": %s, \"us_latency\": %s, \"exact\": %s}\n",
-					       forms[form], mix ? "rx+reply" : "rx", len, R, ns, fixed_us, n, c.iters_all, c.bursts,
+					       forms[form], mixname[mix], len, R, ns, fixed_us, n, c.iters_all, c.bursts,
 					       c.max_iter * 1e6, c.max_at, per, wk, lt,
 					       !none && c.bad_rx == 0 && c.bad_tx == 0 ? "true" : "false");
 					fflush(stdout);
