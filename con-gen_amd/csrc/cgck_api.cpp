@@ -428,7 +428,7 @@ static void burst_finish_posted(cgck_ctx *c)
 	BurstBox *b = c->bbox;
 	for (uint32_t s = c->bdone, k = 0; s != c->bseq && k < 4; k++) {
 		s = burst_next(s);
-		const uint32_t n = (uint32_t)(__atomic_load_n(&b->req[s & 1], __ATOMIC_ACQUIRE) >> 32);
+		const uint32_t n = (uint32_t)(c->breq[s & 1] >> 32) & ~kBurstVram;
 		const uint32_t W = burst_wgs(n, c->bwgs, c->bper);
 		const double t0 = now_s();
 		uint32_t j = 0;
@@ -479,8 +479,8 @@ static int burst_launch(cgck_ctx *c, uint32_t start_seq)
 		;
 	for (uint32_t j = 0; j < c->bwgs; j++)
 		__atomic_store_n(&c->bbox->alive[j], (uint8_t)1, __ATOMIC_RELEASE);
-	hipError_t e = launch_burst_server(c->bbox_dev, c->bstage_dev, c->bscratch, c->bresp_dev, c->brelay,
-					   c->d_zero, (uint32_t)c->bstage_cap,
+	hipError_t e = launch_burst_server(c->bbox_dev, c->bdoor ? c->bdoor : c->bbox_dev->req, c->bstage_dev, c->bvblk,
+					   c->bscratch, c->bresp_dev, c->brelay, c->d_zero, (uint32_t)c->bstage_cap,
 					   c->bmax, c->bwgs, c->bper, start_seq, epoch, server_opts(), c->bstream);
 	if (e != hipSuccess) {
 		for (uint32_t j = 0; j < c->bwgs; j++)
@@ -707,16 +707,26 @@ int cgck::burst_ready(cgck_ctx *c, const BurstPending *p)
 	return 1;
 }
 
-// The block of the next request, with its slot free: a posted request still
-// holding that slot is collected first.
-static int burst_slot_free(cgck_ctx *c, uint8_t **block)
+// The block of the next request (L.bytes of it), with its slot free: a
+// posted request still holding that slot is collected first.  A block of up
+// to kBurstVramMax bytes (a drop-in call on up to ~1.9 KiB, a burst of up to
+// ~165 descriptors in place) goes to the slot's device-memory block when the
+// device has one: the host writes it through the large BAR (write-combined)
+// and the server reads it locally instead of across the fabric
+// (tools/vramdb: 4.70 against 5.55 us for the bare round trip of a 4 KiB
+// block, profiles/r06/).  Larger blocks stay in host staging: the host's
+// write-combined stores cost ~0.13 us a KiB (0.53 us for 4 KiB against 0.06
+// into host memory), which is the worker's time.
+static const size_t kBurstVramMax = env_size(CGCK_ENV("CGCK_BURST_VRAM_MAX"), 2048); // lab A/B: the bound
+static int burst_slot_free(cgck_ctx *c, const BurstLayout &L, uint8_t **block)
 {
 	const uint32_t seq = burst_next(c->bseq);
 	if (BurstPending *p = c->bslot[seq & 1]) {
 		const int rc = burst_collect(c, p); // its poster reads p->rc
 		(void)rc;
 	}
-	*block = burst_block(c, seq);
+	c->bnext_vram = c->bvblk && L.bytes <= kBurstVramMax && L.bytes <= kBurstFirst;
+	*block = c->bnext_vram ? c->bvblk + (size_t)(seq & 1) * kBurstFirst : burst_block(c, seq);
 	return 0;
 }
 
@@ -728,7 +738,8 @@ static int burst_post(cgck_ctx *c, const uint8_t *base_dev, uint64_t range, uint
 	MapGuard map_g(c);
 	BurstBox *b = c->bbox;
 	const uint32_t seq = burst_next(c->bseq);
-	BurstReq *r = (BurstReq *)burst_block(c, seq);
+	const bool vram = c->bnext_vram;
+	BurstReq *r = (BurstReq *)(vram ? c->bvblk + (size_t)(seq & 1) * kBurstFirst : burst_block(c, seq));
 	r->n = (uint32_t)n;
 	r->flags = flags;
 	r->max_len = max_len;
@@ -743,7 +754,18 @@ static int burst_post(cgck_ctx *c, const uint8_t *base_dev, uint64_t range, uint
 #if CGCK_LAB
 	t_lab_host[0] = (uint64_t)(now_s() * 1e9);
 #endif
-	__atomic_store_n(&b->req[seq & 1], (uint64_t)seq | (uint64_t)n << 32, __ATOMIC_RELEASE);
+	const uint64_t word = (uint64_t)seq | (uint64_t)((uint32_t)n | (vram ? kBurstVram : 0u)) << 32;
+	c->breq[seq & 1] = word;
+	if (c->bdoor) {
+		// The block's stores (write-combined device memory, or host memory)
+		// are out before the doorbell, and the doorbell leaves the
+		// write-combining buffer now rather than at its next eviction.
+		__builtin_ia32_sfence();
+		__atomic_store_n(&c->bdoor[seq & 1], word, __ATOMIC_RELAXED);
+		__builtin_ia32_sfence();
+	} else {
+		__atomic_store_n(&b->req[seq & 1], word, __ATOMIC_RELEASE);
+	}
 	*seq_out = seq;
 	if (!burst_all_alive(c)) {
 		int rc = burst_restart(c); // idled out: a new server picks the pending requests up
@@ -851,7 +873,7 @@ static int desc_host_impl(cgck_ctx *c, void *base, size_t bytes, const cgck_desc
 		// the resident server: no launch, no stream sync
 		const BurstLayout L = burst_layout(in_place ? 0 : pkt_bytes, n);
 		uint8_t *h;
-		if ((rc = burst_slot_free(c, &h)))
+		if ((rc = burst_slot_free(c, L, &h)))
 			return rc;
 		cgck_desc_t *d = (cgck_desc_t *)(h + L.d_off);
 		if (in_place) {
@@ -1028,7 +1050,7 @@ extern "C" int cgck_burst_request(cgck_ctx_t *c, const void *dev_base, uint64_t 
 					"exceed its capacity", (unsigned long long)n);
 	const BurstLayout L = burst_layout(0, n);
 	uint8_t *h;
-	if ((rc = burst_slot_free(c, &h)))
+	if ((rc = burst_slot_free(c, L, &h)))
 		return rc;
 	memcpy(h + L.d_off, desc, 12 * n);
 	uint32_t seq;
@@ -1168,7 +1190,7 @@ int cgck::one_region(cgck_ctx *c, const void *src, uint32_t span, uint32_t ip_le
 		// the resident server: one descriptor, no launch, no stream sync
 		const BurstLayout L = burst_layout(span, 1);
 		uint8_t *h;
-		if ((rc = burst_slot_free(c, &h)))
+		if ((rc = burst_slot_free(c, L, &h)))
 			return rc;
 		if (span)
 			memcpy(h + L.p_off, src, span);
@@ -1215,6 +1237,36 @@ static hipError_t burst_stream(const cgck_ctx *c, hipStream_t *st)
 	return hipExtStreamCreateWithCUMask(st, (uint32_t)words, mask);
 }
 
+// Resident servers a device takes from this process: each holds a hardware
+// queue of its own (burst_stream), and with 20 or more a device could not map
+// every server's queue on every XCD at once — a server's workgroups on one XCD
+// never started (a request not served in 2 s) or waited ms for the
+// scheduler's time slice (tools/txloop workers mode, 16 / 20 / 24 / 28 / 32
+// workers on one MI355X, profiles/r06/).  con-gen's 32 workers bound over a
+// node's eight GPUs hold four each.
+constexpr uint32_t kMaxServersPerDevice = 16;
+
+// The server's stream and memory, freed (no server kernel running).
+static void burst_release(cgck_ctx *c)
+{
+	(void)hipStreamDestroy(c->bstream);
+	(void)hipHostFree(c->bbox);
+	(void)hipHostFree(c->bstage);
+	(void)hipHostFree(c->bresp);
+	(void)hipFree(c->bscratch);
+	(void)hipFree(c->brelay);
+	if (c->bdoor)
+		(void)hipFree(c->bdoor);
+	c->bdoor = nullptr;
+	c->bvblk = nullptr;
+	c->bbox = nullptr;
+	c->bstage = nullptr;
+	c->bstage_cap = 0;
+	c->bresp = nullptr;
+	c->bscratch = nullptr;
+	c->brelay = nullptr;
+}
+
 extern "C" int cgck_burst_open(cgck_ctx_t *c, uint32_t max_pkts, size_t max_bytes, uint32_t idle_ms)
 {
 	if (!c && !(c = thread_ctx()))
@@ -1223,6 +1275,8 @@ extern "C" int cgck_burst_open(cgck_ctx_t *c, uint32_t max_pkts, size_t max_byte
 		return set_err(-EBUSY, "cgck_burst_open: already open on this context");
 	if (max_pkts == 0 || max_bytes == 0)
 		return set_err(-EINVAL, "cgck_burst_open: zero capacity");
+	if (max_pkts >= kBurstVram)
+		return set_err(-EINVAL, "cgck_burst_open: max_pkts %u", max_pkts);
 	HIP_TRY(hipSetDevice(c->device));
 	// the block holds the header, the descriptors and the packet bytes; the
 	// server's first read fetches kBurstFirst bytes whatever the request
@@ -1254,18 +1308,38 @@ extern "C" int cgck_burst_open(cgck_ctx_t *c, uint32_t max_pkts, size_t max_byte
 		e = hipHostGetDevicePointer(&sd, st, 0);
 	if (e == hipSuccess)
 		e = hipHostGetDevicePointer(&rd, rs, 0);
+	// The doorbell and the small-block slots in device memory the host writes
+	// through the large BAR (every VRAM allocation is host-mapped there:
+	// tools/vramdb), uncached so the server's polls and reads go to memory,
+	// where the host's writes land.  $CGCK_BURST_HOST_DOOR (lab build): the
+	// host-memory mailbox and blocks alone, the A/B.
+	void *vd = nullptr;
+	int large_bar = 0;
+	if (e == hipSuccess && !CGCK_ENV("CGCK_BURST_HOST_DOOR") &&
+	    hipDeviceGetAttribute(&large_bar, hipDeviceAttributeIsLargeBar, c->device) == hipSuccess && large_bar) {
+		if (hipExtMallocWithFlags(&vd, 64 + 2 * (size_t)kBurstFirst, hipDeviceMallocUncached) != hipSuccess ||
+		    hipMemset(vd, 0, 64 + 2 * (size_t)kBurstFirst) != hipSuccess) {
+			(void)hipGetLastError();
+			if (vd)
+				(void)hipFree(vd);
+			vd = nullptr; // the host-memory mailbox then
+		}
+	}
 	if (e == hipSuccess)
 		e = burst_stream(c, &c->bstream);
 	if (e != hipSuccess) {
 		for (void *h : {box, st, rs})
 			if (h)
 				(void)hipHostFree(h);
-		if (sc)
-			(void)hipFree(sc);
-		if (rl)
-			(void)hipFree(rl);
+		for (void *d : {sc, rl, vd})
+			if (d)
+				(void)hipFree(d);
 		return set_err(-EIO, "cgck_burst_open: %s", hipGetErrorString(e));
 	}
+	c->bdoor = (uint64_t *)vd;
+	c->bvblk = vd ? (uint8_t *)vd + 64 : nullptr;
+	c->bnext_vram = false;
+	c->breq[0] = c->breq[1] = 0;
 	memset(box, 0, sizeof(BurstBox));
 	memset(st, 0, 2 * cap);
 	c->bbox = (BurstBox *)box;
@@ -1296,9 +1370,24 @@ extern "C" int cgck_burst_open(cgck_ctx_t *c, uint32_t max_pkts, size_t max_byte
 	c->bslot[0] = c->bslot[1] = nullptr;
 	c->bbusy = 0;
 	std::lock_guard<std::mutex> map_wr(g_map_wr); // no mapping changes while it joins g_srv and launches
+	bool full = false;
+	uint32_t on_dev = 0;
 	{
 		std::lock_guard<std::mutex> lk(g_srv_mu);
-		g_srv.push_back(c);
+		for (const cgck_ctx *x : g_srv)
+			on_dev += x->device == c->device;
+		full = on_dev >= kMaxServersPerDevice;
+		if (!full)
+			g_srv.push_back(c);
+	}
+	if (full) {
+		burst_release(c);
+		return set_err(-EBUSY,
+			       "cgck_burst_open: %u burst servers already resident on device %d (each holds a hardware "
+			       "queue of its own, and a device maps only ~20 at once: beyond 16, servers' workgroups "
+			       "stall for ms to s, tools/txloop workers mode); bind the workers over more devices "
+			       "(cgck_thread_bind) or leave this one without",
+			       on_dev, c->device);
 	}
 	return burst_launch(c, 0);
 }
@@ -1327,6 +1416,12 @@ extern "C" int cgck_test_burst_seq(cgck_ctx_t *c, uint32_t seq)
 	for (uint32_t j = 0; j < kBurstMaxWG; j++)
 		__atomic_store_n(&c->bbox->done[j], seq, __ATOMIC_RELEASE);
 	c->bbox->req[0] = c->bbox->req[1] = 0;
+	c->breq[0] = c->breq[1] = 0;
+	if (c->bdoor) {
+		__atomic_store_n(&c->bdoor[0], 0ull, __ATOMIC_RELAXED);
+		__atomic_store_n(&c->bdoor[1], 0ull, __ATOMIC_RELAXED);
+		__builtin_ia32_sfence();
+	}
 	c->bbox->refused[0] = c->bbox->refused[1] = 0;
 	c->bseq = c->bdone = seq;
 	return burst_launch(c, seq);
@@ -1412,18 +1507,7 @@ extern "C" int cgck_burst_close(cgck_ctx_t *c)
 	(void)hipSetDevice(c->device);
 	__atomic_store_n(&c->bbox->stop, 1u, __ATOMIC_RELEASE);
 	hipError_t e = hipStreamSynchronize(c->bstream); // the server sees `stop` within one poll
-	(void)hipStreamDestroy(c->bstream);
-	(void)hipHostFree(c->bbox);
-	(void)hipHostFree(c->bstage);
-	(void)hipHostFree(c->bresp);
-	(void)hipFree(c->bscratch);
-	(void)hipFree(c->brelay);
-	c->bbox = nullptr;
-	c->bstage = nullptr;
-	c->bstage_cap = 0;
-	c->bresp = nullptr;
-	c->bscratch = nullptr;
-	c->brelay = nullptr;
+	burst_release(c);
 	if (e != hipSuccess)
 		return set_err(-EIO, "cgck_burst_close: %s", hipGetErrorString(e));
 	return 0;

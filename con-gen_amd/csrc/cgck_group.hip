@@ -436,13 +436,14 @@ __device__ __forceinline__ void relay_store(uint64_t *p, uint64_t v)
 	__hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-__global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const uint8_t *req0, uint8_t *scratch,
-							   uint8_t *resp0, uint64_t *dcmd, const void *zero,
-							   uint32_t cap, uint32_t max_pkts, uint32_t per_wg,
-							   uint32_t start_seq, uint32_t epoch, uint32_t opts)
+__global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const uint64_t *door, const uint8_t *req0,
+							   const uint8_t *vblk, uint8_t *scratch, uint8_t *resp0,
+							   uint64_t *dcmd, const void *zero, uint32_t cap,
+							   uint32_t max_pkts, uint32_t per_wg, uint32_t start_seq,
+							   uint32_t epoch, uint32_t opts)
 {
 	// cmd: 1 serve the request, 2 exit, 3 already served by an earlier launch
-	__shared__ uint32_t cmd, cmd_n, cmd_seq;
+	__shared__ uint32_t cmd, cmd_n, cmd_seq, cmd_vram;
 	__shared__ uint4 hdr_w[4];
 	__shared__ uint32_t sdesc[3 * kSliceLds];
 	__shared__ uint4 sblock[kBurstFirst / 16]; // a small request's block (the one-workgroup path)
@@ -470,8 +471,11 @@ __global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const 
 				// cannot post past the one it waits for.
 				const uint32_t want = burst_next(last);
 				while (c == 0) {
-					// relaxed: an acquire load would invalidate the caches every poll
-					const uint64_t r = sys_relaxed64(&box->req[want & 1]);
+					// relaxed: an acquire load would invalidate the caches every poll.
+					// `door` is device memory the host writes through the large
+					// BAR (uncached: every poll reads memory, a local read instead
+					// of a round trip over the fabric), or box->req in host memory
+					const uint64_t r = sys_relaxed64(&door[want & 1]);
 					if (sys_relaxed(&box->stop))
 						c = 2;
 					else if ((uint32_t)r == want)
@@ -486,7 +490,7 @@ __global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const 
 				// from running out)
 				if (K > 1 && c == 2)
 					relay_store(dcmd + 2, (uint64_t)kBurstExit << 32 | epoch);
-				else if (K > 1 && burst_wgs(n, K, per_wg) > 1)
+				else if (K > 1 && burst_wgs(n & ~kBurstVram, K, per_wg) > 1)
 					relay_store(dcmd + (last & 1), (uint64_t)last | (uint64_t)n << 32);
 			} else {
 				// The others poll the leader's relay in device memory, with
@@ -524,17 +528,20 @@ __global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const 
 					c = 3;
 			}
 			cmd = c;
-			cmd_n = n;
+			cmd_n = n & ~kBurstVram;
+			cmd_vram = n & kBurstVram;
 			cmd_seq = last;
 		}
 		__syncthreads();
 		if (cmd == 2)
 			break;
 		const uint32_t n = cmd_n, seq = cmd_seq;
+		const bool vram = cmd_vram != 0 && vblk != nullptr;
 		const uint32_t W = burst_wgs(n, K, per_wg);
+		const uint64_t nraw = (uint64_t)(n | (vram ? kBurstVram : 0u)) << 32; // the relayed count keeps the flag
 		if (j >= W || cmd == 3) {
 			if (t == 0 && j == 0 && K > 1 && W == 1)
-				relay_store(dcmd + (seq & 1), (uint64_t)seq | (uint64_t)n << 32);
+				relay_store(dcmd + (seq & 1), (uint64_t)seq | nraw);
 			// a workgroup outside the request's W keeps its done word within
 			// kDoneLag of the seqs (done_refresh); the host reads done[j]
 			// only for j < W of the request it waits for
@@ -549,7 +556,7 @@ __global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const 
 		if ((opts & 512) && j > 0)
 			for (const uint64_t d0 = __builtin_amdgcn_s_memrealtime(); __builtin_amdgcn_s_memrealtime() - d0 < 2000;)
 				__builtin_amdgcn_s_sleep(8);
-		const uint8_t *req = req0 + (size_t)(seq & 1) * cap;
+		const uint8_t *req = vram ? vblk + (size_t)(seq & 1) * kBurstFirst : req0 + (size_t)(seq & 1) * cap;
 		uint8_t *resp = resp0 + (size_t)(seq & 1) * rslot;
 		const uint4 *src = reinterpret_cast<const uint4 *>(req);
 		uint4 *dst = reinterpret_cast<uint4 *>(scratch);
@@ -595,7 +602,7 @@ __global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const 
 			sblock[t] = v0;
 			sblock[256 + t] = v1;
 			__syncthreads();
-			ok = burst_hdr_ok(h, n, max_pkts, cap);
+			ok = burst_hdr_ok(h, n, max_pkts, vram ? kBurstFirst : cap);
 			// (lab opts bit 4096: the scratch copy for every block, the A/B)
 			const bool in_lds = !ok || (h.bytes <= kBurstFirst && !(opts & 4096));
 			const uint32_t *sd;
@@ -677,7 +684,9 @@ __global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const 
 			// wait for the header.
 			const uint32_t lo = (uint32_t)((uint64_t)n * j / W), hi = (uint32_t)((uint64_t)n * (j + 1) / W);
 			const uint32_t *sd = reinterpret_cast<const uint32_t *>(req + sizeof(BurstReq));
-			ok = n <= max_pkts;
+			// (a device-memory block holds at most kBurstFirst bytes: no
+			// descriptor read past it, whatever the mailbox word says)
+			ok = n <= max_pkts && (!vram || sizeof(BurstReq) + 12ull * n <= kBurstFirst);
 			for (uint32_t c0 = lo; ok && c0 < hi; c0 += kSliceLds) {
 				const uint32_t c1 = hi - c0 < kSliceLds ? hi : c0 + kSliceLds;
 				const uint32_t nd = 3 * (c1 - c0);
@@ -695,7 +704,7 @@ __global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const 
 				if (c0 == lo && t < 4)
 					hdr_w[t] = hv;
 				__syncthreads();
-				ok = burst_hdr_ok(h, n, max_pkts, cap);
+				ok = burst_hdr_ok(h, n, max_pkts, vram ? kBurstFirst : cap);
 				if (ok) {
 					const uint64_t limit = burst_limit(h);
 					for (uint32_t i = t; i < c1 - c0; i += 256)
@@ -754,22 +763,23 @@ __global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const 
 			else
 				__hip_atomic_store(&box->done[j], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 			if (j == 0 && K > 1 && W == 1)
-				relay_store(dcmd + (seq & 1), (uint64_t)seq | (uint64_t)n << 32);
+				relay_store(dcmd + (seq & 1), (uint64_t)seq | nraw);
 		}
 	}
 	if (t == 0)
 		__hip_atomic_store(&box->alive[j], (uint8_t)0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-hipError_t launch_burst_server(BurstBox *box, const uint8_t *req, uint8_t *scratch, uint8_t *resp, uint64_t *dcmd,
-			       const void *zero, uint32_t cap, uint32_t max_pkts, uint32_t wgs, uint32_t per_wg,
-			       uint32_t start_seq, uint32_t epoch, uint32_t opts, hipStream_t st)
+hipError_t launch_burst_server(BurstBox *box, const uint64_t *door, const uint8_t *req, const uint8_t *vblk,
+			       uint8_t *scratch, uint8_t *resp, uint64_t *dcmd, const void *zero, uint32_t cap,
+			       uint32_t max_pkts, uint32_t wgs, uint32_t per_wg, uint32_t start_seq, uint32_t epoch,
+			       uint32_t opts, hipStream_t st)
 {
 	hipError_t e = hipMemsetAsync(dcmd, 0, 3 * sizeof(uint64_t), st);
 	if (e != hipSuccess)
 		return e;
-	hipLaunchKernelGGL(burst_server_kernel, dim3(wgs), dim3(256), 0, st, box, req, scratch, resp, dcmd, zero, cap,
-			   max_pkts, per_wg, start_seq, epoch, opts);
+	hipLaunchKernelGGL(burst_server_kernel, dim3(wgs), dim3(256), 0, st, box, door, req, vblk, scratch, resp, dcmd,
+			   zero, cap, max_pkts, per_wg, start_seq, epoch, opts);
 	return hipGetLastError();
 }
 

@@ -76,6 +76,13 @@ struct cgck_ctx {
 	uint32_t bdone;             // the last request known complete (a relaunch serves the ones after it)
 	cgck::BurstPending *bslot[2]; // a posted request not yet collected, per slot
 	uint32_t bbusy;             // the owner thread is inside a request (MapGuard, cgck_api.cpp)
+	// device memory the host writes through the large BAR (nullptr: none, the
+	// mailbox words are bbox->req): the two mailbox words the leader polls,
+	// then two kBurstFirst request slots for small blocks
+	uint64_t *bdoor;
+	uint8_t *bvblk;
+	bool bnext_vram;            // the block burst_slot_free handed out is a bvblk slot
+	uint64_t breq[2];           // the last mailbox word posted per slot (host copy)
 	hipStream_t bstream; // the server's own stream (it stays resident)
 };
 
