@@ -368,7 +368,7 @@ def bench_burst():
     return [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
 
 
-def run_pinned(cmd, timeout):
+def run_pinned(cmd, timeout, env=None):
     """A host harness as a child process pinned to one core (the middle CPU
     of this process's set, as cpu_burst pins the reference): the windows'
     per-burst cost is mostly misses on GPU-written lines, and unpinned runs
@@ -379,7 +379,8 @@ def run_pinned(cmd, timeout):
     old = set(cpus)
     try:
         os.sched_setaffinity(0, {cpus[len(cpus) // 2]})  # the child inherits it
-        return subprocess.run(cmd, capture_output=True, text=True, timeout=timeout)
+        return subprocess.run(cmd, capture_output=True, text=True, timeout=timeout,
+                              env=dict(os.environ, **env) if env else None)
     finally:
         os.sched_setaffinity(0, old)
 
@@ -394,10 +395,39 @@ def bench_loop():
     exe = os.path.join(ROOT, "tools", "txloop")
     if not os.path.exists(exe):
         return None
-    r = run_pinned([exe, "0.1"], 300)
+    # mixes: verify only, replies in transmit slots, replies in the stack-local
+    # packet (a full transmit ring: the synchronous calls)
+    r = run_pinned([exe, "0.1"], 300, env={"TXLOOP_MIXES": "0,1,2"})
     if r.returncode != 0:
         return {"error": r.stderr.strip()[-300:]}
     return [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+
+
+WORKERS = "1,4,16"   # worker threads on this GPU, each with its own pool, context and burst server
+
+
+def bench_workers():
+    """con-gen's N-worker mode (con-gen.c:1062-1100) at the checksum
+    boundary: tools/txloop's workers mode, each thread pinned to its own CPU
+    with its own registered pool, context and burst server, 64-frame bursts,
+    replies, 250 ns of stack work a frame, all threads in the same cell at
+    once.  Host-resident: never `value`.  Returns per (N, form) the
+    per-thread us per burst (median / p90 / max over the threads)."""
+    exe = os.path.join(ROOT, "tools", "txloop")
+    if not os.path.exists(exe):
+        return None
+    import subprocess
+    env = dict(os.environ, TXLOOP_WORKERS=WORKERS)
+    r = subprocess.run([exe, "0.1"], capture_output=True, text=True, timeout=300, env=env)
+    if r.returncode != 0:
+        return {"error": r.stderr.strip()[-300:]}
+    rows = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    return {"what": "per-thread us of the checksum path per 64 x 64 B burst with replies, 250 ns/frame of "
+                    "stack work, N workers on one GPU each with its own ring, context and burst server "
+                    "(tools/txloop workers mode)",
+            "rows": [{k: x.get(k) for k in ("workers", "form", "us_per_burst", "us_iter_p90", "us_latency",
+                                            "servers", "exact", "error") if k in x} for x in rows],
+            "exact": all(x.get("exact") for x in rows)}
 
 
 LOOP_FORMS = ("reference", "pipelined", "coalesced", "sync")
@@ -801,10 +831,11 @@ def main():
                            "pci_bus": torch.cuda.get_device_properties(dev).pci_bus_id
                            if hasattr(torch.cuda.get_device_properties(dev), "pci_bus_id") else None})
 
-    burst = loop = None
+    burst = loop = workers = None
     if dist.rank == 0 and dist.world == 1 and not args.no_burst and args.only is None:
         burst = bench_burst()
         loop = bench_loop()
+        workers = bench_workers()
     cpu = cpu_r = cpu_64 = cpu_b = None
     if dist.rank == 0 and dist.world == 1 and not args.no_cpu:
         if burst:
@@ -907,7 +938,7 @@ def main():
                               "cols": BURST_COLS, "rows": burst_summary(burst, cpu_b),
                               "crossover_burst": burst_crossover(burst, cpu_b),
                               "all_rows": path and "gpurun_out/bench_burst.json",
-                              "loop": loop_summary(loop)}
+                              "loop": loop_summary(loop), "workers": workers}
         if extra:
             out["extra"] = extra
         if "value" not in out:   # --only 64 / imix / rss profiling runs

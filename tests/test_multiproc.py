@@ -197,3 +197,26 @@ def test_gpus_2_starts_two_ranks_on_cpu():
     assert r.stderr.count("bench.py: launching") == 1                # the ranks did not re-spawn
     assert "no GPU visible" in r.stderr
     assert r.stdout == ""
+
+
+def test_loop_summary_empty_cell_is_no_win():
+    """a txloop cell that processed no burst prints null
+    figures and exact false (tools/txloop.c); the summary lists it, marks the
+    leg inexact, and never counts it as beating the reference."""
+    rows = []
+    for b in (64, 256, 2048):
+        for f in bench.LOOP_FORMS:
+            v = {"reference": 10.0, "pipelined": 8.0, "coalesced": 7.0, "sync": 12.0}[f] * b / 64
+            r = {"mode": "loop", "form": f, "mix": "rx+reply", "pkt_len": 64, "burst": b,
+                 "stack_ns_per_frame": 0, "stack_us_fixed": 0, "iters": 100, "bursts": 100,
+                 "max_iter_us": 20.0, "us_per_burst": v, "us_worker": v, "us_latency": 30.0, "exact": True}
+            if f == "coalesced" and b == 256:   # the driver's r5 cell: nothing recorded
+                r.update(bursts=0, us_per_burst=None, us_worker=None, us_latency=None, exact=False, iters=0)
+            rows.append(r)
+    s = bench.loop_summary(rows)
+    key = "rx+reply@0ns/frame"
+    assert s["crossover"][key]["coalesced"] == 2048        # the empty 256 cell breaks the run of wins
+    assert s["crossover"][key]["pipelined"] == 64
+    assert s["exact"] is False and len(s["empty_cells"]) == 1 and "/coalesced/256" in s["empty_cells"][0]
+    row256 = [r for r in s["rows"][key] if r[0] == 256][0]
+    assert row256[1 + bench.LOOP_FORMS.index("coalesced")] is None
