@@ -403,6 +403,19 @@ class MapChange {
 static bool burst_all_alive(const cgck_ctx *c);
 static int burst_restart(cgck_ctx *c);
 
+// The stop word the leader polls: beside the device-memory doorbell (written
+// through the large BAR, pushed out of the write-combining buffer) or in the
+// host mailbox.
+static void burst_stop(cgck_ctx *c, uint32_t v)
+{
+	if (c->bdoor) {
+		__builtin_ia32_sfence();
+		__atomic_store_n((uint32_t *)(c->bdoor + 2), v, __ATOMIC_RELAXED);
+		__builtin_ia32_sfence();
+	}
+	__atomic_store_n(&c->bbox->stop, v, __ATOMIC_RELEASE);
+}
+
 // Requests complete in order, so the last one known complete is the latest
 // seq collected, whatever order the posted requests are collected in (the
 // pipelined windows collect a TX fill, then the older RX burst that shares
@@ -466,9 +479,9 @@ static void burst_quiesce_all()
 			continue;
 		(void)hipSetDevice(c->device);
 		burst_finish_posted(c);
-		__atomic_store_n(&c->bbox->stop, 1u, __ATOMIC_RELEASE);
+		burst_stop(c, 1u);
 		(void)hipStreamSynchronize(c->bstream);
-		__atomic_store_n(&c->bbox->stop, 0u, __ATOMIC_RELEASE);
+		burst_stop(c, 0u);
 	}
 }
 
@@ -479,7 +492,8 @@ static int burst_launch(cgck_ctx *c, uint32_t start_seq)
 		;
 	for (uint32_t j = 0; j < c->bwgs; j++)
 		__atomic_store_n(&c->bbox->alive[j], (uint8_t)1, __ATOMIC_RELEASE);
-	hipError_t e = launch_burst_server(c->bbox_dev, c->bdoor ? c->bdoor : c->bbox_dev->req, c->bstage_dev, c->bvblk,
+	hipError_t e = launch_burst_server(c->bbox_dev, c->bdoor ? c->bdoor : c->bbox_dev->req,
+					   c->bdoor ? (const uint32_t *)(c->bdoor + 2) : &c->bbox_dev->stop, c->bstage_dev, c->bvblk,
 					   c->bscratch, c->bresp_dev, c->brelay, c->d_zero, (uint32_t)c->bstage_cap,
 					   c->bmax, c->bwgs, c->bper, start_seq, epoch, server_opts(), c->bstream);
 	if (e != hipSuccess) {
@@ -504,9 +518,9 @@ static bool burst_all_alive(const cgck_ctx *c)
 static int burst_restart(cgck_ctx *c)
 {
 	(void)hipSetDevice(c->device);
-	__atomic_store_n(&c->bbox->stop, 1u, __ATOMIC_RELEASE);
+	burst_stop(c, 1u);
 	const hipError_t e = hipStreamSynchronize(c->bstream);
-	__atomic_store_n(&c->bbox->stop, 0u, __ATOMIC_RELEASE);
+	burst_stop(c, 0u);
 	if (e != hipSuccess)
 		return set_err(-EIO, "burst server drain: %s", hipGetErrorString(e));
 	return burst_launch(c, c->bdone);
@@ -618,9 +632,9 @@ static int burst_wait(cgck_ctx *c, uint32_t seq, uint32_t n, uint64_t range)
 					at += snprintf(miss + at, sizeof(miss) - at, " %u:%u", k,
 						       __atomic_load_n(&b->done[k], __ATOMIC_ACQUIRE));
 			miss[at] = 0;
-			__atomic_store_n(&b->stop, 1u, __ATOMIC_RELEASE);
+			burst_stop(c, 1u);
 			(void)hipStreamSynchronize(c->bstream);
-			__atomic_store_n(&b->stop, 0u, __ATOMIC_RELEASE);
+			burst_stop(c, 0u);
 			uint64_t relay[3] = {0, 0, 0};
 			(void)hipMemcpy(relay, c->brelay, sizeof(relay), hipMemcpyDeviceToHost);
 			burst_done_at(c, seq); // abandoned: the next launch starts after it
@@ -1242,9 +1256,12 @@ static hipError_t burst_stream(const cgck_ctx *c, hipStream_t *st)
 // every server's queue on every XCD at once — a server's workgroups on one XCD
 // never started (a request not served in 2 s) or waited ms for the
 // scheduler's time slice (tools/txloop workers mode, 16 / 20 / 24 / 28 / 32
-// workers on one MI355X, profiles/r06/).  con-gen's 32 workers bound over a
-// node's eight GPUs hold four each.
-constexpr uint32_t kMaxServersPerDevice = 16;
+// workers on one MI355X, profiles/r06/).  With 16 servers the process's
+// other streams (HIP's shared queues, GPU_MAX_HW_QUEUES = 4) starved in
+// turn: 16 more workers launching their requests recorded no burst in 0.3 s
+// (profiles/r06/doorab/workers.log), so the cap leaves them room.  con-gen's
+// 32 workers bound over a node's eight GPUs hold four each.
+constexpr uint32_t kMaxServersPerDevice = 12;
 
 // The server's stream and memory, freed (no server kernel running).
 static void burst_release(cgck_ctx *c)
@@ -1384,9 +1401,9 @@ extern "C" int cgck_burst_open(cgck_ctx_t *c, uint32_t max_pkts, size_t max_byte
 		burst_release(c);
 		return set_err(-EBUSY,
 			       "cgck_burst_open: %u burst servers already resident on device %d (each holds a hardware "
-			       "queue of its own, and a device maps only ~20 at once: beyond 16, servers' workgroups "
-			       "stall for ms to s, tools/txloop workers mode); bind the workers over more devices "
-			       "(cgck_thread_bind) or leave this one without",
+			       "queue of its own, and a device maps only ~20 at once: beyond that, servers' workgroups "
+			       "and other streams' launches stall for ms to s, tools/txloop workers mode); bind the "
+			       "workers over more devices (cgck_thread_bind) or leave this one without",
 			       on_dev, c->device);
 	}
 	return burst_launch(c, 0);
@@ -1408,9 +1425,9 @@ extern "C" int cgck_test_burst_seq(cgck_ctx_t *c, uint32_t seq)
 	if (seq == 0)
 		return set_err(-EINVAL, "cgck_test_burst_seq: seq 0 is never posted");
 	MapGuard map_g(c);
-	__atomic_store_n(&c->bbox->stop, 1u, __ATOMIC_RELEASE);
+	burst_stop(c, 1u);
 	const hipError_t e = hipStreamSynchronize(c->bstream);
-	__atomic_store_n(&c->bbox->stop, 0u, __ATOMIC_RELEASE);
+	burst_stop(c, 0u);
 	if (e != hipSuccess)
 		return set_err(-EIO, "cgck_test_burst_seq: drain: %s", hipGetErrorString(e));
 	for (uint32_t j = 0; j < kBurstMaxWG; j++)
@@ -1505,7 +1522,7 @@ extern "C" int cgck_burst_close(cgck_ctx_t *c)
 			}
 	}
 	(void)hipSetDevice(c->device);
-	__atomic_store_n(&c->bbox->stop, 1u, __ATOMIC_RELEASE);
+	burst_stop(c, 1u);
 	hipError_t e = hipStreamSynchronize(c->bstream); // the server sees `stop` within one poll
 	burst_release(c);
 	if (e != hipSuccess)

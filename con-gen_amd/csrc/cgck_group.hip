@@ -436,7 +436,8 @@ __device__ __forceinline__ void relay_store(uint64_t *p, uint64_t v)
 	__hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-__global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const uint64_t *door, const uint8_t *req0,
+__global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const uint64_t *door, const uint32_t *stopw,
+							   const uint8_t *req0,
 							   const uint8_t *vblk, uint8_t *scratch, uint8_t *resp0,
 							   uint64_t *dcmd, const void *zero, uint32_t cap,
 							   uint32_t max_pkts, uint32_t per_wg, uint32_t start_seq,
@@ -476,7 +477,11 @@ __global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const 
 					// BAR (uncached: every poll reads memory, a local read instead
 					// of a round trip over the fabric), or box->req in host memory
 					const uint64_t r = sys_relaxed64(&door[want & 1]);
-					if (sys_relaxed(&box->stop))
+					// the stop word beside the mailbox words: with the doorbell in
+					// device memory a poll reads no host line at all (a host read
+					// in the loop set its period to a fabric round trip: the
+					// doorbell's gain lost, profiles/r06/)
+					if (sys_relaxed(stopw))
 						c = 2;
 					else if ((uint32_t)r == want)
 						c = 1, last = want, n = (uint32_t)(r >> 32);
@@ -770,16 +775,16 @@ __global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const 
 		__hip_atomic_store(&box->alive[j], (uint8_t)0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-hipError_t launch_burst_server(BurstBox *box, const uint64_t *door, const uint8_t *req, const uint8_t *vblk,
-			       uint8_t *scratch, uint8_t *resp, uint64_t *dcmd, const void *zero, uint32_t cap,
-			       uint32_t max_pkts, uint32_t wgs, uint32_t per_wg, uint32_t start_seq, uint32_t epoch,
-			       uint32_t opts, hipStream_t st)
+hipError_t launch_burst_server(BurstBox *box, const uint64_t *door, const uint32_t *stopw, const uint8_t *req,
+			       const uint8_t *vblk, uint8_t *scratch, uint8_t *resp, uint64_t *dcmd, const void *zero,
+			       uint32_t cap, uint32_t max_pkts, uint32_t wgs, uint32_t per_wg, uint32_t start_seq,
+			       uint32_t epoch, uint32_t opts, hipStream_t st)
 {
 	hipError_t e = hipMemsetAsync(dcmd, 0, 3 * sizeof(uint64_t), st);
 	if (e != hipSuccess)
 		return e;
-	hipLaunchKernelGGL(burst_server_kernel, dim3(wgs), dim3(256), 0, st, box, door, req, vblk, scratch, resp, dcmd,
-			   zero, cap, max_pkts, per_wg, start_seq, epoch, opts);
+	hipLaunchKernelGGL(burst_server_kernel, dim3(wgs), dim3(256), 0, st, box, door, stopw, req, vblk, scratch, resp,
+			   dcmd, zero, cap, max_pkts, per_wg, start_seq, epoch, opts);
 	return hipGetLastError();
 }
 

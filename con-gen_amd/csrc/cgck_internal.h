@@ -156,14 +156,15 @@ __host__ __device__ constexpr uint32_t burst_resp_slot(uint32_t max_pkts)
 // completed (the server serves burst_next(start_seq) first); epoch: nonzero,
 // new for every launch; opts: lab A/B bits (0 in the product).
 // door: the two mailbox words the leader polls (box->req in host memory, or
-// the device-memory doorbell the host writes through the large BAR); vblk:
+// the device-memory doorbell the host writes through the large BAR); stopw:
+// the stop word it polls with them (box->stop, or beside the doorbell); vblk:
 // the device-memory request slots of small blocks (kBurstFirst bytes each,
 // nullptr: none), used by a request whose mailbox word has kBurstVram set in
 // its count.
-hipError_t launch_burst_server(BurstBox *box, const uint64_t *door, const uint8_t *req, const uint8_t *vblk,
-			       uint8_t *scratch, uint8_t *resp, uint64_t *dcmd, const void *zero, uint32_t cap,
-			       uint32_t max_pkts, uint32_t wgs, uint32_t per_wg, uint32_t start_seq, uint32_t epoch,
-			       uint32_t opts, hipStream_t st);
+hipError_t launch_burst_server(BurstBox *box, const uint64_t *door, const uint32_t *stopw, const uint8_t *req,
+			       const uint8_t *vblk, uint8_t *scratch, uint8_t *resp, uint64_t *dcmd, const void *zero,
+			       uint32_t cap, uint32_t max_pkts, uint32_t wgs, uint32_t per_wg, uint32_t start_seq,
+			       uint32_t epoch, uint32_t opts, hipStream_t st);
 // In the mailbox word's count (bits 32-63): the request's block is in the
 // device-memory slot (vblk) of its parity, not in the host staging.
 constexpr uint32_t kBurstVram = 1u << 31;

@@ -117,7 +117,7 @@ for step in "$@"; do
 			run srvlat_64_fill_vram$i 120 tools/srvlat 64 fill || exit 1
 			CGCK_BURST_HOST_DOOR=1 run srvlat_64_fill_host$i 120 tools/srvlat 64 fill || exit 1
 		done ;;
-	workers4) TXLOOP_WORKERS=1,8,16,32 run workers 600 tools/txloop 0.3 || exit 1 ;;
+	workers4) TXLOOP_WORKERS=1,8,12,16,32 run workers 600 tools/txloop 0.3 || exit 1 ;;
 	vramdb) run vramdb 120 tools/vramdb 0.3 || exit 1 ;;
 	shards) run shards 600 python -u -m pytest tests/test_gpu_shards.py -m gpu -x -v -s --timeout 500 --timeout-method thread || exit 1 ;;
 	prof) bash tools/gpu_prof_layouts.sh $(basename $O)/prof || exit 1 ;;
