@@ -117,6 +117,18 @@ for step in "$@"; do
 			run srvlat_64_fill_vram$i 120 tools/srvlat 64 fill || exit 1
 			CGCK_BURST_HOST_DOOR=1 run srvlat_64_fill_host$i 120 tools/srvlat 64 fill || exit 1
 		done ;;
+	doorab2) # the doorbell A/B after the stop word moved beside it: host mailbox and blocks (HOST_DOOR),
+		# doorbell and small blocks in device memory (default), doorbell alone (VRAM_MAX=0); srvlat and the
+		# loop's small bursts, interleaved, twice
+		for i in 1 2; do
+			for m in host vram door; do
+				case $m in host) E="CGCK_BURST_HOST_DOOR=1";; vram) E="X=1";; door) E="CGCK_BURST_VRAM_MAX=0";; esac
+				env $E timeout -k 10 120 tools/srvlat 64 > $O/srvlat_64_${m}$i.log 2>&1 || exit 1
+				env $E timeout -k 10 120 tools/srvlat 64 fill > $O/srvlat_64_fill_${m}$i.log 2>&1 || exit 1
+				env $E TXLOOP_BURSTS=1,16,64,256 TXLOOP_NS=250 TXLOOP_MIXES=0,1 timeout -k 10 200 tools/txloop_lab 0.15 > $O/txloop_${m}$i.log 2>&1 || exit 1
+				echo "$m $i"; head -1 $O/srvlat_64_${m}$i.log
+			done
+		done ;;
 	workers4) TXLOOP_WORKERS=1,8,12,16,32 run workers 600 tools/txloop 0.3 || exit 1 ;;
 	vramdb) run vramdb 120 tools/vramdb 0.3 || exit 1 ;;
 	shards) run shards 600 python -u -m pytest tests/test_gpu_shards.py -m gpu -x -v -s --timeout 500 --timeout-method thread || exit 1 ;;
