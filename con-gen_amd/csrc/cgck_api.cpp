@@ -730,16 +730,19 @@ int cgck::burst_ready(cgck_ctx *c, const BurstPending *p)
 // (tools/vramdb: 4.70 against 5.55 us for the bare round trip of a 4 KiB
 // block, profiles/r06/).  Larger blocks stay in host staging: the host's
 // write-combined stores cost ~0.13 us a KiB (0.53 us for 4 KiB against 0.06
-// into host memory), which is the worker's time.
+// into host memory), which is the worker's time.  So do the blocks of posted
+// requests (the pipelined / coalesced windows): their latency is hidden
+// behind the stack's work, while the write-combined stores would be the
+// worker's own; only their doorbell goes to device memory.
 static const size_t kBurstVramMax = env_size(CGCK_ENV("CGCK_BURST_VRAM_MAX"), 2048); // lab A/B: the bound
-static int burst_slot_free(cgck_ctx *c, const BurstLayout &L, uint8_t **block)
+static int burst_slot_free(cgck_ctx *c, const BurstLayout &L, uint8_t **block, bool posted = false)
 {
 	const uint32_t seq = burst_next(c->bseq);
 	if (BurstPending *p = c->bslot[seq & 1]) {
 		const int rc = burst_collect(c, p); // its poster reads p->rc
 		(void)rc;
 	}
-	c->bnext_vram = c->bvblk && L.bytes <= kBurstVramMax && L.bytes <= kBurstFirst;
+	c->bnext_vram = c->bvblk && !posted && L.bytes <= kBurstVramMax && L.bytes <= kBurstFirst;
 	*block = c->bnext_vram ? c->bvblk + (size_t)(seq & 1) * kBurstFirst : burst_block(c, seq);
 	return 0;
 }
@@ -887,7 +890,7 @@ static int desc_host_impl(cgck_ctx *c, void *base, size_t bytes, const cgck_desc
 		// the resident server: no launch, no stream sync
 		const BurstLayout L = burst_layout(in_place ? 0 : pkt_bytes, n);
 		uint8_t *h;
-		if ((rc = burst_slot_free(c, L, &h)))
+		if ((rc = burst_slot_free(c, L, &h, pend != nullptr)))
 			return rc;
 		cgck_desc_t *d = (cgck_desc_t *)(h + L.d_off);
 		if (in_place) {

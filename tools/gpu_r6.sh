@@ -129,6 +129,17 @@ for step in "$@"; do
 				echo "$m $i"; head -1 $O/srvlat_64_${m}$i.log
 			done
 		done ;;
+	doorab3) # pinned, interleaved: the host mailbox (HOST_DOOR) against the default (doorbell in device
+		# memory; synchronous requests' small blocks there too, posted ones' in host staging)
+		C=$(python3 -c "import os; c=sorted(os.sched_getaffinity(0)); print(c[len(c)//2])")
+		for i in 1 2 3; do
+			for m in host dflt; do
+				case $m in host) E="CGCK_BURST_HOST_DOOR=1";; dflt) E="X=1";; esac
+				env $E timeout -k 10 120 taskset -c $C tools/srvlat 64 > $O/srvlat_64_${m}$i.log 2>&1 || exit 1
+				env $E TXLOOP_BURSTS=1,16,64,256 TXLOOP_NS=250 TXLOOP_MIXES=0,1 timeout -k 10 200 taskset -c $C tools/txloop_lab 0.15 > $O/txloop_${m}$i.log 2>&1 || exit 1
+				echo "$m $i"; head -1 $O/srvlat_64_${m}$i.log
+			done
+		done ;;
 	workers4) TXLOOP_WORKERS=1,8,12,16,32 run workers 600 tools/txloop 0.3 || exit 1 ;;
 	vramdb) run vramdb 120 tools/vramdb 0.3 || exit 1 ;;
 	shards) run shards 600 python -u -m pytest tests/test_gpu_shards.py -m gpu -x -v -s --timeout 500 --timeout-method thread || exit 1 ;;
