@@ -403,7 +403,7 @@ def bench_loop():
     return [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
 
 
-WORKERS = "1,4,16"   # worker threads on this GPU, each with its own pool, context and burst server
+WORKERS = "1,4,12"   # worker threads on this GPU, each with its own pool, context and burst server (<= 12 a device)
 
 
 def bench_workers():
