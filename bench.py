@@ -396,8 +396,10 @@ def bench_loop():
     if not os.path.exists(exe):
         return None
     # mixes: verify only, replies in transmit slots, replies in the stack-local
-    # packet (a full transmit ring: the synchronous calls)
-    r = run_pinned([exe, "0.1"], 300, env={"TXLOOP_MIXES": "0,1,2"})
+    # packet (a full transmit ring: the synchronous calls),
+    # and the full ring with the pending packets in a registered pool
+    # (queued like ring slots, drained after their fill)
+    r = run_pinned([exe, "0.1"], 300, env={"TXLOOP_MIXES": "0,1,2,3"})
     if r.returncode != 0:
         return {"error": r.stderr.strip()[-300:]}
     return [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]

@@ -109,7 +109,7 @@ for step in "$@"; do
 		TXLOOP_SLEEP=1 TXLOOP_WORKERS=1,16,24,32 run workers_sleep 600 tools/txloop 0.3 || exit 1 ;;
 	txfull) # the full-transmit-ring regime: replies built in the stack-local packet (computed synchronously)
 		C=$(python3 -c "import os; c=sorted(os.sched_getaffinity(0)); print(c[len(c)//2])")
-		TXLOOP_MIXES=1,2 TXLOOP_BURSTS=1,16,64,256 run txloop_full 300 taskset -c $C tools/txloop 0.2 || exit 1 ;;
+		TXLOOP_MIXES=1,2,3 TXLOOP_BURSTS=1,16,64,256 run txloop_full 300 taskset -c $C tools/txloop 0.2 || exit 1 ;;
 	doorab) # the device-memory doorbell and small-block slots against the host-memory mailbox (lab build)
 		for i in 1 2; do
 			run srvlat_64_vram$i 120 tools/srvlat 64 || exit 1
@@ -143,6 +143,7 @@ for step in "$@"; do
 	workers4) TXLOOP_WORKERS=1,8,12,16,32 run workers 600 tools/txloop 0.3 || exit 1 ;;
 	vramdb) run vramdb 120 tools/vramdb 0.3 || exit 1 ;;
 	shards) run shards 600 python -u -m pytest tests/test_gpu_shards.py -m gpu -x -v -s --timeout 500 --timeout-method thread || exit 1 ;;
+	profbench) BENCH_ARGS="--steps 10 --warmup 3 --no-cpu --no-pmc --no-burst" bash tools/gpu_prof.sh || exit 1 ;;
 	prof) bash tools/gpu_prof_layouts.sh $(basename $O)/prof || exit 1 ;;
 	*) echo "unknown step $step"; exit 2 ;;
 	esac

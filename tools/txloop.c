@@ -224,6 +224,22 @@ static int reply_body(const uint8_t *rx, in_fn fin, udp_fn fudp, int i)
 	return bad;
 }
 
+/* mix 3, the full-transmit-ring regime with the integration of INTEGRATION.md
+ * §2: the stack builds the segment in a pending packet taken from a
+ * registered pool (not the stack-local pkt_body), so the TX window queues its
+ * calls as for a ring slot; once the fill covering it has completed, the
+ * transport drains it into the ring (add_pending_packet's copy, subr.c:264-
+ * 286, then the ring copy when a slot frees): modelled as one 54-byte copy a
+ * reply into a ring area, in the worker's time. */
+static __thread int g_pend;
+static __thread uint8_t g_ring[MAXB * 64];
+
+static void drain_pending(const uint8_t *tx0, long first, long cnt)
+{
+	for (long i = 0; i < cnt; i++)
+		memcpy(g_ring + (size_t)(i % MAXB) * 64, tx0 + (size_t)((first + i) % (2 * MAXB)) * SLOT, L3 + 40);
+}
+
 /* the coalesced form's posted fills: their first reply slot and count */
 struct fills {
 	long start[64], cnt[64], nrep[64];
@@ -251,6 +267,8 @@ static int fill_done(struct fills *f, int mix, const uint8_t *tx0, struct cell *
 	if (done < 0)
 		return done;
 	const long cnt = f->cnt[f->h], nrep = f->nrep[f->h];
+	if (g_pend && nrep > 0)
+		drain_pending(tx0, f->start[f->h], nrep);
 	if (mix && nrep > 0) {
 		c->bad_tx += done != 2 * nrep;
 		c->bad_tx += check_replies(tx0 + (size_t)(f->start[f->h] % (2 * MAXB)) * SLOT, 1);
@@ -339,7 +357,8 @@ static int run_cell(struct wk *W, int form, int mix, int R, double ns, double fi
 	/* mix 2: the replies go to the stack-local struct packet (a full
 	 * transmit ring), mix 1 to transmit slots; below, `mix` is the latter */
 	const int body = mix == 2;
-	mix = body ? 0 : mix;
+	g_pend = mix == 3; /* replies in registered pending packets, drained after their fill */
+	mix = body ? 0 : g_pend ? 1 : mix;
 	c.it = c.itl = c.bad_rx = c.bad_tx = c.bad_tx_checked = 0;
 	c.total = 0;
 	c.bursts = 0;
@@ -366,6 +385,8 @@ static int run_cell(struct wk *W, int form, int mix, int R, double ns, double fi
 					c.bad_tx += reply_body(ip, ref_in, ref_udp, i);
 				if (mix)
 					reply(tx + (size_t)i * SLOT + L3, ip, ref_in, ref_udp);
+				if (g_pend)
+					drain_pending(tx, i, 1);
 			}
 			lat = now() - a;
 		} else if (form == 1) {
@@ -374,6 +395,8 @@ static int run_cell(struct wk *W, int form, int mix, int R, double ns, double fi
 			w += now() - w0;
 			if (done < 0)
 				return -1;
+			if (g_pend && k > 0 && done == 2 * R)
+				drain_pending(txh[(k + 1) & 1], 0, R);
 			if (mix && k > 0 && done == 2 * R) {
 				c.bad_tx += check_replies(txh[(k + 1) & 1], R);
 				c.bad_tx_checked++;
@@ -490,6 +513,8 @@ static int run_cell(struct wk *W, int form, int mix, int R, double ns, double fi
 			const double w0 = now();
 			if (cgck_tx_flush() != (mix ? 2 * R : 0))
 				return -1;
+			if (g_pend)
+				drain_pending(tx, 0, R);
 			w += now() - w0;
 			if (mix) {
 				c.bad_tx += check_replies(tx, R);
@@ -904,25 +929,32 @@ int main(int argc, char **argv)
 	}
 	static const char *forms[4] = {"reference", "pipelined", "sync", "coalesced"};
 	/* TXLOOP_MIXES: 0 rx, 1 rx + replies in transmit slots, 2 rx + replies
-	 * in the stack-local packet (a full transmit ring); default 0,1 */
-	int mixes[3] = {0, 1, 2}, nmix = 2;
+	 * in the stack-local packet (a full transmit ring), 3 the same regime
+	 * with the pending packets in a registered pool (drained into the ring
+	 * after their fill completes); default 0,1 */
+	int mixes[4] = {0, 1, 2, 3}, nmix = 2;
 	if (getenv("TXLOOP_MIXES")) {
 		nmix = 0;
-		for (char *e = getenv("TXLOOP_MIXES"); *e && nmix < 3;) {
+		for (char *e = getenv("TXLOOP_MIXES"); *e && nmix < 4;) {
 			const int v = (int)strtol(e, &e, 10);
-			if (v >= 0 && v <= 2)
+			if (v >= 0 && v <= 3)
 				mixes[nmix++] = v;
 			while (*e == ',')
 				e++;
 		}
 	}
-	static const char *mixname[3] = {"rx", "rx+reply", "rx+reply(full ring)"};
+	static const char *mixname[4] = {"rx", "rx+reply", "rx+reply(full ring)", "rx+reply(full ring, registered pending)"};
 	for (int mi = 0; mi < nmix; mi++) {
 		const int mix = mixes[mi];
 		for (int bud = 0; bud <= nns; bud++) {
 			const double ns = bud < nns ? nsl[bud] : 0, fixed_us = bud < nns ? 0 : 50;
 			for (int bi = 0; bi < nb; bi++) {
 				const int R = bursts[bi];
+				/* the full-ring mix pays two synchronous requests a reply
+				 * (~12 us): 2048 frames take ~25 ms an iteration, too long
+				 * for a cell's budget and its 20 unrecorded iterations */
+				if (mix == 2 && R > 256)
+					continue;
 				for (int form = 0; form < 4; form++) {
 					if (run_cell(&W0, form, mix, R, ns, fixed_us, budget, &c) < 0)
 						goto fail;
