@@ -1337,12 +1337,16 @@ extern "C" int cgck_burst_open(cgck_ctx_t *c, uint32_t max_pkts, size_t max_byte
 	int large_bar = 0;
 	if (e == hipSuccess && !CGCK_ENV("CGCK_BURST_HOST_DOOR") &&
 	    hipDeviceGetAttribute(&large_bar, hipDeviceAttributeIsLargeBar, c->device) == hipSuccess && large_bar) {
-		if (hipExtMallocWithFlags(&vd, 64 + 2 * (size_t)kBurstFirst, hipDeviceMallocUncached) != hipSuccess ||
-		    hipMemset(vd, 0, 64 + 2 * (size_t)kBurstFirst) != hipSuccess) {
+		if (hipExtMallocWithFlags(&vd, 64 + 2 * (size_t)kBurstFirst, hipDeviceMallocUncached) != hipSuccess) {
 			(void)hipGetLastError();
-			if (vd)
-				(void)hipFree(vd);
 			vd = nullptr; // the host-memory mailbox then
+		} else {
+			// zeroed by the host itself: a hipMemset is asynchronous to the
+			// host, and one still in flight when the first request's doorbell
+			// was written wiped it (request 1 never served:
+			// profiles/r06/bench_r6g)
+			memset(vd, 0, 64 + 2 * (size_t)kBurstFirst);
+			__builtin_ia32_sfence();
 		}
 	}
 	if (e == hipSuccess)
