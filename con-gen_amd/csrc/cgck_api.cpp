@@ -613,6 +613,23 @@ static int burst_wait(cgck_ctx *c, uint32_t seq, uint32_t n, uint64_t range)
 		__builtin_ia32_pause();
 		if ((++spin & 1023) != 0)
 			continue;
+#if CGCK_LAB
+		// lab: a wait past 20 ms says what the server looked like (the
+		// driver's bench once saw one loop iteration take the server's
+		// 200 ms idle bound)
+		if (now_s() - t0 > 0.02 && !(spin & ((1u << 20) - 1))) {
+			char dw[200];
+			int at = 0;
+			for (uint32_t k = 0; k < c->bwgs && at < (int)sizeof(dw) - 16; k++)
+				at += snprintf(dw + at, sizeof(dw) - at, " %u:%u%s", k, __atomic_load_n(&b->done[k], __ATOMIC_ACQUIRE),
+					       __atomic_load_n(&b->alive[k], __ATOMIC_ACQUIRE) ? "" : "x");
+			fprintf(stderr,
+				"cgck lab: wait %.1f ms for seq %u (n %u, W %u): bseq %u bdone %u breq %#llx %#llx "
+				"slots %p %p done/alive%s\n",
+				(now_s() - t0) * 1e3, seq, n, W, c->bseq, c->bdone, (unsigned long long)c->breq[0],
+				(unsigned long long)c->breq[1], (void *)c->bslot[0], (void *)c->bslot[1], dw);
+		}
+#endif
 		if (!burst_all_alive(c)) {
 			// a workgroup exited between the post and its last poll: drain
 			// and relaunch for the pending requests (slices already served

@@ -140,6 +140,11 @@ for step in "$@"; do
 				echo "$m $i"; head -1 $O/srvlat_64_${m}$i.log
 			done
 		done ;;
+	stall) # repro of the 200 ms loop stall (rx+reply, 0 ns, 256 frames, coalesced after sync), lab then product
+		C=$(python3 -c "import os; c=sorted(os.sched_getaffinity(0)); print(c[len(c)//2])")
+		TXLOOP_MIXES=1 TXLOOP_NS=0 TXLOOP_BURSTS=64,256 TXLOOP_REPEAT=12 timeout -k 10 280 taskset -c $C tools/txloop_lab 0.1 > $O/stall_lab.log 2> $O/stall_lab.err || exit 1
+		TXLOOP_MIXES=1 TXLOOP_NS=0 TXLOOP_BURSTS=64,256 TXLOOP_REPEAT=12 timeout -k 10 280 taskset -c $C tools/txloop 0.1 > $O/stall.log 2> $O/stall.err || exit 1
+		grep -c slow $O/stall_lab.err $O/stall.err || true ;;
 	workers4) TXLOOP_WORKERS=1,8,12,16,32 run workers 600 tools/txloop 0.3 || exit 1 ;;
 	vramdb) run vramdb 120 tools/vramdb 0.3 || exit 1 ;;
 	shards) run shards 600 python -u -m pytest tests/test_gpu_shards.py -m gpu -x -v -s --timeout 500 --timeout-method thread || exit 1 ;;

@@ -368,6 +368,8 @@ static int run_cell(struct wk *W, int form, int mix, int R, double ns, double fi
 	long copened = 0; /* coalesced form: bursts opened */
 	struct fills cf;
 	memset(&cf, 0, sizeof(cf));
+	double ph[8] = {0};
+	int nopen = 0;
 	const double t0 = now();
 	while (c.it < MAXIT && now() - t0 < budget) {
 		const int rec = k >= 20;
@@ -434,15 +436,19 @@ static int run_cell(struct wk *W, int form, int mix, int R, double ns, double fi
 			 * cursor over both transmit halves; a fill's
 			 * slots are reused only after it completed. */
 			double w0 = now();
+			ph[0] = w0;
 			while (cf.n > 0 && (cgck_tx_ready() == 1 || cf.n >= 48)) {
 				if (fill_done(&cf, mix, txh[0], &c) < 0)
 					return -1;
 			}
 			w += now() - w0;
+			ph[1] = now();
 			cgck_tx_begin();
 			tpost[k % 64] = now();
 			if (cgck_rx_post(pool, pool_bytes, descs[k & 1], R) != R)
 				return -1;
+			ph[2] = now();
+			nopen = 0;
 			int got = 0;
 			long cur = 0; /* this iteration's reply slots */
 			const long at = cf.cursor % (2 * MAXB);
@@ -460,6 +466,8 @@ static int run_cell(struct wk *W, int form, int mix, int R, double ns, double fi
 				if (cgck_rx_begin_posted() != R)
 					return -1;
 				w += now() - w0;
+				if (nopen < 4)
+					ph[3 + nopen++] = now() - w0;
 				uint8_t *rx = rxh[copened & 1];
 				for (int i = 0; i < R; i++) {
 					uint8_t *ip = rx + (size_t)i * SLOT + L3;
@@ -507,8 +515,15 @@ static int run_cell(struct wk *W, int form, int mix, int R, double ns, double fi
 		spin(other);
 		const double spun = now() - a_spin;
 		if (form == 1 || form == 3) {
+			const double tp0 = now();
 			if (cgck_tx_post() < 0)
 				return -1;
+			if (form == 3 && now() - a > 0.02) /* a slow iteration: where its time went */
+				fprintf(stderr,
+					"txloop: slow iteration %d (%.1f ms): fills %.3f, rx_post %.3f, opens %d (%.3f %.3f %.3f "
+					"%.3f), tx_post %.3f ms; fills out %d\n",
+					k, (now() - a) * 1e3, (ph[1] - ph[0]) * 1e3, (ph[2] - ph[1]) * 1e3, nopen, ph[3] * 1e3,
+					ph[4] * 1e3, ph[5] * 1e3, ph[6] * 1e3, (now() - tp0) * 1e3, cf.n);
 		} else if (form == 2) {
 			const double w0 = now();
 			if (cgck_tx_flush() != (mix ? 2 * R : 0))
@@ -943,6 +958,20 @@ int main(int argc, char **argv)
 				e++;
 		}
 	}
+	/* TXLOOP_FORMS (0 reference, 1 pipelined, 2 sync, 3 coalesced; default all)
+	 * and TXLOOP_REPEAT (each cell that many times): a repro harness */
+	int formlist[4] = {0, 1, 2, 3}, nforms = 4;
+	if (getenv("TXLOOP_FORMS")) {
+		nforms = 0;
+		for (char *e = getenv("TXLOOP_FORMS"); *e && nforms < 4;) {
+			const int v = (int)strtol(e, &e, 10);
+			if (v >= 0 && v <= 3)
+				formlist[nforms++] = v;
+			while (*e == ',')
+				e++;
+		}
+	}
+	const int nrep = getenv("TXLOOP_REPEAT") && atoi(getenv("TXLOOP_REPEAT")) > 0 ? atoi(getenv("TXLOOP_REPEAT")) : 1;
 	static const char *mixname[4] = {"rx", "rx+reply", "rx+reply(full ring)", "rx+reply(full ring, registered pending)"};
 	for (int mi = 0; mi < nmix; mi++) {
 		const int mix = mixes[mi];
@@ -955,7 +984,8 @@ int main(int argc, char **argv)
 				 * for a cell's budget and its 20 unrecorded iterations */
 				if (mix == 2 && R > 256)
 					continue;
-				for (int form = 0; form < 4; form++) {
+				for (int fi = 0; fi < nforms * nrep; fi++) {
+					const int form = formlist[fi % nforms];
 					if (run_cell(&W0, form, mix, R, ns, fixed_us, budget, &c) < 0)
 						goto fail;
 					const int n = c.it;
