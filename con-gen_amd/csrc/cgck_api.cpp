@@ -177,7 +177,7 @@ extern "C" int cgck_ctx_destroy(cgck_ctx_t *c)
 	(void)hipSetDevice(c->device);
 	if (c->bbox)
 		(void)cgck_burst_close(c);
-	(void)hipStreamSynchronize(c->stream);
+	(void)CGCK_SYNC(c->stream);
 	(void)hipStreamDestroy(c->stream);
 	if (c->h_stage)
 		(void)hipHostFree(c->h_stage);
@@ -208,7 +208,7 @@ extern "C" int cgck_ctx_sync(cgck_ctx_t *c)
 {
 	if (!c)
 		return set_err(-EINVAL, "cgck_ctx_sync: NULL context");
-	HIP_TRY(hipStreamSynchronize(c->stream));
+	HIP_TRY(CGCK_SYNC(c->stream));
 	return 0;
 }
 
@@ -309,6 +309,17 @@ static double now_s()
 	clock_gettime(CLOCK_MONOTONIC, &ts);
 	return ts.tv_sec + ts.tv_nsec * 1e-9;
 }
+
+#if CGCK_LAB
+hipError_t cgck::lab_sync(const char *where, hipStream_t st)
+{
+	const double t0 = now_s();
+	const hipError_t e = hipStreamSynchronize(st);
+	if (now_s() - t0 > 0.02)
+		fprintf(stderr, "cgck lab: hipStreamSynchronize at %s took %.1f ms\n", where, (now_s() - t0) * 1e3);
+	return e;
+}
+#endif
 
 // (Re)launch the server's K workgroups; the first request each serves is
 // the one after start_seq.
@@ -480,7 +491,7 @@ static void burst_quiesce_all()
 		(void)hipSetDevice(c->device);
 		burst_finish_posted(c);
 		burst_stop(c, 1u);
-		(void)hipStreamSynchronize(c->bstream);
+		(void)CGCK_SYNC(c->bstream);
 		burst_stop(c, 0u);
 	}
 }
@@ -519,7 +530,7 @@ static int burst_restart(cgck_ctx *c)
 {
 	(void)hipSetDevice(c->device);
 	burst_stop(c, 1u);
-	const hipError_t e = hipStreamSynchronize(c->bstream);
+	const hipError_t e = CGCK_SYNC(c->bstream);
 	burst_stop(c, 0u);
 	if (e != hipSuccess)
 		return set_err(-EIO, "burst server drain: %s", hipGetErrorString(e));
@@ -650,7 +661,7 @@ static int burst_wait(cgck_ctx *c, uint32_t seq, uint32_t n, uint64_t range)
 						       __atomic_load_n(&b->done[k], __ATOMIC_ACQUIRE));
 			miss[at] = 0;
 			burst_stop(c, 1u);
-			(void)hipStreamSynchronize(c->bstream);
+			(void)CGCK_SYNC(c->bstream);
 			burst_stop(c, 0u);
 			uint64_t relay[3] = {0, 0, 0};
 			(void)hipMemcpy(relay, c->brelay, sizeof(relay), hipMemcpyDeviceToHost);
@@ -981,7 +992,7 @@ static int desc_host_impl(cgck_ctx *c, void *base, size_t bytes, const cgck_desc
 		KParams p = {dev_base ? (const uint8_t *)dev_base : h, d, n, 0, 0, 0, flags, o, v, nullptr, 0, nullptr, m};
 		if ((rc = run(c, p, hint, st)))
 			return rc;
-		HIP_TRY(hipStreamSynchronize(st));
+		HIP_TRY(CGCK_SYNC(st));
 		if (out)
 			memcpy(out, o, 4 * n);
 		if (meta)
@@ -1025,7 +1036,7 @@ static int desc_host_impl(cgck_ctx *c, void *base, size_t bytes, const cgck_desc
 		back = c->h_stage;
 		HIP_TRY(hipMemcpyAsync(back, c->d_bytes, bytes, hipMemcpyDeviceToHost, st));
 	}
-	HIP_TRY(hipStreamSynchronize(st));
+	HIP_TRY(CGCK_SYNC(st));
 	if (back)
 		for (uint64_t i = 0; i < n; i++) {
 			const size_t o = desc[i].frame_off + desc[i].l3_off;
@@ -1246,7 +1257,7 @@ int cgck::one_region(cgck_ctx *c, const void *src, uint32_t span, uint32_t ip_le
 	KParams p = {c->h_stage, nullptr, 1, 0, 0, ip_len, flags | kFlagGroup, c->h_out, nullptr, nullptr, 0, nullptr};
 	if ((rc = run(c, p, ip_len, c->stream)))
 		return rc;
-	HIP_TRY(hipStreamSynchronize(c->stream));
+	HIP_TRY(CGCK_SYNC(c->stream));
 	*out = c->h_out[0];
 	return 0;
 }
@@ -1450,7 +1461,7 @@ extern "C" int cgck_test_burst_seq(cgck_ctx_t *c, uint32_t seq)
 		return set_err(-EINVAL, "cgck_test_burst_seq: seq 0 is never posted");
 	MapGuard map_g(c);
 	burst_stop(c, 1u);
-	const hipError_t e = hipStreamSynchronize(c->bstream);
+	const hipError_t e = CGCK_SYNC(c->bstream);
 	burst_stop(c, 0u);
 	if (e != hipSuccess)
 		return set_err(-EIO, "cgck_test_burst_seq: drain: %s", hipGetErrorString(e));
@@ -1547,7 +1558,7 @@ extern "C" int cgck_burst_close(cgck_ctx_t *c)
 	}
 	(void)hipSetDevice(c->device);
 	burst_stop(c, 1u);
-	hipError_t e = hipStreamSynchronize(c->bstream); // the server sees `stop` within one poll
+	hipError_t e = CGCK_SYNC(c->bstream); // the server sees `stop` within one poll
 	burst_release(c);
 	if (e != hipSuccess)
 		return set_err(-EIO, "cgck_burst_close: %s", hipGetErrorString(e));
@@ -1668,7 +1679,7 @@ int cgck::rss_prepare(cgck_ctx *c, const uint8_t *key, int key_size, uint32_t cn
 	c->rss_key_len = klen;
 	rss_tables(key, key_size, tcnt, c->h_rss_tab);
 	HIP_TRY(hipMemcpyAsync(c->d_rss_tab, c->h_rss_tab, tbytes, hipMemcpyHostToDevice, st));
-	HIP_TRY(hipStreamSynchronize(st)); // h_rss_tab is pageable and reused
+	HIP_TRY(CGCK_SYNC(st)); // h_rss_tab is pageable and reused
 	c->rss_cnt = tcnt;
 	c->rss_valid = true;
 	return 0;
@@ -1778,7 +1789,7 @@ extern "C" int cgck_dst_cache_host(cgck_ctx_t *c, const cgck_dst_params_t *prm, 
 	// count, then the control words (timeout flag) when the launch ran
 	HIP_TRY(hipMemcpyAsync(c->h_out, d_count, 4, hipMemcpyDeviceToHost, c->stream));
 	HIP_TRY(hipMemcpyAsync(c->h_out + 1, c->d_dst, 16, hipMemcpyDeviceToHost, c->stream));
-	HIP_TRY(hipStreamSynchronize(c->stream));
+	HIP_TRY(CGCK_SYNC(c->stream));
 	if (c->h_out[1 + 2])
 		return set_err(-ETIMEDOUT, "cgck_dst_cache: look-back spin limit reached");
 	const uint32_t got = c->h_out[0];

@@ -1401,7 +1401,7 @@ int tx_build(cgck_ctx *c, TxFill &f, PostItem &x)
 	KParams p = {h, d, n, 0, 0, 0, x.flags, o, nullptr, nullptr, 0, nullptr};
 	if ((rc = run(c, p, 1500, c->stream)))
 		return rc;
-	HIP_TRY(hipStreamSynchronize(c->stream));
+	HIP_TRY(CGCK_SYNC(c->stream));
 	x.vals.assign(o, o + n);
 	x.d.clear();
 	x.n = 0;
@@ -1548,7 +1548,15 @@ extern "C" int cgck_tx_post(void)
 		return -ENODEV;
 	TxFill &f = t.txf[q.next_slot()];
 	PostItem &x = q.push();
+#if CGCK_LAB
+	struct timespec lt[5];
+	clock_gettime(CLOCK_MONOTONIC, &lt[0]);
+#define LAB_TP(i) clock_gettime(CLOCK_MONOTONIC, &lt[i])
+#else
+#define LAB_TP(i) ((void)0)
+#endif
 	int rc = tx_take(t, f, x);
+	LAB_TP(1);
 	if (rc == 0) {
 		x.own = true; // nothing queued: complete as it stands
 	} else if (!f.fast && (rc = tx_build(c, f, x)) < 0) {
@@ -1557,8 +1565,19 @@ extern "C" int cgck_tx_post(void)
 		f.q.clear();
 		return rc;
 	}
+	LAB_TP(2);
 	t.post.pump(c, kTx, false);
+	LAB_TP(3);
 	t.post.bound(c, kTx);
+	LAB_TP(4);
+#if CGCK_LAB
+	auto ms = [&](int i) { return (lt[i].tv_sec - lt[i - 1].tv_sec) * 1e3 + (lt[i].tv_nsec - lt[i - 1].tv_nsec) * 1e-6; };
+	if (ms(1) + ms(2) + ms(3) + ms(4) > 20)
+		fprintf(stderr, "cgck lab: tx_post %.1f ms: take %.3f build %.3f (fast %d, own %d, n %llu) pump %.3f bound %.3f\n",
+			ms(1) + ms(2) + ms(3) + ms(4), ms(1), ms(2), (int)f.fast, (int)x.own, (unsigned long long)x.n, ms(3),
+			ms(4));
+#endif
+#undef LAB_TP
 	if (old_rc < 0)
 		return set_err(old_rc, "cgck_tx_post: this window was posted, but completing the oldest fill failed "
 				       "(its fields are not written): %s", old_msg);
@@ -1624,7 +1643,7 @@ uint32_t one_toeplitz(const uint8_t *data, uint32_t cnt, const uint8_t *key, int
 	RssParams p = {c->h_stage, 1, 0, cnt, mask, c->d_rss_tab, c->h_out};
 	hipError_t e = launch_toeplitz(p, c->num_cus, c->stream);
 	if (e == hipSuccess)
-		e = hipStreamSynchronize(c->stream);
+		e = CGCK_SYNC(c->stream);
 	if (e != hipSuccess) {
 		set_err(-EIO, "toeplitz: %s", hipGetErrorString(e));
 		die("toeplitz kernel");

@@ -91,6 +91,17 @@ struct cgck_ctx {
 #pragma GCC visibility push(hidden)
 namespace cgck {
 
+// hipStreamSynchronize; the lab build reports a synchronisation that takes
+// more than 20 ms, with where it was called (a loop stall's diagnosis).
+#if CGCK_LAB
+hipError_t lab_sync(const char *where, hipStream_t st);
+#define CGCK_STR2(x) #x
+#define CGCK_STR(x) CGCK_STR2(x)
+#define CGCK_SYNC(st) ::cgck::lab_sync(__FILE__ ":" CGCK_STR(__LINE__), st)
+#else
+#define CGCK_SYNC(st) hipStreamSynchronize(st)
+#endif
+
 // Thread-local error text (cgck_last_error); returns `code`.
 int set_err(int code, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
 const char *err_text();
