@@ -57,13 +57,22 @@ struct cgck_event {
 	hipEvent_t ev;
 };
 
+// hipFree / hipHostFree synchronise the device: with a burst server resident
+// on it (a persistent kernel) such a free waits until every server idles out
+// — 200 ms of a worker's loop (a coalesced loop whose fills outgrew the
+// staging: tools/txloop, profiles/r06/stall/), or forever while other
+// workers keep theirs busy.  So while any server is resident a buffer is not
+// freed but parked, and parked buffers are freed once the last server has
+// closed (burst_close).
+static void free_or_park(void *p, bool host);
+
 int cgck::grow_host(void **p, size_t *cap, size_t need)
 {
 	if (need <= *cap)
 		return 0;
 	size_t n = need < 4096 ? 4096 : need + need / 2;
 	if (*p)
-		(void)hipHostFree(*p);
+		free_or_park(*p, true);
 	*p = nullptr;
 	*cap = 0;
 	HIP_TRY(hipHostMalloc(p, n, hipHostMallocDefault));
@@ -77,7 +86,7 @@ int cgck::grow_dev(void **p, size_t *cap, size_t need)
 		return 0;
 	size_t n = need < 65536 ? 65536 : need + need / 4;
 	if (*p)
-		(void)hipFree(*p);
+		free_or_park(*p, false);
 	*p = nullptr;
 	*cap = 0;
 	HIP_TRY(hipMalloc(p, n));
@@ -179,20 +188,12 @@ extern "C" int cgck_ctx_destroy(cgck_ctx_t *c)
 		(void)cgck_burst_close(c);
 	(void)CGCK_SYNC(c->stream);
 	(void)hipStreamDestroy(c->stream);
-	if (c->h_stage)
-		(void)hipHostFree(c->h_stage);
-	if (c->h_out)
-		(void)hipHostFree(c->h_out);
-	if (c->d_bytes)
-		(void)hipFree(c->d_bytes);
-	if (c->d_aux)
-		(void)hipFree(c->d_aux);
-	if (c->d_zero)
-		(void)hipFree(c->d_zero);
-	if (c->d_rss_tab)
-		(void)hipFree(c->d_rss_tab);
-	if (c->d_dst)
-		(void)hipFree(c->d_dst);
+	for (void *h : {(void *)c->h_stage, (void *)c->h_out})
+		if (h)
+			free_or_park(h, true);
+	for (void *d : {(void *)c->d_bytes, (void *)c->d_aux, c->d_zero, (void *)c->d_rss_tab, (void *)c->d_dst})
+		if (d)
+			free_or_park(d, false);
 	rss_users_free(c);
 	free(c->h_rss_tab);
 	free(c->rss_key);
@@ -357,6 +358,8 @@ static std::atomic<uint32_t> g_burst_epoch{0};
 // contexts with an open server (changed under g_map_wr).
 namespace {
 std::mutex g_map_wr;
+std::mutex g_park_mu;
+std::vector<std::pair<void *, bool>> g_parked; // (buffer, host)
 std::atomic<uint32_t> g_map_changing{0};
 std::mutex g_srv_mu;
 std::vector<cgck_ctx *> g_srv;
@@ -410,6 +413,46 @@ class MapChange {
 	std::lock_guard<std::mutex> lk_;
 };
 } // namespace
+
+static void free_or_park(void *p, bool host)
+{
+	bool resident;
+	{
+		std::lock_guard<std::mutex> lk(g_srv_mu);
+		resident = !g_srv.empty();
+	}
+	if (resident) {
+		std::lock_guard<std::mutex> lk(g_park_mu);
+		g_parked.emplace_back(p, host);
+		return;
+	}
+	if (host)
+		(void)hipHostFree(p);
+	else
+		(void)hipFree(p);
+}
+
+// The parked buffers, freed once no server is resident (caller: after a
+// close took its server out of g_srv).
+static void free_parked()
+{
+	{
+		std::lock_guard<std::mutex> lk(g_srv_mu);
+		if (!g_srv.empty())
+			return;
+	}
+	std::vector<std::pair<void *, bool>> v;
+	{
+		std::lock_guard<std::mutex> lk(g_park_mu);
+		v.swap(g_parked);
+	}
+	for (const auto &x : v) {
+		if (x.second)
+			(void)hipHostFree(x.first);
+		else
+			(void)hipFree(x.first);
+	}
+}
 
 static bool burst_all_alive(const cgck_ctx *c);
 static int burst_restart(cgck_ctx *c);
@@ -1298,13 +1341,11 @@ constexpr uint32_t kMaxServersPerDevice = 12;
 static void burst_release(cgck_ctx *c)
 {
 	(void)hipStreamDestroy(c->bstream);
-	(void)hipHostFree(c->bbox);
-	(void)hipHostFree(c->bstage);
-	(void)hipHostFree(c->bresp);
-	(void)hipFree(c->bscratch);
-	(void)hipFree(c->brelay);
-	if (c->bdoor)
-		(void)hipFree(c->bdoor);
+	for (void *h : {(void *)c->bbox, (void *)c->bstage, (void *)c->bresp})
+		free_or_park(h, true);
+	for (void *d : {(void *)c->bscratch, (void *)c->brelay, (void *)c->bdoor})
+		if (d)
+			free_or_park(d, false);
 	c->bdoor = nullptr;
 	c->bvblk = nullptr;
 	c->bbox = nullptr;
@@ -1560,6 +1601,7 @@ extern "C" int cgck_burst_close(cgck_ctx_t *c)
 	burst_stop(c, 1u);
 	hipError_t e = CGCK_SYNC(c->bstream); // the server sees `stop` within one poll
 	burst_release(c);
+	free_parked();
 	if (e != hipSuccess)
 		return set_err(-EIO, "cgck_burst_close: %s", hipGetErrorString(e));
 	return 0;
@@ -1910,7 +1952,7 @@ extern "C" int cgck_dev_alloc(size_t bytes, void **ptr)
 extern "C" int cgck_dev_free(void *ptr)
 {
 	if (ptr)
-		HIP_TRY(hipFree(ptr));
+		free_or_park(ptr, false);
 	return 0;
 }
 
@@ -1926,7 +1968,7 @@ extern "C" int cgck_host_alloc(size_t bytes, void **ptr)
 extern "C" int cgck_host_free(void *ptr)
 {
 	if (ptr)
-		HIP_TRY(hipHostFree(ptr));
+		free_or_park(ptr, true);
 	return 0;
 }
 
