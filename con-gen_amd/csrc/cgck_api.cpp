@@ -396,8 +396,14 @@ class MapChange {
 	MapChange() : lk_(g_map_wr)
 	{
 		g_map_changing.store(1, std::memory_order_seq_cst);
-		std::lock_guard<std::mutex> lk(g_srv_mu);
-		for (cgck_ctx *c : g_srv)
+		// (the list copied: no lock held while waiting; it cannot change
+		// meanwhile, burst open / close take g_map_wr)
+		std::vector<cgck_ctx *> srv;
+		{
+			std::lock_guard<std::mutex> lk(g_srv_mu);
+			srv = g_srv;
+		}
+		for (cgck_ctx *c : srv)
 			for (uint32_t k = 0; __atomic_load_n(&c->bbusy, __ATOMIC_SEQ_CST); k++) {
 				if (k < 4096)
 					__builtin_ia32_pause();

@@ -324,15 +324,18 @@ int cgck_window_stats_n(uint64_t *stats, int n);
 
 /* Burst server (latency).  Keeps up to 32 workgroups
  * (one per 64 packets of max_pkts) resident on `ctx` (NULL: this thread's
- * drop-in context) that serve host-resident batches through a host-coherent
- * mailbox: cgck_desc_host, the RX window, the TX window's flush (its queue
+ * drop-in context) that serve host-resident batches through a mailbox (a
+ * doorbell in device memory the host writes through the large BAR, or
+ * host-coherent memory): cgck_desc_host, the RX window, the TX window's flush (its queue
  * read in place when it lies in one registered range, as cgck_desc_host of
  * that range) and the synchronous drop-in calls then skip the kernel launch
  * and the stream synchronisation whenever a batch fits (at most max_pkts packets and max_bytes of packet bytes; a
  * batch of more than 64 packets is split over the workgroups).  Batches
  * above the caps take the launch path, whose many workgroups read host
  * memory faster for hundreds of frames of >= 576 B: max_bytes ~96 KiB routes
- * a mixed workload best.  The server exits after idle_ms
+ * a mixed workload best.  Each server holds a hardware
+ * queue of its own, so a device takes at most 12 from a process (-EBUSY
+ * beyond: that context runs its requests through launches).  The server exits after idle_ms
  * without a request (0: 200 ms) and is relaunched by the next one; close
  * stops it.  cgck_ctx_destroy and cgck_thread_release close it too. */
 int cgck_burst_open(cgck_ctx_t *ctx, uint32_t max_pkts, size_t max_bytes, uint32_t idle_ms);
