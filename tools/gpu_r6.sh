@@ -145,6 +145,17 @@ for step in "$@"; do
 		TXLOOP_MIXES=1 TXLOOP_NS=0 TXLOOP_BURSTS=64,256 TXLOOP_REPEAT=12 timeout -k 10 280 taskset -c $C tools/txloop_lab 0.1 > $O/stall_lab.log 2> $O/stall_lab.err || exit 1
 		TXLOOP_MIXES=1 TXLOOP_NS=0 TXLOOP_BURSTS=64,256 TXLOOP_REPEAT=12 timeout -k 10 280 taskset -c $C tools/txloop 0.1 > $O/stall.log 2> $O/stall.err || exit 1
 		grep -c slow $O/stall_lab.err $O/stall.err || true ;;
+	lpwpmc) # where lpw's time goes: SQ counters per workload (one pass of 8 SQ counters each), and the
+		# lab's DMA-rounds-only variant beside the full kernel
+		cd /tmp && export TMPDIR=/tmp
+		P="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT"
+		for w in imixp ring 1500; do
+			timeout -s KILL 120 rocprofv3 --pmc $P -d $O/pmc_$w -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/tools/one_workload.py $w --launches 3 > $O/pmc_$w.log 2>&1 || exit 1
+		done
+		for w in imixp ring; do
+			CGCK_LIB=$GRAFT_REPO_ROOT/con-gen_amd/libcgck_lab.so CGCK_LPW_NOCONS=1 timeout -s KILL 120 rocprofv3 --pmc $P -d $O/pmc_${w}_dma -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/tools/one_workload.py $w --launches 3 > $O/pmc_${w}_dma.log 2>&1 || exit 1
+		done
+		cd $GRAFT_REPO_ROOT ;;
 	workers4) TXLOOP_WORKERS=1,8,12,16,32 run workers 600 tools/txloop 0.3 || exit 1 ;;
 	vramdb) run vramdb 120 tools/vramdb 0.3 || exit 1 ;;
 	shards) run shards 600 python -u -m pytest tests/test_gpu_shards.py -m gpu -x -v -s --timeout 500 --timeout-method thread || exit 1 ;;
