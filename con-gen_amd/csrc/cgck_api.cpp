@@ -812,6 +812,7 @@ int cgck::burst_ready(cgck_ctx *c, const BurstPending *p)
 // behind the stack's work, while the write-combined stores would be the
 // worker's own; only their doorbell goes to device memory.
 static const size_t kBurstVramMax = env_size(CGCK_ENV("CGCK_BURST_VRAM_MAX"), 2048); // lab A/B: the bound
+static const size_t kBurstVramPostedMax = env_size(CGCK_ENV("CGCK_BURST_VRAM_POSTED_MAX"), 0); // lab A/B: posted ones
 static int burst_slot_free(cgck_ctx *c, const BurstLayout &L, uint8_t **block, bool posted = false)
 {
 	const uint32_t seq = burst_next(c->bseq);
@@ -819,7 +820,7 @@ static int burst_slot_free(cgck_ctx *c, const BurstLayout &L, uint8_t **block, b
 		const int rc = burst_collect(c, p); // its poster reads p->rc
 		(void)rc;
 	}
-	c->bnext_vram = c->bvblk && !posted && L.bytes <= kBurstVramMax && L.bytes <= kBurstFirst;
+	c->bnext_vram = c->bvblk && L.bytes <= (posted ? kBurstVramPostedMax : kBurstVramMax) && L.bytes <= kBurstFirst;
 	*block = c->bnext_vram ? c->bvblk + (size_t)(seq & 1) * kBurstFirst : burst_block(c, seq);
 	return 0;
 }

@@ -150,12 +150,21 @@ for step in "$@"; do
 		cd /tmp && export TMPDIR=/tmp
 		P="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT"
 		for w in imixp ring 1500; do
-			timeout -s KILL 120 rocprofv3 --pmc $P -d $O/pmc_$w -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/tools/one_workload.py $w --launches 3 > $O/pmc_$w.log 2>&1 || exit 1
+			timeout -s KILL 120 rocprofv3 --pmc $P -d $GRAFT_REPO_ROOT/$O/pmc_$w -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/tools/one_workload.py $w --launches 3 > $GRAFT_REPO_ROOT/$O/pmc_$w.log 2>&1 || exit 1
 		done
 		for w in imixp ring; do
-			CGCK_LIB=$GRAFT_REPO_ROOT/con-gen_amd/libcgck_lab.so CGCK_LPW_NOCONS=1 timeout -s KILL 120 rocprofv3 --pmc $P -d $O/pmc_${w}_dma -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/tools/one_workload.py $w --launches 3 > $O/pmc_${w}_dma.log 2>&1 || exit 1
+			CGCK_LIB=$GRAFT_REPO_ROOT/con-gen_amd/libcgck_lab.so CGCK_LPW_NOCONS=1 timeout -s KILL 120 rocprofv3 --pmc $P -d $GRAFT_REPO_ROOT/$O/pmc_${w}_dma -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/tools/one_workload.py $w --launches 3 > $GRAFT_REPO_ROOT/$O/pmc_${w}_dma.log 2>&1 || exit 1
 		done
 		cd $GRAFT_REPO_ROOT ;;
+	postedab) # lab: posted requests' small blocks (up to 512 B: ~37 descriptors) in device memory too, against
+		# the product's choice (host staging), pinned and interleaved: the lone burst and the worker's cost
+		C=$(python3 -c "import os; c=sorted(os.sched_getaffinity(0)); print(c[len(c)//2])")
+		for i in 1 2 3; do
+			for m in host vram; do
+				case $m in host) E="X=1";; vram) E="CGCK_BURST_VRAM_POSTED_MAX=512";; esac
+				env $E TXLOOP_BURSTS=1,4,16,32 TXLOOP_NS=250 TXLOOP_MIXES=0,1 timeout -k 10 200 taskset -c $C tools/txloop_lab 0.15 > $O/txloop_posted_${m}$i.log 2>&1 || exit 1
+			done
+		done ;;
 	workers4) TXLOOP_WORKERS=1,8,12,16,32 run workers 600 tools/txloop 0.3 || exit 1 ;;
 	vramdb) run vramdb 120 tools/vramdb 0.3 || exit 1 ;;
 	shards) run shards 600 python -u -m pytest tests/test_gpu_shards.py -m gpu -x -v -s --timeout 500 --timeout-method thread || exit 1 ;;
