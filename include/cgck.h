@@ -428,7 +428,11 @@ int cgck_dst_cache(cgck_ctx_t *ctx, const cgck_dst_params_t *prm, cgck_dst_entry
 int cgck_dst_cache_host(cgck_ctx_t *ctx, const cgck_dst_params_t *prm, cgck_dst_entry_t *out,
 			uint32_t cap, uint32_t *count);
 
-/* Plumbing for callers without their own runtime (tests, bench, C users). */
+/* Plumbing for callers without their own runtime (tests, bench, C users).
+ * A free while any burst server is resident is deferred until the last one
+ * closes: hipFree / hipHostFree synchronise the device, which would wait for
+ * the resident servers to idle out (the library's own buffers are handled
+ * the same way). */
 int cgck_device_count(void);
 int cgck_dev_alloc(size_t bytes, void **ptr);
 int cgck_dev_free(void *ptr);
