@@ -1334,6 +1334,12 @@ hipError_t launch_slotd(const KParams &p, int num_cus, hipStream_t st)
 #undef CGCK_LPW_SLOTMAJOR
 #define CGCK_LPW_SLOTMAJOR 0
 #endif
+// 1: the window's prefix with a lane per pair of chunks (4 wave scans a
+// window), 0: a lane per chunk (8) — the A/B builds' knob
+#if !CGCK_LAB || !defined(CGCK_LPW_PAIR)
+#undef CGCK_LPW_PAIR
+#define CGCK_LPW_PAIR 1
+#endif
 // LDS index (in 16-byte units) of window chunk idx
 __device__ __forceinline__ int lpw_at(int idx)
 {
@@ -1671,6 +1677,37 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(W ? 4 : 1))
 					u32x4v *p4 = reinterpret_cast<u32x4v *>(pfx + 8 * l);
 					p4[0] = u32x4v{before + xs[0], before + xs[1], before + xs[2], before + xs[3]};
 					p4[1] = u32x4v{before + xs[4], before + xs[5], before + xs[6], before + xs[7]};
+				}
+#elif CGCK_LPW_PAIR
+				// A lane per PAIR of chunks (2 l, 2 l + 1 of each 2 KiB row
+				// pair): half the wave scans of a lane per chunk (4 a window
+				// instead of 8: the scans' DPP chain was the window's largest
+				// issue cost, lpw being issue-bound on the packed layout —
+				// SQ_ACTIVE_INST_ANY 0.49 of its wave cycles against dstr's
+				// 0.20, profiles/r06/lpwpmc/).  The two 16-byte reads of a
+				// lane go first / second by bit 3 of the lane, so lanes l and
+				// l + 8 (32 bytes apart x 8) never hit the same banks.
+				uint32_t ya[kLpwDma / 2], yb[kLpwDma / 2];
+				const int sw = (l >> 3) & 1;
+#pragma unroll
+				for (int r = 0; r < kLpwDma / 2; ++r) {
+					const int c = 128 * r + 2 * l;
+					const uint4 va = win[c + sw], vb = win[c + 1 - sw];
+					const uint32_t sa = wb + (uint64_t)(c + sw) < cur.E ? sum4(va, 0u) : 0u;
+					const uint32_t sb = wb + (uint64_t)(c + 1 - sw) < cur.E ? sum4(vb, 0u) : 0u;
+					const uint32_t s1 = sw ? sa : sb; // chunk c + 1's sum
+					const uint32_t inc = wave_scan_dpp(sa + sb);
+					yb[r] = inc;
+					ya[r] = inc - s1;
+				}
+				asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // every read of the slot's chunks is done
+				uint32_t *pfx = reinterpret_cast<uint32_t *>(smem + (kiss & 1) * kLpwSlot);
+				uint32_t carry = 0;
+#pragma unroll
+				for (int r = 0; r < kLpwDma / 2; ++r) {
+					typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
+					*reinterpret_cast<u32x2v *>(pfx + 128 * r + 2 * l) = u32x2v{ya[r] + carry, yb[r] + carry};
+					carry += __builtin_amdgcn_readlane(yb[r], 63);
 				}
 #else
 				uint32_t xs[kLpwDma];

@@ -165,6 +165,11 @@ for step in "$@"; do
 				env $E TXLOOP_BURSTS=1,4,16,32 TXLOOP_NS=250 TXLOOP_MIXES=0,1 timeout -k 10 200 taskset -c $C tools/txloop_lab 0.15 > $O/txloop_posted_${m}$i.log 2>&1 || exit 1
 			done
 		done ;;
+	lpwab) # in-process A/B of lpw (libcgck_base.so: the previous build) on the IMIX layouts, twice
+		for i in 1 2; do
+			run lpwab$i 300 python -u tools/ab_inproc.py --libs con-gen_amd/libcgck_base.so,con-gen_amd/libcgck.so --workloads imixp,ring,imix --rounds 6 || exit 1
+		done ;;
+	lpwtests) run pytest_lpw 300 python -u -m pytest tests/test_gpu_lpw.py -m gpu -x -q --timeout 200 --timeout-method thread || exit 1 ;;
 	workers4) TXLOOP_WORKERS=1,8,12,16,32 run workers 600 tools/txloop 0.3 || exit 1 ;;
 	vramdb) run vramdb 120 tools/vramdb 0.3 || exit 1 ;;
 	shards) run shards 600 python -u -m pytest tests/test_gpu_shards.py -m gpu -x -v -s --timeout 500 --timeout-method thread || exit 1 ;;
