@@ -165,7 +165,7 @@ for step in "$@"; do
 				env $E TXLOOP_BURSTS=1,4,16,32 TXLOOP_NS=250 TXLOOP_MIXES=0,1 timeout -k 10 200 taskset -c $C tools/txloop_lab 0.15 > $O/txloop_posted_${m}$i.log 2>&1 || exit 1
 			done
 		done ;;
-	lpwab) # in-process A/B of lpw (libcgck_base.so: the previous build) on the IMIX layouts, twice
+	lpwab2) # in-process A/B of lpw (libcgck_base.so: the previous build) on the IMIX layouts, twice
 		for i in 1 2; do
 			run lpwab$i 300 python -u tools/ab_inproc.py --libs con-gen_amd/libcgck_base.so,con-gen_amd/libcgck.so --workloads imixp,ring,imix --rounds 6 || exit 1
 		done ;;
