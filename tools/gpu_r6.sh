@@ -169,6 +169,10 @@ for step in "$@"; do
 		for i in 1 2; do
 			run lpwab$i 300 python -u tools/ab_inproc.py --libs con-gen_amd/libcgck_base.so,con-gen_amd/libcgck.so --workloads imixp,ring,imix --rounds 6 || exit 1
 		done ;;
+	lpwdma) # lab variants: smaller lpw windows (6 / 4 KiB) with more waves per CU, in-process against the product
+		CGCK_LPW_WPC=10 run lpwdma6 300 python -u tools/ab_inproc.py --libs con-gen_amd/libcgck.so,con-gen_amd/libcgck_v6.so --workloads imixp,ring --rounds 6 || exit 1
+		CGCK_LPW_WPC=12 run lpwdma4 300 python -u tools/ab_inproc.py --libs con-gen_amd/libcgck.so,con-gen_amd/libcgck_v4.so --workloads imixp,ring --rounds 6 || exit 1
+		CGCK_LPW_WPC=8 run lpwdma6w8 300 python -u tools/ab_inproc.py --libs con-gen_amd/libcgck.so,con-gen_amd/libcgck_v6.so --workloads imixp,ring --rounds 6 || exit 1 ;;
 	lpwtests) run pytest_lpw 300 python -u -m pytest tests/test_gpu_lpw.py -m gpu -x -q --timeout 200 --timeout-method thread || exit 1 ;;
 	workers4) TXLOOP_WORKERS=1,8,12,16,32 run workers 600 tools/txloop 0.3 || exit 1 ;;
 	vramdb) run vramdb 120 tools/vramdb 0.3 || exit 1 ;;
