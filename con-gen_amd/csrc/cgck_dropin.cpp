@@ -889,8 +889,6 @@ extern "C" uint16_t udp_cksum(struct ip *ipp, int len)
 
 namespace {
 
-constexpr uint32_t kRxFlags = CGCK_IP | CGCK_L4 | CGCK_ZERO_FIELDS | kFlagL4Auto | kFlagRx;
-
 // The unsent items of one kind that go out together: as many as share the
 // first one's range and flags and fit what is left of the server's caps
 // (without a server the request is a launch, computed at once).  Items
@@ -1313,11 +1311,10 @@ extern "C" int cgck_tx_begin(void)
 
 namespace {
 
-// Both kinds in one batch: IP entries ask for the header checksum, L4
-// entries for the segment checksum; both read their fields as zero, as the
-// reference's callers have just stored them (ip_output.c:61, tcp_subr.c:75 /
-// gbtcp/tcp.c:426,436).
-constexpr uint32_t kTxFlags = CGCK_IP | CGCK_L4 | CGCK_ZERO_FIELDS;
+// Both kinds in one batch (kTxFlags, cgck_internal.h): IP entries ask for
+// the header checksum, L4 entries for the segment checksum; both read their
+// fields as zero, as the reference's callers have just stored them
+// (ip_output.c:61, tcp_subr.c:75 / gbtcp/tcp.c:426,436).
 
 // A fill with ICMP messages also asks for their values without the
 // pseudo-header (kFlagL4Auto: by ip_p, as the RX window does); TCP and UDP

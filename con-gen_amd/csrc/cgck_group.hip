@@ -34,8 +34,9 @@ constexpr int kGrpStage = 2048;
 // host memory): the burst server's outputs and in-place fields, which it then
 // publishes after the stores' own completion instead of an L2 write-back.
 // LDSP: packet bytes in LDS (p.base and p.zero generic pointers into it).
+// FL: the flags, known at compile time (0: p.flags, read at run time).
 template <int G, int S, int U, bool DESC, bool NT, bool LDSD = false, bool SYS = false, bool SYSST = false,
-	  bool LDSP = false>
+	  bool LDSP = false, uint32_t FL = 0>
 __device__ __forceinline__ void cksum_body(const KParams &p, uint32_t bid, uint32_t nb)
 {
 	__shared__ uint32_t so[kGrpStage];
@@ -44,7 +45,7 @@ __device__ __forceinline__ void cksum_body(const KParams &p, uint32_t bid, uint3
 	const int lane = threadIdx.x;
 	const int gib = lane / G;           // group in block
 	const int gl = lane % G;            // lane in group
-	const uint32_t flags = p.flags;
+	const uint32_t flags = FL ? FL : p.flags;
 	const bool raw = flags & CGCK_RAW;
 	const bool need_hdr = !raw;
 	const bool rx = flags & kFlagRx; // uniform
@@ -310,7 +311,7 @@ __device__ __forceinline__ uint64_t sys_relaxed64(const uint64_t *p)
 
 // The group body over a request's packets [lo, hi) (block 0 of 1); desc is
 // packet lo's descriptor (in LDS when LDSD); LDSP: the packet bytes too.
-template <bool LDSD, bool SYS = false, bool LDSP = false, bool WT = true>
+template <bool LDSD, bool SYS = false, bool LDSP = false, bool WT = true, uint32_t FL = 0>
 __device__ __forceinline__ void burst_part(const BurstReq &h, uint32_t flags, const uint32_t *desc, uint32_t lo,
 					   uint32_t hi, uint32_t *out, uint32_t *meta, uint8_t *verdict,
 					   const void *zero, const uint8_t *base)
@@ -324,16 +325,16 @@ __device__ __forceinline__ void burst_part(const BurstReq &h, uint32_t flags, co
 	// writes: 2048 x 1500 B in place 79 -> 86 us, tools/e2e.py)
 	if constexpr (SYS) { // burst_sys_ok: one packet per group covers the part
 		if (h.max_len <= 80)
-			cksum_body<4, 2, 1, true, false, LDSD, true, true>(p, 0, 1);
+			cksum_body<4, 2, 1, true, false, LDSD, true, true, false, FL>(p, 0, 1);
 		else
-			cksum_body<16, 6, 1, true, false, LDSD, true, true>(p, 0, 1);
+			cksum_body<16, 6, 1, true, false, LDSD, true, true, false, FL>(p, 0, 1);
 		return;
 	}
 	if constexpr (LDSP) { // a block of <= 8 KiB: at most ~64 small packets
 		if (h.max_len <= 80)
-			cksum_body<4, 2, 1, true, false, LDSD, false, true, true>(p, 0, 1);
+			cksum_body<4, 2, 1, true, false, LDSD, false, true, true, FL>(p, 0, 1);
 		else
-			cksum_body<16, 6, 1, true, false, LDSD, false, true, true>(p, 0, 1);
+			cksum_body<16, 6, 1, true, false, LDSD, false, true, true, FL>(p, 0, 1);
 		return;
 	}
 	// A part the block covers in one pass with one packet per group runs
@@ -341,21 +342,21 @@ __device__ __forceinline__ void burst_part(const BurstReq &h, uint32_t flags, co
 	// VALU chain, which four unrolled packets per group quadruple.
 	if (h.max_len <= 80) {
 		if (hi - lo <= 64)
-			cksum_body<4, 2, 1, true, false, LDSD, false, WT>(p, 0, 1);
+			cksum_body<4, 2, 1, true, false, LDSD, false, WT, false, FL>(p, 0, 1);
 		else
-			cksum_body<4, 2, 4, true, false, LDSD, false, WT>(p, 0, 1);
+			cksum_body<4, 2, 4, true, false, LDSD, false, WT, false, FL>(p, 0, 1);
 	} else {
 		if (hi - lo <= 16)
-			cksum_body<16, 6, 1, true, false, LDSD, false, WT>(p, 0, 1);
+			cksum_body<16, 6, 1, true, false, LDSD, false, WT, false, FL>(p, 0, 1);
 		else
-			cksum_body<16, 6, 4, true, false, LDSD, false, WT>(p, 0, 1);
+			cksum_body<16, 6, 4, true, false, LDSD, false, WT, false, FL>(p, 0, 1);
 	}
 }
 
 // A request may carry two parts (a receive burst's frames, then a TX fill's
 // packets: BurstReq.n1): packets [lo, hi) on either side of n1 run with that
 // part's flags.
-template <bool LDSD, bool SYS = false, bool LDSP = false, bool WT = true>
+template <bool LDSD, bool SYS = false, bool LDSP = false, bool WT = true, uint32_t FL = 0>
 __device__ __forceinline__ void burst_body(const BurstReq &h, const uint32_t *desc, uint32_t lo, uint32_t hi,
 					   uint32_t *out, uint32_t *meta, uint8_t *verdict, const void *zero,
 					   const uint8_t *base)
@@ -366,9 +367,53 @@ __device__ __forceinline__ void burst_body(const BurstReq &h, const uint32_t *de
 		__syncthreads(); // (the body's LDS staging is reused)
 		burst_part<LDSD, SYS, LDSP, WT>(h, h.flags2, desc + 3 * (n1 - lo), n1, hi, out, meta, verdict, zero, base);
 	} else {
-		burst_part<LDSD, SYS, LDSP, WT>(h, n1 && lo >= n1 ? h.flags2 : h.flags, desc, lo, hi, out, meta, verdict,
-					    zero, base);
+		burst_part<LDSD, SYS, LDSP, WT, FL>(h, n1 && lo >= n1 ? h.flags2 : h.flags, desc, lo, hi, out, meta,
+						verdict, zero, base);
 	}
+}
+
+// burst_body for a one-workgroup request, compiled for the flag sets the
+// library posts (FL: every flag test folds, 0.9-1.1 k of a small request's
+// 2.2-4.3 k body cycles, tools/bodylat): the drop-in in_cksum / udp_cksum
+// calls, the RX and TX windows' requests, cgck_desc_host's BSD verify and
+// in-place fill; any other set, and a two-part request, take the run-time
+// flags.
+// (Lab opts bit 8192: the run-time flags for every request, the A/B.)
+template <bool LDSD, bool SYS = false, bool LDSP = false>
+__device__ __forceinline__ void burst_body_spec(const BurstReq &h, const uint32_t *desc, uint32_t n, uint32_t *out,
+						uint32_t *meta, uint8_t *verdict, const void *zero, const uint8_t *base,
+						uint32_t opts)
+{
+#if !CGCK_LAB
+	(void)opts;
+#else
+	if (!(opts & 8192))
+#endif
+	if (!(h.n1 && h.n1 < h.n)) {
+		switch (h.flags) {
+		case kRxFlags:
+			return burst_body<LDSD, SYS, LDSP, true, kRxFlags>(h, desc, 0, n, out, meta, verdict, zero, base);
+		case kTxFlags:
+			return burst_body<LDSD, SYS, LDSP, true, kTxFlags>(h, desc, 0, n, out, meta, verdict, zero, base);
+		case kTxFlags | kFlagL4Auto:
+			return burst_body<LDSD, SYS, LDSP, true, kTxFlags | kFlagL4Auto>(h, desc, 0, n, out, meta, verdict,
+											  zero, base);
+		case CGCK_VERIFY_BSD:
+			return burst_body<LDSD, SYS, LDSP, true, CGCK_VERIFY_BSD>(h, desc, 0, n, out, meta, verdict, zero,
+										  base);
+		case CGCK_FILL_BOTH:
+			return burst_body<LDSD, SYS, LDSP, true, CGCK_FILL_BOTH>(h, desc, 0, n, out, meta, verdict, zero,
+										 base);
+		}
+		if constexpr (LDSP) { // the drop-in symbols' one region, staged
+			if (h.flags == CGCK_RAW)
+				return burst_body<LDSD, SYS, LDSP, true, CGCK_RAW>(h, desc, 0, n, out, meta, verdict, zero, base);
+			if (h.flags == (CGCK_L4 | kFlagNoLenCheck))
+				return burst_body<LDSD, SYS, LDSP, true, CGCK_L4 | kFlagNoLenCheck>(h, desc, 0, n, out, meta,
+												     verdict, zero, base);
+		}
+	}
+	burst_body<LDSD, SYS, LDSP>(h, desc, 0, n, out, meta, verdict, zero, base);
 }
 
 // Can a one-workgroup request of n packets read its packet bytes in place
@@ -668,11 +713,11 @@ __global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const 
 					const uint8_t *base = h.base ? reinterpret_cast<const uint8_t *>(h.base)
 								     : reinterpret_cast<const uint8_t *>(sblock) + h.p_off;
 					if (sys)
-						burst_body<true, true>(h, sd, 0, n, o32, meta, ver, zero, base);
+						burst_body_spec<true, true>(h, sd, n, o32, meta, ver, zero, base, opts);
 					else if (h.base)
 						burst_body<true>(h, sd, 0, n, o32, meta, ver, zero, base);
 					else
-						burst_body<true, false, true>(h, sd, 0, n, o32, meta, ver, &szero, base);
+						burst_body_spec<true, false, true>(h, sd, n, o32, meta, ver, &szero, base, opts);
 				} else {
 					const uint8_t *base = h.base ? reinterpret_cast<const uint8_t *>(h.base) : scratch + h.p_off;
 					if (sys)

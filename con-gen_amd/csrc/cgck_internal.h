@@ -44,6 +44,14 @@ constexpr uint32_t kRxOkIp = 1, kRxOkL4 = 2, kRxIcmp = 4;
 // a 20-byte in_cksum read its DMA steps over the fabric: 31 vs 14 us).
 constexpr uint32_t kFlagGroup = 1u << 12;
 
+// The flag sets of the windows' requests (cgck_dropin.cpp): every frame of a
+// receive burst (its meta word, both results by ip_p, fields read as zero),
+// and a transmit fill's headers and segments (both fields read as zero;
+// kFlagL4Auto too when the fill holds ICMP messages).  The burst server's
+// one-workgroup body is compiled for each (burst_body_spec, cgck_group.hip).
+constexpr uint32_t kRxFlags = CGCK_IP | CGCK_L4 | CGCK_ZERO_FIELDS | kFlagL4Auto | kFlagRx;
+constexpr uint32_t kTxFlags = CGCK_IP | CGCK_L4 | CGCK_ZERO_FIELDS;
+
 constexpr uint32_t kImixCycleBytes = 4252; // 7*64 + 4*576 + 1500
 
 // Zeroed device bytes per context: 64 lines of 64 B, so dummy loads can be

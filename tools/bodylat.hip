@@ -7,7 +7,7 @@
 // held in LDS, and reports the shader-clock cycles of each run (s_memtime
 // around the body and the barrier after it, as the server's lab timers).
 //
-//   bodylat [npkts] [len] [raw|verify|fill] [reps]
+//   bodylat [npkts] [len] [raw|verify|fill] [reps] [spec]
 //
 // One JSON line: median / p10 / p90 cycles, and the outputs of packet 0 for
 // a sanity check against the host's own sum.
@@ -36,6 +36,7 @@ const char *intern(const char *fmt, ...) { return fmt; }
 		}                                                                         \
 	} while (0)
 
+template <uint32_t FL>
 __global__ __launch_bounds__(256) void bodylat_kernel(const uint8_t *blk, uint32_t *out, uint32_t *meta, uint8_t *ver,
 						       uint64_t *ticks, int reps)
 {
@@ -59,7 +60,7 @@ __global__ __launch_bounds__(256) void bodylat_kernel(const uint8_t *blk, uint32
 	for (int r = 0; r < reps; ++r) {
 		__syncthreads();
 		const uint64_t c0 = __builtin_amdgcn_s_memtime();
-		burst_body<true, false, true>(h, sd, 0, n, out, meta, ver, &szero, base);
+		burst_body<true, false, true, true, FL>(h, sd, 0, n, out, meta, ver, &szero, base);
 		__syncthreads();
 		const uint64_t c1 = __builtin_amdgcn_s_memtime();
 		if (t == 0)
@@ -116,7 +117,18 @@ int main(int argc, char **argv)
 	CHECK(hipHostMalloc((void **)&meta, 4 * 64 + 64, hipHostMallocCoherent));
 	CHECK(hipHostMalloc((void **)&ver, 64 + 64, hipHostMallocCoherent));
 	CHECK(hipMalloc((void **)&ticks, sizeof(uint64_t) * reps));
-	hipLaunchKernelGGL(bodylat_kernel, dim3(1), dim3(256), 0, 0, blk, out, meta, ver, ticks, reps);
+	// argv[5] "spec": the body compiled for these flags (FL), else read at run time
+	const bool spec = argc > 5 && !strcmp(argv[5], "spec");
+	if (!spec)
+		hipLaunchKernelGGL(bodylat_kernel<0>, dim3(1), dim3(256), 0, 0, blk, out, meta, ver, ticks, reps);
+	else if (flags == CGCK_RAW)
+		hipLaunchKernelGGL(bodylat_kernel<CGCK_RAW>, dim3(1), dim3(256), 0, 0, blk, out, meta, ver, ticks, reps);
+	else if (flags == (CGCK_IP | CGCK_L4 | CGCK_ZERO_FIELDS))
+		hipLaunchKernelGGL(bodylat_kernel<CGCK_IP | CGCK_L4 | CGCK_ZERO_FIELDS>, dim3(1), dim3(256), 0, 0, blk, out,
+				   meta, ver, ticks, reps);
+	else
+		hipLaunchKernelGGL(bodylat_kernel<CGCK_VERIFY_BSD>, dim3(1), dim3(256), 0, 0, blk, out, meta, ver, ticks,
+				   reps);
 	CHECK(hipGetLastError());
 	CHECK(hipDeviceSynchronize());
 	std::vector<uint64_t> tk(reps);
@@ -131,9 +143,9 @@ int main(int argc, char **argv)
 		s += ip[len - 1];
 	while (s >> 16)
 		s = (s & 0xffff) + (s >> 16);
-	printf("{\"npkts\": %u, \"len\": %u, \"mode\": \"%s\", \"reps\": %d, \"cycles_median\": %llu, \"cycles_p10\": %llu, "
+	printf("{\"npkts\": %u, \"len\": %u, \"mode\": \"%s\", \"spec\": %d, \"reps\": %d, \"cycles_median\": %llu, \"cycles_p10\": %llu, "
 	       "\"cycles_p90\": %llu, \"out0\": \"0x%08x\", \"ver0\": %u, \"host_raw0\": \"0x%04x\"}\n",
-	       n, len, mode, reps, (unsigned long long)tk[reps / 2], (unsigned long long)tk[reps / 10],
+	       n, len, mode, (int)spec, reps, (unsigned long long)tk[reps / 2], (unsigned long long)tk[reps / 10],
 	       (unsigned long long)tk[reps * 9 / 10], out[0], ver[0], (~s) & 0xffff);
 	return 0;
 }

@@ -173,11 +173,22 @@ for step in "$@"; do
 		CGCK_LPW_WPC=10 run lpwdma6 300 python -u tools/ab_inproc.py --libs con-gen_amd/libcgck.so,con-gen_amd/libcgck_v6.so --workloads imixp,ring --rounds 6 || exit 1
 		CGCK_LPW_WPC=12 run lpwdma4 300 python -u tools/ab_inproc.py --libs con-gen_amd/libcgck.so,con-gen_amd/libcgck_v4.so --workloads imixp,ring --rounds 6 || exit 1
 		CGCK_LPW_WPC=8 run lpwdma6w8 300 python -u tools/ab_inproc.py --libs con-gen_amd/libcgck.so,con-gen_amd/libcgck_v6.so --workloads imixp,ring --rounds 6 || exit 1 ;;
+	spec) # the one-workgroup body compiled per flag set: srvlat (verify staged / fill in place), pinned
+		# against the run-time flags (lab opts 8192), interleaved on the same CPU
+		for i in 1 2 3; do for m in spec rt; do
+			E=CGCK_SERVER_OPTS=0; [ $m = rt ] && E=CGCK_SERVER_OPTS=8192
+			for k in verify fill raw; do
+				env $E timeout -k 10 120 taskset -c 2 tools/srvlat 64 $k > $O/srvlat_64_${k}_$m$i.log 2>&1 || exit 1
+				echo "$k $m $i $(head -1 $O/srvlat_64_${k}_$m$i.log)"
+			done
+		done; done ;;
 	bodylat) # the server body's cycles for one small request, by mode and burst (tools/bodylat.hip)
-		for m in raw verify fill; do for n in 1 16 64; do
-			timeout -k 10 60 tools/bodylat $n 64 $m 2000 >> $O/bodylat.log 2>&1 || exit 1
-		done; done
-		timeout -k 10 60 tools/bodylat 1 1500 verify 2000 >> $O/bodylat.log 2>&1 || exit 1
+		for sp in rt spec; do
+			for m in raw verify fill; do for n in 1 64; do
+				timeout -k 10 60 tools/bodylat $n 64 $m 2000 $sp >> $O/bodylat.log 2>&1 || exit 1
+			done; done
+			timeout -k 10 60 tools/bodylat 1 1500 verify 2000 $sp >> $O/bodylat.log 2>&1 || exit 1
+		done
 		cat $O/bodylat.log ;;
 	lpwtests) run pytest_lpw 300 python -u -m pytest tests/test_gpu_lpw.py -m gpu -x -q --timeout 200 --timeout-method thread || exit 1 ;;
 	workers4) TXLOOP_WORKERS=1,8,12,16,32 run workers 600 tools/txloop 0.3 || exit 1 ;;
