@@ -140,6 +140,15 @@ for step in "$@"; do
 				echo "$m $i"; head -1 $O/srvlat_64_${m}$i.log
 			done
 		done ;;
+	specloop) # pinned, interleaved: the windows with the body compiled per flag set against the run-time flags (lab opts 8192)
+		C=$(python3 -c "import os; c=sorted(os.sched_getaffinity(0)); print(c[len(c)//2])")
+		for i in 1 2 3; do
+			for m in spec rt; do
+				case $m in rt) E="CGCK_SERVER_OPTS=8192";; spec) E="CGCK_SERVER_OPTS=0";; esac
+				env $E TXLOOP_BURSTS=1,16,64,256 TXLOOP_NS=250 TXLOOP_MIXES=0,1 timeout -k 10 200 taskset -c $C tools/txloop_lab 0.15 > $O/txloop_${m}$i.log 2>&1 || exit 1
+				echo "$m $i"
+			done
+		done ;;
 	stall) # repro of the 200 ms loop stall (rx+reply, 0 ns, 256 frames, coalesced after sync), lab then product
 		C=$(python3 -c "import os; c=sorted(os.sched_getaffinity(0)); print(c[len(c)//2])")
 		TXLOOP_MIXES=1 TXLOOP_NS=0 TXLOOP_BURSTS=64,256 TXLOOP_REPEAT=12 timeout -k 10 280 taskset -c $C tools/txloop_lab 0.1 > $O/stall_lab.log 2> $O/stall_lab.err || exit 1
