@@ -1,6 +1,6 @@
 #!/bin/sh
 # Copy one round's GPU evidence from gpurun_out/ (merged back by gpurun after
-# tools/gpu_round.sh) into profiles/$ROUND/ (tracked).  Host side only.
+# tools/gpu_r6.sh) into profiles/$ROUND/ (tracked).  Host side only.
 set -eu
 R=${1:-r01}
 G=gpurun_out
