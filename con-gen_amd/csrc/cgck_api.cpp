@@ -1582,6 +1582,13 @@ extern "C" int cgck_lab_burst_times(cgck_ctx_t *c, uint64_t dev[5], uint64_t hos
 	host[1] = t_lab_host[1];
 	return 0;
 }
+
+// Lab: thread 0's shader clocks over the last one-workgroup request's body
+// call alone (tools/srvlat's body_cycles, against tools/bodylat's).
+extern "C" uint64_t cgck_lab_burst_body(cgck_ctx_t *c)
+{
+	return c && c->bbox ? __atomic_load_n(&c->bbox->lab_body, __ATOMIC_ACQUIRE) : 0;
+}
 #endif
 
 extern "C" int cgck_burst_close(cgck_ctx_t *c)

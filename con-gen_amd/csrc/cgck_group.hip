@@ -702,7 +702,15 @@ __global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const 
 			lab_t1 = __builtin_amdgcn_s_memrealtime();
 			lab_c1 = __builtin_amdgcn_s_memtime();
 #endif
+			// (lab opts bit 16384: the body runs twice, lab_body timing the
+			// second — warm against cold, tools/srvlat)
+#if CGCK_LAB
+			for (int lab_rep = 0; ok && lab_rep < ((opts & 16384) ? 2 : 1); ++lab_rep)
+#endif
 			if (ok) {
+#if CGCK_LAB
+				const uint64_t lab_b0 = __builtin_amdgcn_s_memtime();
+#endif
 				// staged packet bytes are read from the LDS or scratch copy;
 				// packet bytes in place by the system-coherent body, or with
 				// plain loads after the acquire (lab opts bit 256: always so)
@@ -725,6 +733,11 @@ __global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const 
 					else
 						burst_body<false>(h, sd, 0, n, o32, meta, ver, zero, base);
 				}
+#if CGCK_LAB
+				if (t == 0 && j == 0)
+					__hip_atomic_store(&box->lab_body, __builtin_amdgcn_s_memtime() - lab_b0, __ATOMIC_RELAXED,
+							   __HIP_MEMORY_SCOPE_SYSTEM);
+#endif
 			}
 		} else {
 			// Slice [lo, hi) in passes of up to kSliceLds descriptors: the

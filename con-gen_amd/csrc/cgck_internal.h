@@ -98,7 +98,8 @@ struct BurstBox {
 	uint64_t idle_ticks; // 100 MHz ticks without a request before the server exits
 	uint32_t refused[2]; // device -> host: seq of the last refused request in each slot
 	uint64_t lab_cyc;    // lab build: workgroup 0's shader clocks (s_memtime) over the compute phase
-	uint32_t pad[4];
+	uint64_t lab_body;   // lab build: thread 0's shader clocks over the one-workgroup body call alone
+	uint32_t pad[2];
 	uint32_t done[kBurstMaxWG]; // device -> host: the last request workgroup j served
 	uint8_t alive[kBurstMaxWG]; // host sets 1 at launch; workgroup j clears its byte on exit
 	uint64_t lab_t[4];   // lab build: workgroup 0's s_memrealtime at seen / read / computed / published

@@ -140,6 +140,17 @@ for step in "$@"; do
 				echo "$m $i"; head -1 $O/srvlat_64_${m}$i.log
 			done
 		done ;;
+	bodysplit) # the one-workgroup body inside the server (srvlat body_cycles) against the same body alone (bodylat)
+		for k in verify fill raw; do
+			timeout -k 10 120 taskset -c 2 tools/srvlat 64 $k > $O/srvlat_64_$k.log 2>&1 || exit 1
+			echo "$k $(head -1 $O/srvlat_64_$k.log)"
+		done
+		for k in verify raw; do
+			CGCK_SERVER_OPTS=16384 timeout -k 10 120 taskset -c 2 tools/srvlat 64 $k > $O/srvlat_64_${k}_twice.log 2>&1 || exit 1
+			echo "$k twice $(head -1 $O/srvlat_64_${k}_twice.log)"
+		done
+		for m in raw verify fill; do timeout -k 10 60 tools/bodylat 1 64 $m 2000 spec >> $O/bodylat.log 2>&1 || exit 1; done
+		cat $O/bodylat.log ;;
 	specloop) # pinned, interleaved: the windows with the body compiled per flag set against the run-time flags (lab opts 8192)
 		C=$(python3 -c "import os; c=sorted(os.sched_getaffinity(0)); print(c[len(c)//2])")
 		for i in 1 2 3; do

@@ -15,6 +15,7 @@
 #include "cgck.h"
 
 int cgck_lab_burst_times(cgck_ctx_t *c, uint64_t dev[5], uint64_t host[2]);
+uint64_t cgck_lab_burst_body(cgck_ctx_t *c);
 
 #define SLOT 2048
 #define L3 14
@@ -49,8 +50,8 @@ int main(int argc, char **argv)
 	cgck_desc_t *desc = malloc(sizeof(cgck_desc_t) * maxb);
 	uint32_t *out = malloc(4 * maxb);
 	uint8_t *ver = malloc(maxb);
-	double *tt = malloc(sizeof(double) * it), *ph[6];
-	for (int k = 0; k < 6; k++)
+	double *tt = malloc(sizeof(double) * it), *ph[7];
+	for (int k = 0; k < 7; k++)
 		ph[k] = malloc(sizeof(double) * it);
 	cgck_ctx_t *ctx;
 	if (!ring || cgck_ctx_create(0, &ctx))
@@ -100,11 +101,13 @@ int main(int argc, char **argv)
 			ph[3][i] = (h[1] - h[0]) / 1000.0; /* host post -> done seen */
 			ph[4][i] = tt[i] - ph[3][i];       /* host work outside the wait */
 			ph[5][i] = d[2] > d[1] ? d[4] / ((d[2] - d[1]) * 10.0) : 0; /* shader clock in GHz */
+			ph[6][i] = (double)cgck_lab_burst_body(ctx); /* one-workgroup body call alone, shader clocks */
 		}
 		printf("{\"pkt_len\": %d, \"burst\": %d, \"us_call\": %.2f, \"us_wait\": %.2f, \"us_host_rest\": %.2f, "
-		       "\"us_read\": %.2f, \"us_compute\": %.2f, \"us_release\": %.2f, \"ghz_compute\": %.2f}\n",
+		       "\"us_read\": %.2f, \"us_compute\": %.2f, \"us_release\": %.2f, \"ghz_compute\": %.2f, "
+		       "\"body_cycles\": %.0f}\n",
 		       len, R, med(tt, it), med(ph[3], it), med(ph[4], it), med(ph[0], it), med(ph[1], it),
-		       med(ph[2], it), med(ph[5], it));
+		       med(ph[2], it), med(ph[5], it), med(ph[6], it));
 		fflush(stdout);
 	}
 	cgck_burst_close(ctx);
