@@ -36,9 +36,16 @@ const char *intern(const char *fmt, ...) { return fmt; }
 		}                                                                         \
 	} while (0)
 
-template <uint32_t FL>
+// LIVE: uniform values kept live across the body (the server kernel's state
+// around its body: its arguments, loop and request words), the A/B of
+// "bodylat ... live"
+struct LiveArgs {
+	uint64_t v[20];
+};
+
+template <uint32_t FL, bool LIVE = false>
 __global__ __launch_bounds__(256) void bodylat_kernel(const uint8_t *blk, uint32_t *out, uint32_t *meta, uint8_t *ver,
-						       uint64_t *ticks, int reps)
+						       uint64_t *ticks, int reps, LiveArgs la = {})
 {
 	__shared__ uint4 hdr_w[4];
 	__shared__ uint4 sblock[kBurstFirst / 16];
@@ -60,11 +67,25 @@ __global__ __launch_bounds__(256) void bodylat_kernel(const uint8_t *blk, uint32
 	for (int r = 0; r < reps; ++r) {
 		__syncthreads();
 		const uint64_t c0 = __builtin_amdgcn_s_memtime();
+		uint64_t lv[20];
+		if constexpr (LIVE) {
+#pragma unroll
+			for (int i = 0; i < 20; ++i)
+				lv[i] = la.v[i] * (uint64_t)(r + 1); // uniform, defined before the body
+		}
 		burst_body<true, false, true, true, FL>(h, sd, 0, n, out, meta, ver, &szero, base);
 		__syncthreads();
 		const uint64_t c1 = __builtin_amdgcn_s_memtime();
 		if (t == 0)
 			ticks[r] = c1 - c0;
+		if constexpr (LIVE) { // ... and used after it
+			uint64_t x = 0;
+#pragma unroll
+			for (int i = 0; i < 20; ++i)
+				x ^= lv[i] >> (i & 7);
+			if (t == 0 && x == 0x123456789ull)
+				ticks[reps] = x;
+		}
 		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 	}
 }
@@ -116,10 +137,21 @@ int main(int argc, char **argv)
 	CHECK(hipHostMalloc((void **)&out, 4 * 64 + 64, hipHostMallocCoherent));
 	CHECK(hipHostMalloc((void **)&meta, 4 * 64 + 64, hipHostMallocCoherent));
 	CHECK(hipHostMalloc((void **)&ver, 64 + 64, hipHostMallocCoherent));
-	CHECK(hipMalloc((void **)&ticks, sizeof(uint64_t) * reps));
-	// argv[5] "spec": the body compiled for these flags (FL), else read at run time
+	CHECK(hipMalloc((void **)&ticks, sizeof(uint64_t) * (reps + 1)));
+	// argv[5] "spec": the body compiled for these flags (FL), else read at run time;
+	// "live": the BSD verify body with 20 uniform 64-bit values live across it
 	const bool spec = argc > 5 && !strcmp(argv[5], "spec");
-	if (!spec)
+	const bool live = argc > 5 && !strcmp(argv[5], "live");
+	LiveArgs la;
+	for (int i = 0; i < 20; i++)
+		la.v[i] = 0x9E3779B97F4A7C15ull * (uint64_t)(i + 1);
+	if (live && flags == CGCK_RAW)
+		hipLaunchKernelGGL((bodylat_kernel<CGCK_RAW, true>), dim3(1), dim3(256), 0, 0, blk, out, meta, ver, ticks,
+				   reps, la);
+	else if (live)
+		hipLaunchKernelGGL((bodylat_kernel<CGCK_VERIFY_BSD, true>), dim3(1), dim3(256), 0, 0, blk, out, meta, ver,
+				   ticks, reps, la);
+	else if (!spec)
 		hipLaunchKernelGGL(bodylat_kernel<0>, dim3(1), dim3(256), 0, 0, blk, out, meta, ver, ticks, reps);
 	else if (flags == CGCK_RAW)
 		hipLaunchKernelGGL(bodylat_kernel<CGCK_RAW>, dim3(1), dim3(256), 0, 0, blk, out, meta, ver, ticks, reps);
@@ -143,9 +175,9 @@ int main(int argc, char **argv)
 		s += ip[len - 1];
 	while (s >> 16)
 		s = (s & 0xffff) + (s >> 16);
-	printf("{\"npkts\": %u, \"len\": %u, \"mode\": \"%s\", \"spec\": %d, \"reps\": %d, \"cycles_median\": %llu, \"cycles_p10\": %llu, "
+	printf("{\"npkts\": %u, \"len\": %u, \"mode\": \"%s\", \"spec\": %d, \"live\": %d, \"reps\": %d, \"cycles_median\": %llu, \"cycles_p10\": %llu, "
 	       "\"cycles_p90\": %llu, \"out0\": \"0x%08x\", \"ver0\": %u, \"host_raw0\": \"0x%04x\"}\n",
-	       n, len, mode, (int)spec, reps, (unsigned long long)tk[reps / 2], (unsigned long long)tk[reps / 10],
+	       n, len, mode, (int)spec, (int)live, reps, (unsigned long long)tk[reps / 2], (unsigned long long)tk[reps / 10],
 	       (unsigned long long)tk[reps * 9 / 10], out[0], ver[0], (~s) & 0xffff);
 	return 0;
 }

@@ -140,6 +140,11 @@ for step in "$@"; do
 				echo "$m $i"; head -1 $O/srvlat_64_${m}$i.log
 			done
 		done ;;
+	bodylive) # the body alone with 20 uniform 64-bit values live across it, against without
+		for m in raw verify; do for sp in spec live spec live; do
+			timeout -k 10 60 tools/bodylat 1 64 $m 2000 $sp >> $O/bodylive.log 2>&1 || exit 1
+		done; done
+		cat $O/bodylive.log ;;
 	bodysplit) # the one-workgroup body inside the server (srvlat body_cycles) against the same body alone (bodylat)
 		for k in verify fill raw; do
 			timeout -k 10 120 taskset -c 2 tools/srvlat 64 $k > $O/srvlat_64_$k.log 2>&1 || exit 1
