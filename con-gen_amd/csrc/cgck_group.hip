@@ -372,6 +372,14 @@ __device__ __forceinline__ void burst_body(const BurstReq &h, const uint32_t *de
 	}
 }
 
+// Lab A/B build (-DCGCK_SERVER_SMALL_ONLY=1): a server kernel with only the
+// staged one-workgroup path (every other request refused) — how much of the
+// small path's cost is the size of the function around it.
+#if !CGCK_LAB || !defined(CGCK_SERVER_SMALL_ONLY)
+#undef CGCK_SERVER_SMALL_ONLY
+#define CGCK_SERVER_SMALL_ONLY 0
+#endif
+
 // burst_body for a one-workgroup request, compiled for the flag sets the
 // library posts (FL: every flag test folds, 0.9-1.1 k of a small request's
 // 2.2-4.3 k body cycles, tools/bodylat): the drop-in in_cksum / udp_cksum
@@ -492,6 +500,7 @@ __global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const 
 	__shared__ uint32_t cmd, cmd_n, cmd_seq, cmd_vram;
 	__shared__ uint4 hdr_w[4];
 	__shared__ uint32_t sdesc[3 * kSliceLds];
+	(void)sdesc;
 	__shared__ uint4 sblock[kBurstFirst / 16]; // a small request's block (the one-workgroup path)
 	__shared__ uint4 szero;                    // the zero chunk of the LDS-resident body
 	if (threadIdx.x == 0)
@@ -720,18 +729,22 @@ __global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const 
 				if (in_lds) {
 					const uint8_t *base = h.base ? reinterpret_cast<const uint8_t *>(h.base)
 								     : reinterpret_cast<const uint8_t *>(sblock) + h.p_off;
+#if !CGCK_SERVER_SMALL_ONLY
 					if (sys)
 						burst_body_spec<true, true>(h, sd, n, o32, meta, ver, zero, base, opts);
 					else if (h.base)
 						burst_body<true>(h, sd, 0, n, o32, meta, ver, zero, base);
 					else
+#endif
 						burst_body_spec<true, false, true>(h, sd, n, o32, meta, ver, &szero, base, opts);
 				} else {
+#if !CGCK_SERVER_SMALL_ONLY
 					const uint8_t *base = h.base ? reinterpret_cast<const uint8_t *>(h.base) : scratch + h.p_off;
 					if (sys)
 						burst_body<false, true>(h, sd, 0, n, o32, meta, ver, zero, base);
 					else
 						burst_body<false>(h, sd, 0, n, o32, meta, ver, zero, base);
+#endif
 				}
 #if CGCK_LAB
 				if (t == 0 && j == 0)
@@ -745,6 +758,9 @@ __global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const 
 			// trip, as dwords (a slice starts on a 4-byte boundary), into
 			// LDS; the count comes from the poll, so the slice does not
 			// wait for the header.
+#if CGCK_SERVER_SMALL_ONLY
+			ok = false;
+#else
 			const uint32_t lo = (uint32_t)((uint64_t)n * j / W), hi = (uint32_t)((uint64_t)n * (j + 1) / W);
 			const uint32_t *sd = reinterpret_cast<const uint32_t *>(req + sizeof(BurstReq));
 			// (a device-memory block holds at most kBurstFirst bytes: no
@@ -786,6 +802,7 @@ __global__ __launch_bounds__(256) void burst_server_kernel(BurstBox *box, const 
 				burst_body<true, false, false, false>(h, sdesc, c0, c1, o32, meta, ver, zero, base);
 				__syncthreads(); // the next pass rewrites sdesc
 			}
+#endif
 		}
 		if (!ok && t == 0) {
 			__hip_atomic_store(&box->refused[seq & 1], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

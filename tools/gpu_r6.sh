@@ -140,6 +140,13 @@ for step in "$@"; do
 				echo "$m $i"; head -1 $O/srvlat_64_${m}$i.log
 			done
 		done ;;
+	smallonly) # the staged small path in a server kernel without the other paths (lab -DCGCK_SERVER_SMALL_ONLY=1,
+		# con-gen_amd/small/libcgck_lab.so) against the full lab server; bursts past 64 are refused there (srvlat stops)
+		for i in 1 2; do for m in full small; do for k in verify raw; do
+			D=con-gen_amd; [ $m = small ] && D=con-gen_amd/small
+			LD_LIBRARY_PATH=$D timeout -k 10 120 taskset -c 2 tools/srvlat 64 $k > $O/srvlat_64_${k}_$m$i.log 2>&1 || true
+			echo "$k $m $i $(head -1 $O/srvlat_64_${k}_$m$i.log)"
+		done; done; done ;;
 	bodylive) # the body alone with 20 uniform 64-bit values live across it, against without
 		for m in raw verify; do for sp in spec live spec live; do
 			timeout -k 10 60 tools/bodylat 1 64 $m 2000 $sp >> $O/bodylive.log 2>&1 || exit 1
